@@ -1,0 +1,252 @@
+"""Positional mirror of the reference's pybind module `diff_gaussian_rasterization._C`.
+
+Reference: DGR/ext.cpp:15-19 and DGR/rasterize_points.cu:35-246 (DGR =
+submodules_fsgs/diff-gaussian-rasterization-confidence).  The three functions
+keep the reference's exact positional signatures and return tuples, so the
+reference's own autograd wrapper could call them unchanged; they allocate
+outputs with torch (caching allocator) and hand raw device pointers to the
+HIP C ABI (libgsplat_hip.so).  There is no CPU fallback: non-device inputs or
+a missing library raise.
+
+Superset behaviour (documented in DESIGN.md "Boundary"):
+  * semantic_feature may be None/empty (F = 0), [P, F] or [P, 1, F]; any F is
+    accepted and zero-padded to the next compiled width (0, 8, 16, 32, 64).
+  * keyword-only `compat` selects "reference" (as-shipped numerics, default)
+    or "fixed" numerics; see DESIGN.md "Quirks".
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import GsCamera, GsGaussians, check
+
+_default_compat = "reference"
+
+
+def set_default_compat(mode: str) -> None:
+    """Process-wide default numerics mode ("reference" or "fixed")."""
+    global _default_compat
+    if mode not in _lib.GS_COMPAT:
+        raise ValueError(f"compat must be one of {list(_lib.GS_COMPAT)}, got {mode!r}")
+    _default_compat = mode
+
+
+def get_default_compat() -> str:
+    return _default_compat
+
+
+def _present(t) -> bool:
+    return t is not None and isinstance(t, torch.Tensor) and t.numel() > 0
+
+
+def _dev(t: torch.Tensor, device, name: str) -> torch.Tensor:
+    if t.device != device:
+        raise _lib.GsplatError(f"{name} is on {t.device}, expected {device} (HIP device tensors only)")
+    if t.dtype != torch.float32:
+        t = t.float()
+    return t.contiguous()
+
+
+def _ptr(t) -> int | None:
+    return t.data_ptr() if t is not None else None
+
+
+def _feature_width(F: int) -> int:
+    for k in _lib.SUPPORTED_F:
+        if k >= F:
+            return k
+    raise _lib.GsplatError(f"semantic feature width {F} exceeds the largest compiled width "
+                           f"{_lib.SUPPORTED_F[-1]}")
+
+
+def _stream(device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _compat_code(compat) -> int:
+    mode = _default_compat if compat is None else compat
+    if mode not in _lib.GS_COMPAT:
+        raise ValueError(f"compat must be one of {list(_lib.GS_COMPAT)}, got {mode!r}")
+    return _lib.GS_COMPAT[mode]
+
+
+class _Inputs:
+    """Device-resident, contiguous views of the per-Gaussian inputs."""
+
+    def __init__(self, means3D, colors, semantic_feature, opacity, scales, rotations,
+                 scale_modifier, cov3D_precomp, sh, degree):
+        if means3D.ndimension() != 2 or means3D.size(1) != 3:
+            raise RuntimeError("means3D must have dimensions (num_points, 3)")  # rasterize_points.cu:60-62
+        dev = means3D.device
+        if dev.type != "cuda":
+            raise _lib.GsplatError("the HIP rasterizer needs device tensors (means3D is on the CPU)")
+        self.device = dev
+        self.P = P = means3D.size(0)
+        self.means3D = _dev(means3D, dev, "means3D")
+        self.colors = _dev(colors, dev, "colors_precomp") if _present(colors) else None
+        self.opacity = _dev(opacity, dev, "opacities") if _present(opacity) else None
+        self.scales = _dev(scales, dev, "scales") if _present(scales) else None
+        self.rotations = _dev(rotations, dev, "rotations") if _present(rotations) else None
+        self.cov3D = _dev(cov3D_precomp, dev, "cov3D_precomp") if _present(cov3D_precomp) else None
+        self.sh = _dev(sh, dev, "sh") if _present(sh) else None
+        self.M = self.sh.size(1) if self.sh is not None else 0
+        self.D = int(degree)
+        self.scale_modifier = float(scale_modifier)
+        if _present(semantic_feature):
+            sem = _dev(semantic_feature, dev, "semantic_feature").reshape(P, -1)
+            self.F_user = sem.size(1)
+            self.F = _feature_width(self.F_user)
+            if self.F != self.F_user:
+                sem = torch.nn.functional.pad(sem, (0, self.F - self.F_user))
+            self.sem = sem.contiguous()
+        else:
+            self.F_user, self.F, self.sem = 0, 0, None
+
+    def struct(self) -> GsGaussians:
+        return GsGaussians(P=self.P, D=self.D, M=self.M, F=self.F,
+                           means3D=_ptr(self.means3D), shs=_ptr(self.sh),
+                           colors_precomp=_ptr(self.colors), semantic_feature=_ptr(self.sem),
+                           opacities=_ptr(self.opacity), scales=_ptr(self.scales),
+                           rotations=_ptr(self.rotations), cov3D_precomp=_ptr(self.cov3D),
+                           scale_modifier=self.scale_modifier, _pad=0)
+
+
+def _camera(dev, background, viewmatrix, projmatrix, campos, c_x, c_y, tan_fovx, tan_fovy, W, H):
+    keep = [_dev(background, dev, "bg").reshape(-1), _dev(viewmatrix, dev, "viewmatrix").reshape(-1),
+            _dev(projmatrix, dev, "projmatrix").reshape(-1), _dev(campos, dev, "campos").reshape(-1)]
+    cam = GsCamera(viewmatrix=_ptr(keep[1]), projmatrix=_ptr(keep[2]), campos=_ptr(keep[3]),
+                   background=_ptr(keep[0]), c_x=float(c_x), c_y=float(c_y),
+                   tan_fovx=float(tan_fovx), tan_fovy=float(tan_fovy),
+                   image_width=int(W), image_height=int(H))
+    return cam, keep
+
+
+def rasterize_gaussians(background, means3D, colors, semantic_feature, opacity, scales, rotations,
+                        scale_modifier, cov3D_precomp, viewmatrix, projmatrix, c_x, c_y, tan_fovx,
+                        tan_fovy, image_height, image_width, sh, degree, campos, prefiltered, debug,
+                        *, compat=None):
+    """RasterizeGaussiansCUDA (DGR/rasterize_points.cu:35-126).
+
+    Returns (num_rendered, color[3,H,W], feature_map[F,H,W], depth[1,H,W],
+    alpha[1,H,W], radii[P] int32, geomBuffer, binningBuffer, imgBuffer).
+    """
+    L_ = _lib.load()
+    cm = _compat_code(compat)
+    inp = _Inputs(means3D, colors, semantic_feature, opacity, scales, rotations, scale_modifier,
+                  cov3D_precomp, sh, degree)
+    dev, P = inp.device, inp.P
+    H, W = int(image_height), int(image_width)
+    f32 = dict(dtype=torch.float32, device=dev)
+    u8 = dict(dtype=torch.uint8, device=dev)
+    if P == 0:
+        return (0, torch.zeros(3, H, W, **f32), torch.zeros(inp.F_user, H, W, **f32),
+                torch.zeros(1, H, W, **f32), torch.zeros(1, H, W, **f32),
+                torch.zeros(0, dtype=torch.int32, device=dev), torch.empty(0, **u8),
+                torch.empty(0, **u8), torch.empty(0, **u8))
+    cam, keep = _camera(dev, background, viewmatrix, projmatrix, campos, c_x, c_y, tan_fovx,
+                        tan_fovy, W, H)
+    g = inp.struct()
+    out_color = torch.empty(3, H, W, **f32)
+    out_feature = torch.empty(inp.F, H, W, **f32)
+    out_depth = torch.empty(1, H, W, **f32)
+    # Q1: the reference never writes out_alpha (it stays 0); "fixed" writes 1 - T.
+    out_alpha = torch.zeros(1, H, W, **f32) if cm == 0 else torch.empty(1, H, W, **f32)
+    radii = torch.empty(P, dtype=torch.int32, device=dev)
+    geom = torch.empty(L_.gs_geom_buffer_bytes(P), **u8)
+    img = torch.empty(L_.gs_image_buffer_bytes(W, H), **u8)
+    stream = _stream(dev)
+    L = ctypes.c_int64(0)
+    check(L_.gs_forward_plan(ctypes.byref(g), ctypes.byref(cam), int(bool(prefiltered)),
+                             int(bool(debug)), cm, geom.data_ptr(), radii.data_ptr(), ctypes.byref(L),
+                             stream), "rasterize_gaussians (preprocess)")
+    num_rendered = int(L.value)
+    binning = torch.empty(L_.gs_binning_buffer_bytes(num_rendered), **u8)
+    check(L_.gs_forward_render(ctypes.byref(g), ctypes.byref(cam), int(bool(debug)), cm,
+                               geom.data_ptr(), binning.data_ptr(), img.data_ptr(), num_rendered,
+                               radii.data_ptr(), out_color.data_ptr(),
+                               out_feature.data_ptr() if inp.F else None, out_depth.data_ptr(),
+                               out_alpha.data_ptr(), stream), "rasterize_gaussians (render)")
+    del keep
+    feature_map = out_feature[:inp.F_user] if inp.F_user != inp.F else out_feature
+    return (num_rendered, out_color, feature_map, out_depth, out_alpha, radii, geom, binning, img)
+
+
+def rasterize_gaussians_backward(background, means3D, radii, colors, semantic_feature, scales,
+                                 rotations, scale_modifier, cov3D_precomp, viewmatrix, projmatrix,
+                                 c_x, c_y, tan_fovx, tan_fovy, dL_dout_color, dL_dout_feature,
+                                 dL_dout_depth, dL_dout_alpha, sh, degree, campos, geomBuffer, R,
+                                 binningBuffer, imageBuffer, alphas, debug, *, compat=None):
+    """RasterizeGaussiansBackwardCUDA (DGR/rasterize_points.cu:128-225).
+
+    Camera scalars are consumed in this positional order, exactly as the
+    reference binding consumes them.  Returns (dL_dmeans2D[P,3],
+    dL_dcolors[P,3], dL_dsemantic[P,F], dL_dopacity[P,1], dL_dmeans3D[P,3],
+    dL_dcov3D[P,6], dL_dsh[P,M,3], dL_dscales[P,3], dL_drotations[P,4]).
+    """
+    L_ = _lib.load()
+    cm = _compat_code(compat)
+    inp = _Inputs(means3D, colors, semantic_feature, None, scales, rotations, scale_modifier,
+                  cov3D_precomp, sh, degree)
+    dev, P = inp.device, inp.P
+    H, W = dL_dout_color.size(1), dL_dout_color.size(2)  # rasterize_points.cu:160-161
+    f32 = dict(dtype=torch.float32, device=dev)
+    if P == 0:
+        z = lambda *s: torch.zeros(*s, **f32)  # noqa: E731
+        return (z(0, 3), z(0, 3), z(0, inp.F_user), z(0, 1), z(0, 3), z(0, 6), z(0, inp.M, 3),
+                z(0, 3), z(0, 4))
+    cam, keep = _camera(dev, background, viewmatrix, projmatrix, campos, c_x, c_y, tan_fovx,
+                        tan_fovy, W, H)
+    g = inp.struct()
+    dLc = _dev(dL_dout_color, dev, "dL_dout_color")
+    dLd = _dev(dL_dout_depth, dev, "dL_dout_depth")
+    dLa = _dev(dL_dout_alpha, dev, "dL_dout_alpha")
+    alphas_c = _dev(alphas, dev, "alpha")
+    dLf = None
+    if inp.F:
+        if _present(dL_dout_feature):
+            dLf = _dev(dL_dout_feature, dev, "dL_dout_feature").reshape(-1, H, W)
+            if dLf.size(0) < inp.F:
+                dLf = torch.cat([dLf, torch.zeros(inp.F - dLf.size(0), H, W, **f32)]).contiguous()
+        else:
+            dLf = torch.zeros(inp.F, H, W, **f32)
+    radii_c = radii.to(device=dev, dtype=torch.int32).contiguous()
+    out = dict(
+        dmeans2D=torch.empty(P, 3, **f32), dcolors=torch.empty(P, 3, **f32),
+        dsem=torch.empty(P, inp.F, **f32), dopacity=torch.empty(P, 1, **f32),
+        dmeans3D=torch.empty(P, 3, **f32), dcov3D=torch.empty(P, 6, **f32),
+        dsh=torch.empty(P, inp.M, 3, **f32), dscales=torch.empty(P, 3, **f32),
+        drot=torch.empty(P, 4, **f32))
+    scratch = torch.empty(L_.gs_backward_scratch_bytes(P, inp.F), dtype=torch.uint8, device=dev)
+    stream = _stream(dev)
+    p = lambda t: t.data_ptr() if (t is not None and t.numel()) else None  # noqa: E731
+    check(L_.gs_backward(ctypes.byref(g), ctypes.byref(cam), radii_c.data_ptr(), int(bool(debug)), cm,
+                         geomBuffer.data_ptr(), p(binningBuffer), imageBuffer.data_ptr(), int(R),
+                         alphas_c.data_ptr(), dLc.data_ptr(), p(dLf), dLd.data_ptr(), dLa.data_ptr(),
+                         scratch.data_ptr(), out["dmeans2D"].data_ptr(), out["dcolors"].data_ptr(),
+                         p(out["dsem"]), out["dopacity"].data_ptr(), out["dmeans3D"].data_ptr(),
+                         out["dcov3D"].data_ptr(), p(out["dsh"]), out["dscales"].data_ptr(),
+                         out["drot"].data_ptr(), stream), "rasterize_gaussians_backward")
+    del keep
+    dsem = out["dsem"][:, :inp.F_user] if inp.F_user != inp.F else out["dsem"]
+    return (out["dmeans2D"], out["dcolors"], dsem, out["dopacity"], out["dmeans3D"],
+            out["dcov3D"], out["dsh"], out["dscales"], out["drot"])
+
+
+def mark_visible(means3D, viewmatrix, projmatrix):
+    """markVisible (DGR/rasterize_points.cu:227-246): bool[P], view-space z > 0."""
+    L_ = _lib.load()
+    dev = means3D.device
+    if dev.type != "cuda":
+        raise _lib.GsplatError("mark_visible needs device tensors")
+    P = means3D.size(0)
+    present = torch.zeros(P, dtype=torch.bool, device=dev)
+    if P:
+        m = _dev(means3D, dev, "means3D")
+        v = _dev(viewmatrix, dev, "viewmatrix").reshape(-1)
+        pr = _dev(projmatrix, dev, "projmatrix").reshape(-1)
+        check(L_.gs_mark_visible(P, m.data_ptr(), v.data_ptr(), pr.data_ptr(), present.data_ptr(),
+                                 _stream(dev)), "mark_visible")
+    return present

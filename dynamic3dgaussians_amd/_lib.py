@@ -1,0 +1,111 @@
+"""ctypes binding of libgsplat_hip.so (C ABI: include/gsplat_hip.h).
+
+This is the only way the package reaches the GPU: there is no CPU or PyTorch
+fallback.  If the HIP library is missing or cannot be loaded, every entry point
+raises immediately with the reason.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+from . import build as _build
+
+_lock = threading.Lock()
+_lib = None
+
+c_void_p = ctypes.c_void_p
+c_int32, c_int64, c_float, c_size_t = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_size_t
+
+GS_COMPAT = {"reference": 0, "fixed": 1}
+SUPPORTED_F = (0, 8, 16, 32, 64)
+
+
+class GsGaussians(ctypes.Structure):
+    _fields_ = [("P", c_int32), ("D", c_int32), ("M", c_int32), ("F", c_int32),
+                ("means3D", c_void_p), ("shs", c_void_p), ("colors_precomp", c_void_p),
+                ("semantic_feature", c_void_p), ("opacities", c_void_p), ("scales", c_void_p),
+                ("rotations", c_void_p), ("cov3D_precomp", c_void_p),
+                ("scale_modifier", c_float), ("_pad", c_int32)]
+
+
+class GsCamera(ctypes.Structure):
+    _fields_ = [("viewmatrix", c_void_p), ("projmatrix", c_void_p), ("campos", c_void_p),
+                ("background", c_void_p), ("c_x", c_float), ("c_y", c_float),
+                ("tan_fovx", c_float), ("tan_fovy", c_float),
+                ("image_width", c_int32), ("image_height", c_int32)]
+
+
+P_G = ctypes.POINTER(GsGaussians)
+P_C = ctypes.POINTER(GsCamera)
+
+# name -> (restype, argtypes); must match include/gsplat_hip.h
+PROTOTYPES = {
+    "gs_version": (ctypes.c_int, []),
+    "gs_last_error": (ctypes.c_char_p, []),
+    "gs_geom_buffer_bytes": (c_size_t, [c_int64]),
+    "gs_binning_buffer_bytes": (c_size_t, [c_int64]),
+    "gs_image_buffer_bytes": (c_size_t, [c_int32, c_int32]),
+    "gs_backward_scratch_bytes": (c_size_t, [c_int64, c_int32]),
+    "gs_forward_plan": (ctypes.c_int, [P_G, P_C, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void_p,
+                                       c_void_p, ctypes.POINTER(c_int64), c_void_p]),
+    "gs_forward_render": (ctypes.c_int, [P_G, P_C, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p,
+                                         c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
+                                         c_void_p, c_void_p]),
+    "gs_backward": (ctypes.c_int, [P_G, P_C, c_void_p, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p,
+                                   c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
+                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "gs_mark_visible": (ctypes.c_int, [c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "gs_debug_export": (ctypes.c_int, [c_int64, c_int32, c_int32, c_void_p, c_void_p, c_void_p,
+                                       c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                       c_void_p, c_void_p, c_void_p, c_void_p]),
+    "gs_sort_scratch_bytes": (c_size_t, [c_int64]),
+    "gs_sort_pairs": (ctypes.c_int, [c_int64, c_void_p, c_void_p, ctypes.c_int, c_void_p, c_void_p]),
+    "gs_test_wave_reduce": (ctypes.c_int, [ctypes.c_int, c_void_p, c_void_p, c_void_p]),
+}
+
+
+class GsplatError(RuntimeError):
+    pass
+
+
+def lib_path() -> str:
+    return _build.LIB
+
+
+def load(auto_build: bool = True):
+    """Load libgsplat_hip.so (building it first if stale and hipcc is present)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        path = _build.LIB
+        if auto_build:
+            try:
+                if _build.is_stale():
+                    _build.build()
+            except RuntimeError:
+                if not os.path.exists(path):
+                    raise
+        if not os.path.exists(path):
+            raise GsplatError(
+                f"libgsplat_hip.so not found at {path}; build it with "
+                "`python -m dynamic3dgaussians_amd.build` (requires ROCm hipcc). "
+                "There is no CPU fallback.")
+        L = ctypes.CDLL(path)
+        for name, (res, args) in PROTOTYPES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        if L.gs_version() != 1:
+            raise GsplatError(f"ABI version mismatch: library reports {L.gs_version()}")
+        _lib = L
+        return L
+
+
+def check(code: int, what: str):
+    if code != 0:
+        msg = load().gs_last_error().decode(errors="replace")
+        raise GsplatError(f"{what} failed (status {code}): {msg}")

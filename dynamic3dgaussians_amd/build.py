@@ -1,0 +1,101 @@
+"""Build libgsplat_hip.so (hand-written HIP kernels for gfx950) in-tree.
+
+    python -m dynamic3dgaussians_amd.build          # build if stale
+    python -m dynamic3dgaussians_amd.build --force  # rebuild
+
+Each .hip translation unit is compiled to an object with hipcc and the objects
+are linked into one shared library exposing the C ABI of include/gsplat_hip.h.
+The library is written next to this file (lib/), so it travels with the repo
+snapshot to the GPU box.  hipcc cross-compiles for gfx950 without a GPU.
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+INCLUDE = os.path.join(REPO, "include")
+OUT_DIR = os.path.join(PKG, "lib")
+BUILD_DIR = os.path.join(OUT_DIR, "obj")
+LIB = os.path.join(OUT_DIR, "libgsplat_hip.so")
+ARCH = os.environ.get("GSPLAT_OFFLOAD_ARCH", "gfx950")
+
+# Per-file flags.  The preprocess kernels are compiled without FMA
+# contraction so that they follow the CPU oracle's operation order exactly.
+SOURCES = {
+    "gs_preprocess.hip": ["-ffp-contract=off"],
+    "gs_binning.hip": [],
+    "gs_render.hip": [],
+    "gs_api.hip": [],
+}
+COMMON = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall",
+          "-Wno-unused-function", "-I", CSRC, "-I", INCLUDE]
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found: the HIP toolchain (ROCm) is required to build libgsplat_hip.so")
+
+
+def _deps() -> list[str]:
+    files = [os.path.join(CSRC, f) for f in os.listdir(CSRC)]
+    files.append(os.path.join(INCLUDE, "gsplat_hip.h"))
+    files.append(os.path.abspath(__file__))
+    return files
+
+
+def is_stale() -> bool:
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    return any(os.path.getmtime(f) > t for f in _deps())
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not is_stale():
+        return LIB
+    os.makedirs(BUILD_DIR, exist_ok=True)
+    cc = hipcc()
+
+    def compile_one(item):
+        src, extra = item
+        obj = os.path.join(BUILD_DIR, src.replace(".hip", ".o"))
+        cmd = [cc, *COMMON, *extra, "-c", os.path.join(CSRC, src), "-o", obj]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed on {src}:\n{r.stdout}\n{r.stderr}")
+        if verbose and r.stderr.strip():
+            print(r.stderr, file=sys.stderr)
+        return obj
+
+    with cf.ThreadPoolExecutor(max_workers=min(4, os.cpu_count() or 1)) as ex:
+        objs = list(ex.map(compile_one, SOURCES.items()))
+    tmp = LIB + ".tmp"
+    cmd = [cc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", tmp]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+    os.replace(tmp, LIB)
+    return LIB
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-v", "--verbose", action="store_true")
+    args = ap.parse_args()
+    print(build(force=args.force, verbose=args.verbose))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,324 @@
+// gs_api.hip -- the C ABI (include/gsplat_hip.h): argument checks, opaque
+// state-buffer carving, launch order and error reporting.  Host code only.
+//
+// Launch order mirrors CudaRasterizer::Rasterizer::forward/backward
+// (DGR/cuda_rasterizer/rasterizer_impl.cu:198-467), but everything goes to
+// the caller's stream, nothing is allocated inside the library, and the
+// backward's per-call cudaMalloc/cudaFree (:408-409, :436) is gone.
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+
+#include "../../include/gsplat_hip.h"
+#include "gs_common.h"
+#include "gs_kernels.h"
+
+using namespace gs;
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+// Post-launch check: always catch launch errors; with `debug`, also
+// synchronise and surface asynchronous faults (the reference's CHECK_CUDA
+// debug mode, CR/auxiliary.h:172-179).
+int check(const char* what, int debug, hipStream_t s) {
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess && debug) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return fail((int)e, "%s: %s", what, hipGetErrorString(e));
+  return 0;
+}
+
+int higher_msb(uint32_t n) {  // getHigherMsb, CR/rasterizer_impl.cu:35-50
+  uint32_t msb = sizeof(n) * 4, step = msb;
+  while (step > 1) {
+    step /= 2;
+    if (n >> msb) msb += step; else msb -= step;
+  }
+  if (n >> msb) msb++;
+  return (int)msb;
+}
+
+// Which ping-pong slot holds the sorted (key, id) pairs after the radix sort:
+// every 8-bit pass swaps the slots (see launch_radix_sort).
+int sorted_slot(int64_t L, int W, int H) {
+  if (L <= 1) return 0;
+  const int gx = (W + TILE - 1) / TILE, gy = (H + TILE - 1) / TILE;
+  const int end_bit = 32 + higher_msb((uint32_t)(gx * gy));
+  return ((end_bit + 7) / 8) & 1;
+}
+
+template <class T>
+T* at(void* base, size_t off) { return reinterpret_cast<T*>(static_cast<char*>(base) + off); }
+template <class T>
+const T* at(const void* base, size_t off) { return reinterpret_cast<const T*>(static_cast<const char*>(base) + off); }
+
+bool feature_supported(int F) { return F == 0 || F == 8 || F == 16 || F == 32 || F == 64; }
+
+int check_gaussians(const gs_gaussians* g, const gs_camera* c, bool forward) {
+  if (!g || !c) return fail(-1, "null argument block");
+  if (g->P < 0) return fail(-1, "P must be >= 0 (got %d)", g->P);
+  if (c->image_width <= 0 || c->image_height <= 0)
+    return fail(-1, "image size must be positive (got %dx%d)", c->image_width, c->image_height);
+  if (!feature_supported(g->F))
+    return fail(-1, "semantic feature width %d not instantiated (0, 8, 16, 32, 64)", g->F);
+  if (g->P > 0) {
+    if (!g->means3D || (forward && !g->opacities)) return fail(-1, "means3D and opacities are required");
+    if (!c->viewmatrix || !c->projmatrix || !c->campos || !c->background)
+      return fail(-1, "camera matrices, campos and background are required");
+    if (!g->colors_precomp && !g->shs) return fail(-1, "provide SHs or precomputed colors");
+    if (!g->cov3D_precomp && (!g->scales || !g->rotations))
+      return fail(-1, "provide scales+rotations or a precomputed 3D covariance");
+    if (g->shs && (g->D < 0 || g->D > 3 || g->M < (g->D + 1) * (g->D + 1)))
+      return fail(-1, "SH degree %d needs M >= %d coefficients (got M=%d)", g->D, (g->D + 1) * (g->D + 1), g->M);
+    if (g->F > 0 && !g->semantic_feature) return fail(-1, "F > 0 but semantic_feature is null");
+  }
+  return 0;
+}
+}  // namespace
+
+extern "C" {
+
+int gs_version(void) { return GS_ABI_VERSION; }
+const char* gs_last_error(void) { return g_err.c_str(); }
+
+size_t gs_geom_buffer_bytes(int64_t P) { return GeomLayout(P > 0 ? P : 0).total; }
+size_t gs_binning_buffer_bytes(int64_t L) { return BinLayout(L > 0 ? L : 0).total; }
+size_t gs_image_buffer_bytes(int32_t W, int32_t H) { return ImgLayout(W, H).total; }
+size_t gs_backward_scratch_bytes(int64_t P, int32_t F) {
+  return align_up(sizeof(float) * (size_t)(A_FEAT + F) * (size_t)(P > 0 ? P : 0), 256) + 256;
+}
+
+int gs_forward_plan(const gs_gaussians* g, const gs_camera* cam, int prefiltered, int debug, int compat,
+                    void* geom, int32_t* radii, int64_t* num_rendered, gs_stream_t stream) {
+  if (int e = check_gaussians(g, cam, true)) return e;
+  if (!num_rendered) return fail(-1, "num_rendered is null");
+  *num_rendered = 0;
+  const int P = g->P;
+  if (P == 0) return 0;
+  if (!geom || !radii) return fail(-1, "geom buffer and radii are required");
+  hipStream_t s = (hipStream_t)stream;
+  const GeomLayout gl(P);
+  const int W = cam->image_width, H = cam->image_height;
+  PreprocessArgs a{};
+  a.P = P; a.D = g->D; a.M = g->M; a.W = W; a.H = H;
+  a.grid_x = (W + TILE - 1) / TILE; a.grid_y = (H + TILE - 1) / TILE;
+  a.prefiltered = prefiltered;
+  a.means3D = g->means3D; a.scales = g->scales; a.rotations = g->rotations; a.opacities = g->opacities;
+  a.shs = g->shs; a.cov3D_precomp = g->cov3D_precomp; a.colors_precomp = g->colors_precomp;
+  a.view = cam->viewmatrix; a.proj = cam->projmatrix; a.campos = cam->campos;
+  a.scale_modifier = g->scale_modifier;
+  a.c_x = cam->c_x; a.c_y = cam->c_y; a.tan_fovx = cam->tan_fovx; a.tan_fovy = cam->tan_fovy;
+  a.focal_y = (float)H / (2.0f * cam->tan_fovy);  // CR/rasterizer_impl.cu:227-228
+  a.focal_x = (float)W / (2.0f * cam->tan_fovx);
+  a.radii = radii;
+  a.rec = at<float>(geom, gl.rec);
+  a.cov3D = at<float>(geom, gl.cov3D);
+  a.clamped = at<uint8_t>(geom, gl.clamped);
+  a.tiles = at<uint32_t>(geom, gl.tiles);
+  a.status = at<int>(geom, gl.status);
+  (void)hipMemsetAsync(a.status, 0, 16, s);
+  launch_preprocess_fwd(a, s);
+  if (int e = check("preprocess", debug, s)) return e;
+  uint32_t* offsets = at<uint32_t>(geom, gl.offsets);
+  launch_scan(a.tiles, offsets, at<uint32_t>(geom, gl.blocksums), P, s);
+  if (int e = check("scan", debug, s)) return e;
+  // The one host read of the forward (CR/rasterizer_impl.cu:287): the total
+  // instance count sizes the binning buffer.  The status word rides along.
+  uint32_t host[2] = {0, 0};
+  hipError_t he = hipMemcpyAsync(&host[0], offsets + P - 1, 4, hipMemcpyDeviceToHost, s);
+  if (he == hipSuccess) he = hipMemcpyAsync(&host[1], a.status, 4, hipMemcpyDeviceToHost, s);
+  if (he == hipSuccess) he = hipStreamSynchronize(s);
+  if (he != hipSuccess) return fail((int)he, "num_rendered readback: %s", hipGetErrorString(he));
+  if (host[1]) return fail(-2, "Point is filtered although prefiltered is set. This shouldn't happen!");
+  *num_rendered = host[0];
+  (void)compat;
+  return 0;
+}
+
+int gs_forward_render(const gs_gaussians* g, const gs_camera* cam, int debug, int compat, void* geom,
+                      void* binning, void* image, int64_t L, const int32_t* radii, float* out_color,
+                      float* out_feature, float* out_depth, float* out_alpha, gs_stream_t stream) {
+  if (int e = check_gaussians(g, cam, true)) return e;
+  const int P = g->P;
+  if (P == 0) return 0;  // the reference leaves the zero-filled outputs untouched
+  if (!geom || !image || (L > 0 && !binning) || !radii) return fail(-1, "state buffers are required");
+  if (!out_color || !out_depth || (g->F > 0 && !out_feature) || (compat != COMPAT_REFERENCE && !out_alpha))
+    return fail(-1, "output image pointers are required");
+  hipStream_t s = (hipStream_t)stream;
+  const int W = cam->image_width, H = cam->image_height;
+  const int gx = (W + TILE - 1) / TILE, gy = (H + TILE - 1) / TILE;
+  const GeomLayout gl(P);
+  const BinLayout bl(L);
+  const ImgLayout il(W, H);
+  const float* rec = at<float>(geom, gl.rec);
+  uint2* ranges = at<uint2>(image, il.ranges);
+  const uint32_t* point_list = nullptr;
+  const uint64_t* sorted_keys = nullptr;
+  if (L > 0) {
+    uint64_t* k0 = at<uint64_t>(binning, bl.keys0);
+    uint64_t* k1 = at<uint64_t>(binning, bl.keys1);
+    uint32_t* v0 = at<uint32_t>(binning, bl.vals0);
+    uint32_t* v1 = at<uint32_t>(binning, bl.vals1);
+    launch_duplicate(P, rec, at<uint32_t>(geom, gl.offsets), radii, gx, gy, k0, v0, s);
+    if (int e = check("duplicateWithKeys", debug, s)) return e;
+    const int bit = higher_msb((uint32_t)(gx * gy));
+    const int which = launch_radix_sort(L, k0, v0, k1, v1, at<uint32_t>(binning, bl.hist),
+                                        at<uint32_t>(binning, bl.rowtot), 32 + bit, s);
+    if (int e = check("radix sort", debug, s)) return e;
+    if (which != sorted_slot(L, W, H)) return fail(-3, "internal: sort slot mismatch");
+    sorted_keys = which ? k1 : k0;
+    point_list = which ? v1 : v0;
+  }
+  launch_tile_ranges(L, sorted_keys, ranges, gx * gy, s);
+  if (int e = check("identifyTileRanges", debug, s)) return e;
+  RenderArgs ra{};
+  ra.W = W; ra.H = H; ra.grid_x = gx; ra.num_tiles = gx * gy; ra.F = g->F; ra.compat = compat;
+  ra.ranges = ranges; ra.point_list = point_list; ra.rec = rec; ra.feats = g->semantic_feature;
+  ra.bg = cam->background;
+  ra.out_color = out_color; ra.out_feature = out_feature; ra.out_depth = out_depth; ra.out_alpha = out_alpha;
+  ra.n_contrib = at<uint32_t>(image, il.n_contrib);
+  if (!launch_render_fwd(ra, s)) return fail(-1, "unsupported feature width %d", g->F);
+  return check("render", debug, s);
+}
+
+int gs_backward(const gs_gaussians* g, const gs_camera* cam, const int32_t* radii, int debug, int compat,
+                const void* geom, const void* binning, const void* image, int64_t L, const float* alphas,
+                const float* dL_dout_color, const float* dL_dout_feature, const float* dL_dout_depth,
+                const float* dL_dout_alpha, void* scratch, float* dL_dmeans2D, float* dL_dcolors,
+                float* dL_dsemantic, float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh,
+                float* dL_dscales, float* dL_drotations, gs_stream_t stream) {
+  if (int e = check_gaussians(g, cam, false)) return e;
+  const int P = g->P;
+  if (P == 0) return 0;
+  if (!geom || !image || !scratch || !radii || (L > 0 && !binning)) return fail(-1, "state buffers are required");
+  if (!alphas || !dL_dout_color || !dL_dout_depth || !dL_dout_alpha || (g->F > 0 && !dL_dout_feature))
+    return fail(-1, "upstream gradients are required");
+  if (!dL_dmeans2D || !dL_dcolors || !dL_dopacity || !dL_dmeans3D || !dL_dcov3D || !dL_dscales ||
+      !dL_drotations || (g->F > 0 && !dL_dsemantic) || (g->M > 0 && !dL_dsh))
+    return fail(-1, "gradient outputs are required");
+  hipStream_t s = (hipStream_t)stream;
+  const int W = cam->image_width, H = cam->image_height;
+  const int gx = (W + TILE - 1) / TILE, gy = (H + TILE - 1) / TILE;
+  const GeomLayout gl(P);
+  const BinLayout bl(L);
+  const ImgLayout il(W, H);
+  float* acc = static_cast<float*>(scratch);
+  (void)hipMemsetAsync(acc, 0, sizeof(float) * (size_t)(A_FEAT + g->F) * P, s);
+  RenderBwdArgs ra{};
+  ra.W = W; ra.H = H; ra.grid_x = gx; ra.num_tiles = gx * gy; ra.F = g->F; ra.compat = compat;
+  ra.ranges = at<uint2>(image, il.ranges);
+  ra.point_list = L > 0 ? at<uint32_t>(binning, sorted_slot(L, W, H) ? bl.vals1 : bl.vals0) : nullptr;
+  ra.rec = at<float>(geom, gl.rec);
+  ra.feats = g->semantic_feature;
+  ra.bg = cam->background;
+  ra.alphas = alphas;
+  ra.n_contrib = at<uint32_t>(image, il.n_contrib);
+  ra.dL_dpix = dL_dout_color; ra.dL_dfeat = dL_dout_feature; ra.dL_ddepth = dL_dout_depth;
+  ra.dL_dalpha = dL_dout_alpha; ra.acc = acc;
+  if (!launch_render_bwd(ra, s)) return fail(-1, "unsupported feature width %d", g->F);
+  if (int e = check("render backward", debug, s)) return e;
+  PreprocessBwdArgs b{};
+  b.P = P; b.D = g->D; b.M = g->M; b.F = g->F; b.W = W; b.H = H; b.compat = compat;
+  b.means3D = g->means3D; b.radii = radii; b.shs = g->shs; b.clamped = at<uint8_t>(geom, gl.clamped);
+  b.scales = g->scales; b.rotations = g->rotations;
+  b.cov3D = g->cov3D_precomp ? g->cov3D_precomp : at<float>(geom, gl.cov3D);
+  b.view = cam->viewmatrix; b.proj = cam->projmatrix; b.campos = cam->campos;
+  b.scale_modifier = g->scale_modifier;
+  b.c_x = cam->c_x; b.c_y = cam->c_y; b.tan_fovx = cam->tan_fovx; b.tan_fovy = cam->tan_fovy;
+  b.focal_y = (float)H / (2.0f * cam->tan_fovy);  // CR/rasterizer_impl.cu:398-399
+  b.focal_x = (float)W / (2.0f * cam->tan_fovx);
+  b.acc = acc;
+  b.dmeans2D = dL_dmeans2D; b.dcolors = dL_dcolors; b.dsemantic = dL_dsemantic; b.dopacity = dL_dopacity;
+  b.dmeans3D = dL_dmeans3D; b.dcov3D = dL_dcov3D; b.dsh = dL_dsh; b.dscales = dL_dscales;
+  b.drot = dL_drotations;
+  launch_preprocess_bwd(b, s);
+  return check("preprocess backward", debug, s);
+}
+
+int gs_mark_visible(int64_t P, const float* means3D, const float* viewmatrix, const float* projmatrix,
+                    uint8_t* present, gs_stream_t stream) {
+  (void)projmatrix;
+  if (P < 0) return fail(-1, "P must be >= 0");
+  if (P == 0) return 0;
+  if (!means3D || !viewmatrix || !present) return fail(-1, "null argument");
+  hipStream_t s = (hipStream_t)stream;
+  launch_mark_visible((int)P, means3D, viewmatrix, present, s);
+  return check("markVisible", 0, s);
+}
+
+int gs_debug_export(int64_t P, int32_t W, int32_t H, const void* geom, const void* binning, const void* image,
+                    int64_t L, float* means2D, float* depths, float* conic_opacity, float* rgb,
+                    uint32_t* tiles_touched, uint32_t* point_list, uint32_t* ranges, uint32_t* n_contrib,
+                    gs_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const GeomLayout gl(P);
+  const BinLayout bl(L);
+  const ImgLayout il(W, H);
+  const float* rec = at<float>(geom, gl.rec);
+  hipError_t e = hipSuccess;
+  auto cp2d = [&](float* dst, int cols, int first) {
+    if (dst && P > 0 && e == hipSuccess)
+      e = hipMemcpy2DAsync(dst, sizeof(float) * cols, rec + first, sizeof(float) * REC, sizeof(float) * cols,
+                           (size_t)P, hipMemcpyDeviceToDevice, s);
+  };
+  cp2d(means2D, 2, R_X);
+  cp2d(depths, 1, R_DEPTH);
+  if (conic_opacity && P > 0 && e == hipSuccess)
+    e = hipMemcpy2DAsync(conic_opacity, sizeof(float) * 4, rec + R_CA, sizeof(float) * REC, sizeof(float) * 4,
+                         (size_t)P, hipMemcpyDeviceToDevice, s);
+  cp2d(rgb, 3, R_R);
+  if (tiles_touched && P > 0 && e == hipSuccess)
+    e = hipMemcpyAsync(tiles_touched, at<uint32_t>(geom, gl.tiles), 4 * P, hipMemcpyDeviceToDevice, s);
+  if (point_list && L > 0 && e == hipSuccess)
+    e = hipMemcpyAsync(point_list, at<uint32_t>(binning, sorted_slot(L, W, H) ? bl.vals1 : bl.vals0), 4 * L,
+                       hipMemcpyDeviceToDevice, s);
+  const int64_t tiles = (int64_t)((W + TILE - 1) / TILE) * ((H + TILE - 1) / TILE);
+  if (ranges && e == hipSuccess)
+    e = hipMemcpyAsync(ranges, at<uint32_t>(image, il.ranges), 8 * tiles, hipMemcpyDeviceToDevice, s);
+  if (n_contrib && e == hipSuccess)
+    e = hipMemcpyAsync(n_contrib, at<uint32_t>(image, il.n_contrib), 4 * (size_t)W * H, hipMemcpyDeviceToDevice, s);
+  if (e != hipSuccess) return fail((int)e, "debug export: %s", hipGetErrorString(e));
+  return 0;
+}
+
+size_t gs_sort_scratch_bytes(int64_t n) {
+  const BinLayout bl(n);
+  return bl.total;
+}
+
+int gs_sort_pairs(int64_t n, uint64_t* keys, uint32_t* vals, int end_bit, void* scratch, gs_stream_t stream) {
+  if (n < 0 || end_bit < 0 || end_bit > 64) return fail(-1, "bad sort arguments");
+  if (n <= 1) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  const BinLayout bl(n);
+  uint64_t* k1 = at<uint64_t>(scratch, bl.keys1);
+  uint32_t* v1 = at<uint32_t>(scratch, bl.vals1);
+  const int which = launch_radix_sort(n, keys, vals, k1, v1, at<uint32_t>(scratch, bl.hist),
+                                      at<uint32_t>(scratch, bl.rowtot), end_bit, s);
+  if (which) {
+    (void)hipMemcpyAsync(keys, k1, 8 * n, hipMemcpyDeviceToDevice, s);
+    (void)hipMemcpyAsync(vals, v1, 4 * n, hipMemcpyDeviceToDevice, s);
+  }
+  return check("sort", 0, s);
+}
+
+int gs_test_wave_reduce(int n_comp, const float* in, float* out, gs_stream_t stream) {
+  if (n_comp < 1 || n_comp > 64) return fail(-1, "n_comp must be in [1, 64]");
+  launch_test_wave_reduce(n_comp, in, out, (hipStream_t)stream);
+  return check("wave reduce test", 1, (hipStream_t)stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,196 @@
+// gs_common.h -- shared constants, layouts and device helpers of the
+// MI355X-native Gaussian rasterizer (gfx950, wave64).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gs {
+
+// Binning tile = 16x16 pixels, identical to the reference (CR/config.h:18-19)
+// so that tiles_touched / num_rendered / sort keys agree with it.  Inside a
+// tile the blend kernels use 4 waves of 16x4 pixels each.
+constexpr int TILE = 16;
+constexpr int TILE_PIX = TILE * TILE;
+constexpr int WAVE = 64;
+constexpr int WAVE_ROWS = 4;  // a wave covers 16 x 4 pixels of its tile
+
+// Per-Gaussian render record written by preprocess: one 64-B line, read by
+// the blend kernels with a single wave-uniform s_load_dwordx16.
+constexpr int REC = 16;
+enum RecField {
+  R_X = 0, R_Y = 1,           // pixel-space mean (ndc2Pix)
+  R_CA = 2, R_CB = 3, R_CC = 4,  // conic (inverse 2D covariance)
+  R_OP = 5,                   // opacity
+  R_R = 6, R_G = 7, R_B = 8,  // colour (SH-evaluated or precomputed)
+  R_DEPTH = 9,                // view-space z
+  R_EX = 10, R_EY = 11,       // half extents of the alpha >= 1/255 region
+  R_RAD = 12,                 // screen radius (ceil(3 sqrt(lambda_max)))
+};
+
+// Gradient accumulation record per Gaussian (backward scratch): CS = 10 + F
+enum AccField {
+  A_MX = 0, A_MY = 1, A_CA = 2, A_CB = 3, A_CC = 4, A_OP = 5,
+  A_R = 6, A_G = 7, A_B = 8, A_DEPTH = 9, A_FEAT = 10,
+};
+
+constexpr int COMPAT_REFERENCE = 0;
+constexpr int COMPAT_FIXED = 1;
+
+__host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// ---------------------------------------------------------------- layouts
+// Geometry buffer (per-Gaussian state kept from forward to backward).
+struct GeomLayout {
+  size_t rec, cov3D, clamped, tiles, offsets, blocksums, status, total;
+  static constexpr int SCAN_ITEMS = 2048;  // items per scan block
+  __host__ __device__ GeomLayout(int64_t P) {
+    size_t o = 0;
+    rec = o;       o = align_up(o + sizeof(float) * REC * P, 256);
+    cov3D = o;     o = align_up(o + sizeof(float) * 6 * P, 256);
+    clamped = o;   o = align_up(o + P, 256);
+    tiles = o;     o = align_up(o + sizeof(uint32_t) * P, 256);
+    offsets = o;   o = align_up(o + sizeof(uint32_t) * P, 256);
+    blocksums = o; o = align_up(o + sizeof(uint32_t) * ((P + SCAN_ITEMS - 1) / SCAN_ITEMS + 1), 256);
+    status = o;    o = align_up(o + 64, 256);
+    total = o;
+  }
+};
+
+// Binning buffer (per tile/Gaussian instance).
+struct BinLayout {
+  static constexpr int SORT_THREADS = 256;
+  static constexpr int SORT_ITEMS = 16;  // per thread per block
+  static constexpr int SORT_TILE = SORT_THREADS * SORT_ITEMS;
+  size_t keys0, keys1, vals0, vals1, hist, rowtot, total;
+  int64_t nblk;
+  __host__ __device__ BinLayout(int64_t L) {
+    nblk = (L + SORT_TILE - 1) / SORT_TILE;
+    size_t o = 0;
+    keys0 = o; o = align_up(o + sizeof(uint64_t) * L, 256);
+    keys1 = o; o = align_up(o + sizeof(uint64_t) * L, 256);
+    vals0 = o; o = align_up(o + sizeof(uint32_t) * L, 256);
+    vals1 = o; o = align_up(o + sizeof(uint32_t) * L, 256);
+    hist = o;  o = align_up(o + sizeof(uint32_t) * 256 * (nblk > 0 ? nblk : 1), 256);
+    rowtot = o; o = align_up(o + sizeof(uint32_t) * 256, 256);
+    total = o;
+  }
+};
+
+// Image buffer (per pixel / per tile).
+struct ImgLayout {
+  size_t ranges, n_contrib, total;
+  __host__ __device__ ImgLayout(int W, int H) {
+    const int64_t tiles = (int64_t)((W + TILE - 1) / TILE) * ((H + TILE - 1) / TILE);
+    size_t o = 0;
+    ranges = o;    o = align_up(o + sizeof(uint32_t) * 2 * (tiles > 0 ? tiles : 1), 256);
+    n_contrib = o; o = align_up(o + sizeof(uint32_t) * (int64_t)W * H, 256);
+    total = o;
+  }
+};
+
+// ---------------------------------------------------------------- device math
+
+// XCD-aware block -> work-item remap (bijective for any n).  Consecutive
+// work items land on the same XCD (shared L2) instead of being dealt
+// round-robin over the 8 XCDs (cdna_hip_programming.md T1).
+__device__ inline int xcd_remap(int bid, int n) {
+  const int q = n / 8, r = n % 8;
+  const int xcd = bid % 8, slot = bid / 8;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + slot;
+}
+
+__device__ inline float bits_f(uint32_t u) { return __uint_as_float(u); }
+__device__ inline uint32_t f_bits(float f) { return __float_as_uint(f); }
+
+// DPP lane permutations on gfx950 (row = 16 lanes).
+template <int CTRL>
+__device__ inline float dpp(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+constexpr int DPP_ROW_ROR8 = 0x128;      // lane i <- lane (i+8)%16: xor 8
+constexpr int DPP_ROW_HALF_MIRROR = 0x141;  // lane i <- 7-i in each 8: partner differs in bit 2
+constexpr int DPP_QUAD_XOR2 = 0x4E;      // quad_perm [2,3,0,1]
+constexpr int DPP_QUAD_XOR1 = 0xB1;      // quad_perm [1,0,3,2]
+
+// One level of the transposed wave reduction on a pair (a, b) for lane-bit
+// `bit`: lanes with the bit clear end up with a's pair-sum, lanes with it set
+// with b's.  LEVEL 0/1 use the gfx950 permlane32/16 swaps, 2..5 use DPP.
+template <int LEVEL>
+__device__ inline float red_pair(float a, float b, int lane) {
+  if constexpr (LEVEL == 0) {
+    auto r = __builtin_amdgcn_permlane32_swap(f_bits(a), f_bits(b), false, false);
+    return bits_f(r[0]) + bits_f(r[1]);
+  } else if constexpr (LEVEL == 1) {
+    auto r = __builtin_amdgcn_permlane16_swap(f_bits(a), f_bits(b), false, false);
+    return bits_f(r[0]) + bits_f(r[1]);
+  } else {
+    constexpr int bit = 5 - LEVEL;  // 3, 2, 1, 0
+    const bool hi = (lane >> bit) & 1;
+    const float keep = hi ? b : a;
+    const float send = hi ? a : b;
+    if constexpr (LEVEL == 2) return keep + dpp<DPP_ROW_ROR8>(send);
+    else if constexpr (LEVEL == 3) return keep + dpp<DPP_ROW_HALF_MIRROR>(send);
+    else if constexpr (LEVEL == 4) return keep + dpp<DPP_QUAD_XOR2>(send);
+    else return keep + dpp<DPP_QUAD_XOR1>(send);
+  }
+}
+template <int LEVEL>
+__device__ inline float red_self(float a) {
+  if constexpr (LEVEL == 0) {
+    auto r = __builtin_amdgcn_permlane32_swap(f_bits(a), f_bits(a), false, false);
+    return bits_f(r[0]) + bits_f(r[1]);
+  } else if constexpr (LEVEL == 1) {
+    auto r = __builtin_amdgcn_permlane16_swap(f_bits(a), f_bits(a), false, false);
+    return bits_f(r[0]) + bits_f(r[1]);
+  } else if constexpr (LEVEL == 2) return a + dpp<DPP_ROW_ROR8>(a);
+  else if constexpr (LEVEL == 3) return a + dpp<DPP_ROW_HALF_MIRROR>(a);
+  else if constexpr (LEVEL == 4) return a + dpp<DPP_QUAD_XOR2>(a);
+  else return a + dpp<DPP_QUAD_XOR1>(a);
+}
+
+template <int LEVEL, int N>
+__device__ inline void red_level(float (&v)[64], int lane) {
+#pragma unroll
+  for (int i = 0; i < N / 2; ++i) v[i] = red_pair<LEVEL>(v[2 * i], v[2 * i + 1], lane);
+  if constexpr (N % 2) v[N / 2] = red_self<LEVEL>(v[N - 1]);
+}
+
+// Transposed wave64 reduction of N <= 64 per-lane components: on return,
+// lane l holds the 64-lane sum of component bitrev6(l) (lanes whose
+// bitrev6(l) >= N hold duplicates and must be ignored).  Costs about
+// 2N + N/2 + ... VALU ops instead of 6N for N independent butterfly trees,
+// and lets ONE atomic wave-instruction commit all N sums.
+__device__ inline int bitrev6(int l) {
+  return ((l & 1) << 5) | ((l & 2) << 3) | ((l & 4) << 1) | ((l & 8) >> 1) | ((l & 16) >> 3) | ((l & 32) >> 5);
+}
+template <int N>
+__device__ inline float wave_reduce_transposed(float (&v)[64], int lane) {
+  static_assert(N >= 1 && N <= 64, "N in [1,64]");
+  constexpr int N1 = (N + 1) / 2, N2 = (N1 + 1) / 2, N3 = (N2 + 1) / 2, N4 = (N3 + 1) / 2,
+                N5 = (N4 + 1) / 2;
+  red_level<0, N>(v, lane);
+  red_level<1, N1>(v, lane);
+  red_level<2, N2>(v, lane);
+  red_level<3, N3>(v, lane);
+  red_level<4, N4>(v, lane);
+  red_level<5, N5>(v, lane);
+  return v[0];
+}
+
+__device__ inline float wave_max_f(float x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x = fmaxf(x, __shfl_xor(x, o, 64));
+  return x;
+}
+__device__ inline uint32_t wave_max_u(uint32_t x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    uint32_t y = __shfl_xor(x, o, 64);
+    x = x > y ? x : y;
+  }
+  return x;
+}
+
+}  // namespace gs

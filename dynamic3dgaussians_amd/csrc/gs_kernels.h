@@ -1,0 +1,104 @@
+// gs_kernels.h -- kernel argument blocks and host launchers (internal).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gs {
+
+struct PreprocessArgs {
+  int P, D, M, W, H, grid_x, grid_y, prefiltered;
+  const float* means3D;
+  const float* scales;
+  const float* rotations;
+  const float* opacities;
+  const float* shs;
+  const float* cov3D_precomp;
+  const float* colors_precomp;
+  const float* view;
+  const float* proj;
+  const float* campos;
+  float scale_modifier, c_x, c_y, tan_fovx, tan_fovy, focal_x, focal_y;
+  int* radii;
+  float* rec;
+  float* cov3D;
+  uint8_t* clamped;
+  uint32_t* tiles;
+  int* status;
+};
+
+struct PreprocessBwdArgs {
+  int P, D, M, F, W, H, compat;
+  const float* means3D;
+  const int* radii;
+  const float* shs;
+  const uint8_t* clamped;
+  const float* scales;
+  const float* rotations;
+  const float* cov3D;  // precomputed or the forward's
+  const float* view;
+  const float* proj;
+  const float* campos;
+  float scale_modifier, c_x, c_y, tan_fovx, tan_fovy, focal_x, focal_y;
+  const float* acc;  // P x (10+F) blend gradients
+  float* dmeans2D;
+  float* dcolors;
+  float* dsemantic;
+  float* dopacity;
+  float* dmeans3D;
+  float* dcov3D;
+  float* dsh;
+  float* dscales;
+  float* drot;
+};
+
+struct RenderArgs {
+  int W, H, grid_x, num_tiles, F, compat;
+  const uint2* ranges;
+  const uint32_t* point_list;
+  const float* rec;
+  const float* feats;  // P x F
+  const float* bg;     // 3
+  float* out_color;
+  float* out_feature;
+  float* out_depth;
+  float* out_alpha;
+  uint32_t* n_contrib;
+};
+
+struct RenderBwdArgs {
+  int W, H, grid_x, num_tiles, F, compat;
+  const uint2* ranges;
+  const uint32_t* point_list;
+  const float* rec;
+  const float* feats;
+  const float* bg;
+  const float* alphas;
+  const uint32_t* n_contrib;
+  const float* dL_dpix;
+  const float* dL_dfeat;
+  const float* dL_ddepth;
+  const float* dL_dalpha;
+  float* acc;  // P x (10+F), zeroed by the caller
+};
+
+void launch_preprocess_fwd(const PreprocessArgs& a, hipStream_t s);
+void launch_preprocess_bwd(const PreprocessBwdArgs& a, hipStream_t s);
+void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t s);
+
+// Binning: inclusive scan of tiles_touched (P) into offsets, block sums in tmp.
+void launch_scan(const uint32_t* in, uint32_t* out, uint32_t* tmp, int P, hipStream_t s);
+void launch_duplicate(int P, const float* rec, const uint32_t* offsets, const int* radii, int grid_x,
+                      int grid_y, uint64_t* keys, uint32_t* vals, hipStream_t s);
+// Stable LSD radix sort on bits [0, end_bit); the result ends in keys0/vals0
+// or keys1/vals1 -- returns 0 or 1 for which.
+int launch_radix_sort(int64_t n, uint64_t* keys0, uint32_t* vals0, uint64_t* keys1, uint32_t* vals1,
+                      uint32_t* hist, uint32_t* rowtot, int end_bit, hipStream_t s);
+void launch_tile_ranges(int64_t L, const uint64_t* keys, uint2* ranges, int num_tiles, hipStream_t s);
+
+bool launch_render_fwd(const RenderArgs& a, hipStream_t s);
+bool launch_render_bwd(const RenderBwdArgs& a, hipStream_t s);
+
+void launch_test_wave_reduce(int n, const float* in, float* out, hipStream_t s);
+
+}  // namespace gs

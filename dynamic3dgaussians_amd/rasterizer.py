@@ -1,0 +1,213 @@
+"""Autograd boundary of the MI355X rasterizer -- drop-in for
+DGR/diff_gaussian_rasterization/__init__.py (DGR = submodules_fsgs/
+diff-gaussian-rasterization-confidence).
+
+Same public names (GaussianRasterizationSettings, GaussianRasterizer,
+rasterize_gaussians, _RasterizeGaussians), same argument meaning, same
+debug-snapshot and error behaviour, as a SUPERSET of the four caller API
+generations found in Dynamic3DGaussians:
+
+  G1 no label, no semantic_feature -> (color, radii, depth)        train.py:142
+  G2 label,    no semantic_feature -> (color, radii, depth, alpha)  cvpr_dyn.py:241
+  G3 label,    semantic_feature    -> (color, radii, feature_map, depth, alpha)
+                                      (the vendored API, __init__.py:108)
+  G4 no label, semantic_feature    -> (color, feature_map, radii, depth)
+                                      gaussian_renderer/__init__.py:93-102
+
+`rasterize_gaussians` / `_RasterizeGaussians` always return the G3 5-tuple,
+like the reference.  Numerics follow settings.compat (default: the module
+default, "reference"); see DESIGN.md "Quirks".
+"""
+from __future__ import annotations
+
+from typing import NamedTuple, Optional
+
+import torch
+import torch.nn as nn
+
+from . import _C
+
+
+def cpu_deep_copy_tuple(input_tuple):
+    """__init__.py:17-19: CPU copies of the argument tuple for debug snapshots."""
+    return tuple(item.cpu().clone() if isinstance(item, torch.Tensor) else item
+                 for item in input_tuple)
+
+
+def rasterize_gaussians(means3D, means2D, sh, colors_precomp, semantic_feature, opacities, scales,
+                        rotations, cov3Ds_precomp, raster_settings, label=None):
+    """__init__.py:21-46."""
+    return _RasterizeGaussians.apply(means3D, means2D, sh, colors_precomp, semantic_feature,
+                                     opacities, scales, rotations, cov3Ds_precomp, raster_settings,
+                                     label)
+
+
+def _empty_like_none(t):
+    return t if t is not None else torch.Tensor([])
+
+
+def _compat_of(settings) -> str:
+    mode = getattr(settings, "compat", None)
+    return _C.get_default_compat() if mode is None else mode
+
+
+def _principal_point(settings):
+    cx = settings.c_x if settings.c_x is not None else settings.image_width / 2.0
+    cy = settings.c_y if settings.c_y is not None else settings.image_height / 2.0
+    return float(cx), float(cy)
+
+
+class _RasterizeGaussians(torch.autograd.Function):
+    """__init__.py:48-174."""
+
+    @staticmethod
+    def forward(ctx, means3D, means2D, sh, colors_precomp, semantic_feature, opacities, scales,
+                rotations, cov3Ds_precomp, raster_settings, label):
+        compat = _compat_of(raster_settings)
+        c_x, c_y = _principal_point(raster_settings)
+        for name in ("bg", "viewmatrix", "projmatrix", "campos"):
+            if getattr(raster_settings, name) is None:
+                raise TypeError(f"GaussianRasterizationSettings.{name} is required")
+        sh = _empty_like_none(sh)
+        colors_precomp = _empty_like_none(colors_precomp)
+        scales = _empty_like_none(scales)
+        rotations = _empty_like_none(rotations)
+        cov3Ds_precomp = _empty_like_none(cov3Ds_precomp)
+        # Argument order of the C++ binding (__init__.py:67-90)
+        args = (raster_settings.bg, means3D, colors_precomp, semantic_feature, opacities, scales,
+                rotations, raster_settings.scale_modifier, cov3Ds_precomp,
+                raster_settings.viewmatrix, raster_settings.projmatrix, c_x, c_y,
+                raster_settings.tanfovx, raster_settings.tanfovy, raster_settings.image_height,
+                raster_settings.image_width, sh, raster_settings.sh_degree, raster_settings.campos,
+                raster_settings.prefiltered, raster_settings.debug)
+        if raster_settings.debug:
+            cpu_args = cpu_deep_copy_tuple(args)
+            try:
+                out = _C.rasterize_gaussians(*args, compat=compat)
+            except Exception as ex:
+                torch.save(cpu_args, "snapshot_fw.dump")
+                print("\nAn error occured in forward. Please forward snapshot_fw.dump for debugging.")
+                raise ex
+        else:
+            out = _C.rasterize_gaussians(*args, compat=compat)
+        num_rendered, color, feature_map, depth, alpha, radii, geomBuffer, binningBuffer, imgBuffer = out
+
+        ctx.raster_settings = raster_settings
+        ctx.num_rendered = num_rendered
+        ctx.compat = compat
+        ctx.c_xy = (c_x, c_y)
+        ctx.sem_shape = None if semantic_feature is None else tuple(semantic_feature.shape)
+        ctx.save_for_backward(colors_precomp, semantic_feature, means3D, scales, rotations,
+                              cov3Ds_precomp, radii, sh, geomBuffer, binningBuffer, imgBuffer, alpha,
+                              label if isinstance(label, torch.Tensor) else None)
+        ctx.mark_non_differentiable(radii)
+        return color, radii, feature_map, depth, alpha
+
+    @staticmethod
+    def backward(ctx, grad_color, grad_radii, grad_out_feature, grad_depth, grad_alpha):
+        num_rendered = ctx.num_rendered
+        rs = ctx.raster_settings
+        (colors_precomp, semantic_feature, means3D, scales, rotations, cov3Ds_precomp, radii, sh,
+         geomBuffer, binningBuffer, imgBuffer, alpha, label) = ctx.saved_tensors
+        c_x, c_y = ctx.c_xy
+        if ctx.compat == "reference":
+            # Q2: the reference passes tanfovx, tanfovy, c_x, c_y into the
+            # binding's (c_x, c_y, tan_fovx, tan_fovy) slots (__init__.py:130-133
+            # vs rasterize_points.cu:141-144); reproduced in "reference" mode.
+            cam4 = (rs.tanfovx, rs.tanfovy, c_x, c_y)
+        else:
+            cam4 = (c_x, c_y, rs.tanfovx, rs.tanfovy)
+        args = (rs.bg, means3D, radii, colors_precomp, semantic_feature, scales, rotations,
+                rs.scale_modifier, cov3Ds_precomp, rs.viewmatrix, rs.projmatrix, *cam4,
+                grad_color, grad_out_feature, grad_depth, grad_alpha, sh, rs.sh_degree, rs.campos,
+                geomBuffer, num_rendered, binningBuffer, imgBuffer, alpha, rs.debug)
+        if rs.debug:
+            cpu_args = cpu_deep_copy_tuple(args)
+            try:
+                grads = _C.rasterize_gaussians_backward(*args, compat=ctx.compat)
+            except Exception as ex:
+                torch.save(cpu_args, "snapshot_bw.dump")
+                print("\nAn error occured in backward. Writing snapshot_bw.dump for debugging.\n")
+                raise ex
+        else:
+            grads = _C.rasterize_gaussians_backward(*args, compat=ctx.compat)
+        (grad_means2D, grad_colors_precomp, grad_semantic_feature, grad_opacities, grad_means3D,
+         grad_cov3Ds_precomp, grad_sh, grad_scales, grad_rotations) = grads
+        if ctx.sem_shape is not None:
+            grad_semantic_feature = grad_semantic_feature.reshape(ctx.sem_shape)
+        else:
+            grad_semantic_feature = None
+        if label is not None:
+            # __init__.py:159-173: every Gaussian-parameter gradient except
+            # means2D and the semantic feature is masked by `label` (Q12).
+            lab = label.unsqueeze(1)
+            grad_means3D = grad_means3D * lab
+            grad_sh = grad_sh * lab[..., None]
+            grad_colors_precomp = grad_colors_precomp * lab
+            grad_opacities = grad_opacities * lab
+            grad_scales = grad_scales * lab
+            grad_rotations = grad_rotations * lab
+            grad_cov3Ds_precomp = grad_cov3Ds_precomp * lab
+        return (grad_means3D, grad_means2D, grad_sh, grad_colors_precomp, grad_semantic_feature,
+                grad_opacities, grad_scales, grad_rotations, grad_cov3Ds_precomp, None, None)
+
+
+class GaussianRasterizationSettings(NamedTuple):
+    """__init__.py:176-192, as a superset: c_x / c_y default to the image
+    centre (G4 callers omit them), `confidence` is accepted and unused like
+    the reference, and `compat` selects reference/fixed numerics."""
+    image_height: int
+    image_width: int
+    tanfovx: float
+    tanfovy: float
+    c_x: Optional[float] = None
+    c_y: Optional[float] = None
+    bg: Optional[torch.Tensor] = None
+    scale_modifier: float = 1.0
+    viewmatrix: Optional[torch.Tensor] = None
+    projmatrix: Optional[torch.Tensor] = None
+    sh_degree: int = 0
+    campos: Optional[torch.Tensor] = None
+    prefiltered: bool = False
+    debug: bool = False
+    confidence: Optional[torch.Tensor] = None
+    compat: Optional[str] = None
+
+
+_UNSET = object()
+
+
+class GaussianRasterizer(nn.Module):
+    """__init__.py:194-245 with the caller-generation arity dispatch."""
+
+    def __init__(self, raster_settings):
+        super().__init__()
+        self.raster_settings = raster_settings
+
+    def markVisible(self, positions):
+        with torch.no_grad():
+            rs = self.raster_settings
+            return _C.mark_visible(positions, rs.viewmatrix, rs.projmatrix)
+
+    def forward(self, means3D, means2D, opacities=None, shs=None, semantic_feature=None,
+                colors_precomp=None, scales=None, rotations=None, cov3D_precomp=None, label=_UNSET):
+        rs = self.raster_settings
+        if (shs is None and colors_precomp is None) or (shs is not None and colors_precomp is not None):
+            raise Exception('Please provide excatly one of either SHs or precomputed colors!')
+        if ((scales is None or rotations is None) and cov3D_precomp is None) or \
+                ((scales is not None or rotations is not None) and cov3D_precomp is not None):
+            raise Exception('Please provide exactly one of either scale/rotation pair or '
+                            'precomputed 3D covariance!')
+        has_label = label is not _UNSET
+        lab = label if (has_label and isinstance(label, torch.Tensor)) else None
+        color, radii, feature_map, depth, alpha = rasterize_gaussians(
+            means3D, means2D, shs, colors_precomp, semantic_feature, opacities, scales, rotations,
+            cov3D_precomp, rs, lab)
+        has_sem = semantic_feature is not None
+        if has_label and has_sem:      # G3 (vendored API)
+            return color, radii, feature_map, depth, alpha
+        if has_label:                  # G2
+            return color, radii, depth, alpha
+        if has_sem:                    # G4 (feature-3DGS style)
+            return color, feature_map, radii, depth
+        return color, radii, depth     # G1 (upstream "w-depth" API)

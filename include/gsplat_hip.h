@@ -1,0 +1,155 @@
+/*
+ * gsplat_hip.h -- C ABI of the MI355X-native differentiable Gaussian
+ * rasterizer (libgsplat_hip.so, hand-written HIP kernels for gfx950).
+ *
+ * This is the drop-in boundary for the reference's pybind module
+ * `diff_gaussian_rasterization._C` (DGR/ext.cpp:15-19), where
+ * DGR = submodules_fsgs/diff-gaussian-rasterization-confidence and
+ * CR = DGR/cuda_rasterizer.  Each entry point names the reference interface
+ * it replaces.  No torch types cross this boundary: plain device pointers,
+ * sizes, camera scalars and an explicit hipStream_t.
+ *
+ * Conventions (all entry points):
+ *  - Return 0 on success, <0 on an invalid argument, >0 = a hipError_t code.
+ *    The message is in gs_last_error() (thread-local).
+ *  - The library never allocates device memory: the caller supplies the three
+ *    opaque state buffers (sized by gs_*_buffer_bytes) and the backward
+ *    scratch, normally from torch's caching allocator.
+ *  - "Absent" optional inputs are NULL pointers (the reference passes empty
+ *    tensors whose data_ptr is null, DGR/diff_gaussian_rasterization/
+ *    __init__.py:220-230).
+ *  - Camera scalars are in the reference's C++ positional semantics
+ *    (DGR/rasterize_points.h); the Python layer decides what it passes.
+ *  - All work is enqueued on `stream`; gs_forward_plan performs the one
+ *    device->host read the reference also performs (num_rendered,
+ *    CR/rasterizer_impl.cu:287).
+ */
+#ifndef GSPLAT_HIP_H
+#define GSPLAT_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GS_ABI_VERSION 1
+
+/* compat modes: numerics of the as-shipped reference vs corrected ones */
+#define GS_COMPAT_REFERENCE 0
+#define GS_COMPAT_FIXED 1
+
+typedef void *gs_stream_t; /* a hipStream_t (NULL = legacy default stream) */
+
+/* Per-Gaussian inputs (device pointers, fp32, row-major/contiguous).
+ * Mirrors the tensor arguments of RasterizeGaussiansCUDA
+ * (DGR/rasterize_points.cu:36-58). */
+typedef struct gs_gaussians {
+  int32_t P;                      /* number of Gaussians */
+  int32_t D;                      /* active SH degree (0..3) */
+  int32_t M;                      /* SH coefficients per Gaussian (shs is P x M x 3) */
+  int32_t F;                      /* semantic feature channels (0 = none) */
+  const float *means3D;           /* P x 3 */
+  const float *shs;               /* P x M x 3 or NULL */
+  const float *colors_precomp;    /* P x 3 or NULL */
+  const float *semantic_feature;  /* P x F or NULL */
+  const float *opacities;         /* P */
+  const float *scales;            /* P x 3 or NULL */
+  const float *rotations;         /* P x 4 (r,x,y,z) or NULL */
+  const float *cov3D_precomp;     /* P x 6 or NULL */
+  float scale_modifier;
+  int32_t _pad;
+} gs_gaussians;
+
+/* Camera / raster settings (GaussianRasterizationSettings,
+ * DGR/diff_gaussian_rasterization/__init__.py:176-192). */
+typedef struct gs_camera {
+  const float *viewmatrix; /* 16 floats, column-major (device) */
+  const float *projmatrix; /* 16 floats, column-major (device) */
+  const float *campos;     /* 3 floats (device) */
+  const float *background; /* 3 floats (device) */
+  float c_x, c_y, tan_fovx, tan_fovy;
+  int32_t image_width, image_height;
+} gs_camera;
+
+int gs_version(void);
+const char *gs_last_error(void);
+
+/* Opaque state buffer sizes (replace GeometryState/BinningState/ImageState
+ * ::fromChunk + required<>, CR/rasterizer_impl.cu:155-194,
+ * CR/rasterizer_impl.h:67-73). */
+size_t gs_geom_buffer_bytes(int64_t P);
+size_t gs_binning_buffer_bytes(int64_t num_rendered);
+size_t gs_image_buffer_bytes(int32_t W, int32_t H);
+size_t gs_backward_scratch_bytes(int64_t P, int32_t F);
+
+/* Forward, phase 1 -- replaces CR/rasterizer_impl.cu:198-287 (preprocess,
+ * inclusive scan, D2H of num_rendered).  Writes radii[P] and *num_rendered. */
+int gs_forward_plan(const gs_gaussians *g, const gs_camera *cam, int prefiltered,
+                    int debug, int compat, void *geom_buffer, int32_t *radii,
+                    int64_t *num_rendered, gs_stream_t stream);
+
+/* Forward, phase 2 -- replaces CR/rasterizer_impl.cu:289-345 (duplicateWithKeys,
+ * radix sort, identifyTileRanges, render).  Outputs are planar CHW:
+ * out_color 3xHxW, out_feature FxHxW (may be NULL if F==0), out_depth HxW,
+ * out_alpha HxW.  Every output pixel is written. */
+int gs_forward_render(const gs_gaussians *g, const gs_camera *cam, int debug,
+                      int compat, void *geom_buffer, void *binning_buffer,
+                      void *image_buffer, int64_t num_rendered, const int32_t *radii,
+                      float *out_color, float *out_feature, float *out_depth,
+                      float *out_alpha, gs_stream_t stream);
+
+/* Backward -- replaces RasterizeGaussiansBackwardCUDA / Rasterizer::backward
+ * (DGR/rasterize_points.cu:128-225, CR/rasterizer_impl.cu:350-467).
+ * Every element of every gradient output is written (no pre-zeroing needed).
+ * dL_dmeans2D P x 3, dL_dcolors P x 3, dL_dsemantic P x F, dL_dopacity P,
+ * dL_dmeans3D P x 3, dL_dcov3D P x 6, dL_dsh P x M x 3, dL_dscales P x 3,
+ * dL_drotations P x 4. */
+int gs_backward(const gs_gaussians *g, const gs_camera *cam, const int32_t *radii,
+                int debug, int compat, const void *geom_buffer,
+                const void *binning_buffer, const void *image_buffer,
+                int64_t num_rendered, const float *alphas,
+                const float *dL_dout_color, const float *dL_dout_feature,
+                const float *dL_dout_depth, const float *dL_dout_alpha,
+                void *scratch, float *dL_dmeans2D, float *dL_dcolors,
+                float *dL_dsemantic, float *dL_dopacity, float *dL_dmeans3D,
+                float *dL_dcov3D, float *dL_dsh, float *dL_dscales,
+                float *dL_drotations, gs_stream_t stream);
+
+/* markVisible -- replaces DGR/rasterize_points.cu:227-246 and
+ * CR/rasterizer_impl.cu:141-153 (checkFrustum).  present[P] is 0/1 bytes. */
+int gs_mark_visible(int64_t P, const float *means3D, const float *viewmatrix,
+                    const float *projmatrix, uint8_t *present, gs_stream_t stream);
+
+/* ---- inspection entry points (tests and benchmarks; no reference analogue) */
+
+/* Copy the internal per-stage state of the last forward into host-visible
+ * device arrays for stage-level parity checks:
+ *   means2D P x 2, depths P, conic_opacity P x 4, rgb P x 3, tiles_touched P,
+ *   point_list num_rendered, ranges (tiles x 2), n_contrib H x W.
+ * Any output pointer may be NULL. */
+int gs_debug_export(int64_t P, int32_t W, int32_t H, const void *geom_buffer,
+                    const void *binning_buffer, const void *image_buffer,
+                    int64_t num_rendered, float *means2D, float *depths,
+                    float *conic_opacity, float *rgb, uint32_t *tiles_touched,
+                    uint32_t *point_list, uint32_t *ranges, uint32_t *n_contrib,
+                    gs_stream_t stream);
+
+/* Stable LSD radix sort of (u64 key, u32 value) pairs on bits [0, end_bit)
+ * -- the standalone form of the binning sort (cub::DeviceRadixSort::SortPairs
+ * at CR/rasterizer_impl.cu:309).  keys/vals are sorted in place; scratch is
+ * gs_sort_scratch_bytes(n) bytes. */
+size_t gs_sort_scratch_bytes(int64_t n);
+int gs_sort_pairs(int64_t n, uint64_t *keys, uint32_t *vals, int end_bit,
+                  void *scratch, gs_stream_t stream);
+
+/* Self-test of the wave64 transposed reduction used by the backward blend:
+ * in[n_comp][64] -> out[n_comp] (sums over the 64 lanes).  n_comp <= 64. */
+int gs_test_wave_reduce(int n_comp, const float *in, float *out, gs_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GSPLAT_HIP_H */

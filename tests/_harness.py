@@ -1,0 +1,166 @@
+"""Shared test harness: run the HIP rasterizer and the CPU oracle on the same
+seeded inputs and compare.  The oracle is used here only as the checker."""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from dynamic3dgaussians_amd import _C, _lib
+from dynamic3dgaussians_amd.camera import camera_rig, intrinsics, look_at_w2c, setup_camera
+from dynamic3dgaussians_amd.scene import make_gaussians
+from oracle import oracle as O
+
+DEV = "cuda"
+
+
+def scene(P=2000, F=0, sh_degree=0, seed=0, W=128, H=96, cam_index=0, use_sh=False,
+          use_cov=False, scale_mult=3.0, n_cams=27, bg=(0.0, 0.0, 0.0), cx=None, cy=None):
+    """Inputs for one camera as numpy-friendly CPU tensors + camera params."""
+    g = make_gaussians(P, F=F, sh_degree=sh_degree, seed=seed, scale_mult=scale_mult)
+    if cx is None and cy is None:
+        cam = camera_rig(n_cams, W, H)[cam_index]
+    else:
+        eye = np.array([0.3, -1.2, 2.2]) * 1.0
+        cam = setup_camera(W, H, intrinsics(W, H, 60.0, cx=cx, cy=cy), look_at_w2c(eye))
+    inputs = dict(
+        bg=torch.tensor(bg, dtype=torch.float32),
+        means3D=g["means3D"],
+        colors=None if use_sh else g["colors"],
+        semantic_feature=g.get("semantic_feature"),
+        opacity=g["opacities"],
+        scales=None if use_cov else g["scales"],
+        rotations=None if use_cov else g["rotations"],
+        scale_modifier=1.0,
+        cov3D_precomp=None,
+        viewmatrix=torch.from_numpy(cam.viewmatrix.copy()),
+        projmatrix=torch.from_numpy(cam.projmatrix.copy()),
+        c_x=cam.c_x, c_y=cam.c_y, tan_fovx=cam.tanfovx, tan_fovy=cam.tanfovy,
+        image_height=H, image_width=W,
+        sh=g["shs"][:, : (sh_degree + 1) ** 2].contiguous() if use_sh else None,
+        degree=sh_degree,
+        campos=torch.from_numpy(cam.campos.copy()),
+    )
+    if use_cov:
+        # Sigma = (S R)^T (S R) computed in float64, handed over precomputed
+        q = torch.nn.functional.normalize(g["rotations"].double(), dim=1)
+        r, x, y, z = q.unbind(1)
+        R = torch.stack([
+            torch.stack([1 - 2 * (y * y + z * z), 2 * (x * y - r * z), 2 * (x * z + r * y)], 1),
+            torch.stack([2 * (x * y + r * z), 1 - 2 * (x * x + z * z), 2 * (y * z - r * x)], 1),
+            torch.stack([2 * (x * z - r * y), 2 * (y * z + r * x), 1 - 2 * (x * x + y * y)], 1)], 1)
+        M = torch.diag_embed(g["scales"].double()) @ R
+        S = M.transpose(1, 2) @ M
+        inputs["cov3D_precomp"] = torch.stack([S[:, 0, 0], S[:, 0, 1], S[:, 0, 2], S[:, 1, 1],
+                                               S[:, 1, 2], S[:, 2, 2]], 1).float().contiguous()
+    return inputs
+
+
+FWD_ORDER = ["bg", "means3D", "colors", "semantic_feature", "opacity", "scales", "rotations",
+             "scale_modifier", "cov3D_precomp", "viewmatrix", "projmatrix", "c_x", "c_y",
+             "tan_fovx", "tan_fovy", "image_height", "image_width", "sh", "degree", "campos"]
+
+
+def _to(x, dev):
+    if isinstance(x, torch.Tensor):
+        return x.to(dev)
+    if x is None:
+        return torch.Tensor([]).to(dev) if dev != "cpu" else None
+    return x
+
+
+def fwd_args(inp, dev):
+    return [_to(inp[k], dev) for k in FWD_ORDER] + [False, False]
+
+
+def gpu_forward(inp, compat="reference"):
+    out = _C.rasterize_gaussians(*fwd_args(inp, DEV), compat=compat)
+    torch.cuda.synchronize()
+    return out
+
+
+def oracle_forward(inp, compat="reference"):
+    args = [inp[k] for k in FWD_ORDER]
+    return O.rasterize_gaussians(*args, prefiltered=False, debug=False, compat=compat)
+
+
+def upstream_grads(H, W, F, seed=1, alpha_grad=True):
+    g = torch.Generator().manual_seed(seed)
+    dc = torch.randn(3, H, W, generator=g)
+    df = torch.randn(F, H, W, generator=g) if F else torch.zeros(0, H, W)
+    dd = torch.randn(1, H, W, generator=g) * 0.1
+    da = torch.randn(1, H, W, generator=g) if alpha_grad else torch.zeros(1, H, W)
+    return dc, df, dd, da
+
+
+def bwd_cam4(inp, swap):
+    """Camera scalars in the binding's (c_x, c_y, tan_fovx, tan_fovy) slots;
+    `swap` reproduces the reference Python wrapper's ordering (Q2)."""
+    if swap:
+        return inp["tan_fovx"], inp["tan_fovy"], inp["c_x"], inp["c_y"]
+    return inp["c_x"], inp["c_y"], inp["tan_fovx"], inp["tan_fovy"]
+
+
+def gpu_backward(inp, fwd, grads, compat="reference", swap=None):
+    if swap is None:
+        swap = compat == "reference"
+    num_rendered, color, feat, depth, alpha, radii, geom, binning, img = fwd
+    dc, df, dd, da = [t.to(DEV) for t in grads]
+    d = lambda k: _to(inp[k], DEV)  # noqa: E731
+    out = _C.rasterize_gaussians_backward(
+        d("bg"), d("means3D"), radii, d("colors"), d("semantic_feature"), d("scales"),
+        d("rotations"), inp["scale_modifier"], d("cov3D_precomp"), d("viewmatrix"),
+        d("projmatrix"), *bwd_cam4(inp, swap), dc, df, dd, da, d("sh"), inp["degree"],
+        d("campos"), geom, num_rendered, binning, img, alpha, False, compat=compat)
+    torch.cuda.synchronize()
+    return [t.cpu().numpy() for t in out]
+
+
+def oracle_backward(inp, ofwd, grads, compat="reference", swap=None):
+    if swap is None:
+        swap = compat == "reference"
+    L, color, feat, depth, alpha, radii, st = ofwd
+    dc, df, dd, da = [t.numpy() for t in grads]
+    return O.rasterize_gaussians_backward(
+        inp["bg"], inp["means3D"], radii, inp["colors"], inp["semantic_feature"], inp["scales"],
+        inp["rotations"], inp["scale_modifier"], inp["cov3D_precomp"], inp["viewmatrix"],
+        inp["projmatrix"], *bwd_cam4(inp, swap), dc, df, dd, da, inp["sh"], inp["degree"],
+        inp["campos"], st, L, None, None, alpha, compat=compat)
+
+
+def export_state(P, W, H, fwd):
+    """Per-stage GPU state via gs_debug_export (for stage-level parity)."""
+    L_ = _lib.load()
+    num_rendered, color, feat, depth, alpha, radii, geom, binning, img = fwd
+    tiles = ((W + 15) // 16) * ((H + 15) // 16)
+    f = lambda *s: torch.empty(*s, dtype=torch.float32, device=DEV)  # noqa: E731
+    u = lambda *s: torch.empty(*s, dtype=torch.int32, device=DEV)  # noqa: E731
+    st = dict(means2D=f(P, 2), depths=f(P), conic_opacity=f(P, 4), rgb=f(P, 3), tiles=u(P),
+              point_list=u(max(num_rendered, 1)), ranges=u(tiles, 2), n_contrib=u(H * W))
+    s = torch.cuda.current_stream().cuda_stream
+    _lib.check(L_.gs_debug_export(P, W, H, geom.data_ptr(), binning.data_ptr() if binning.numel() else None,
+                                  img.data_ptr(), num_rendered, st["means2D"].data_ptr(),
+                                  st["depths"].data_ptr(), st["conic_opacity"].data_ptr(),
+                                  st["rgb"].data_ptr(), st["tiles"].data_ptr(),
+                                  st["point_list"].data_ptr(), st["ranges"].data_ptr(),
+                                  st["n_contrib"].data_ptr(), s), "debug export")
+    torch.cuda.synchronize()
+    out = {k: v.cpu().numpy() for k, v in st.items()}
+    out["point_list"] = out["point_list"][:num_rendered].view(np.uint32)
+    out["tiles"] = out["tiles"].view(np.uint32)
+    out["ranges"] = out["ranges"].view(np.uint32).reshape(-1)
+    out["n_contrib"] = out["n_contrib"].view(np.uint32)
+    return out
+
+
+def psnr(a, b, peak=1.0):
+    mse = float(np.mean((np.asarray(a, np.float64) - np.asarray(b, np.float64)) ** 2))
+    return float("inf") if mse == 0 else 10 * np.log10(peak * peak / mse)
+
+
+def rel_l2(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    den = np.linalg.norm(b)
+    return float(np.linalg.norm(a - b) / den) if den > 0 else float(np.linalg.norm(a - b))

@@ -1,0 +1,232 @@
+"""GPU parity: the HIP rasterizer (through the C ABI) against the CPU oracle.
+
+Tolerances (DESIGN.md "Parity"):
+  * integer/index work (tile counts, sorted point lists, tile ranges, radii,
+    the radix sort, the wave reduction on integer data): bit-exact;
+  * preprocess floats (means2D, depths, conics, SH colours): bit-exact -- both
+    sides are strict IEEE fp32 in the same operation order;
+  * rendered images: PSNR(HIP vs oracle) >= 80 dB, >= 99.9 % of pixels within
+    1e-4 absolute, and n_contrib identical for >= 99.9 % of pixels (the blend
+    uses FMA contraction and a different expf, so an alpha-threshold decision
+    may flip on a rare pixel);
+  * gradients: relative L2 over all Gaussians <= 1e-3 per output tensor.
+"""
+import numpy as np
+import pytest
+import torch
+
+from tests import _harness as H
+from dynamic3dgaussians_amd import _lib
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _cmp_forward(inp, compat, F):
+    g = H.gpu_forward(inp, compat)
+    o = H.oracle_forward(inp, compat)
+    Lg, cg, fg, dg, ag, rg = g[0], g[1].cpu().numpy(), g[2].cpu().numpy(), g[3].cpu().numpy(), \
+        g[4].cpu().numpy(), g[5].cpu().numpy()
+    Lo, co, fo, do, ao, ro, st = o
+    assert Lg == Lo, "num_rendered differs"
+    np.testing.assert_array_equal(rg, ro)
+    assert H.psnr(cg, co) >= 80.0
+    assert np.mean(np.abs(cg - co) <= 1e-4) >= 0.999
+    assert np.mean(np.abs(dg - do) <= 1e-4 * max(1.0, np.abs(do).max())) >= 0.999
+    if F:
+        assert fg.shape == fo.shape
+        assert np.mean(np.abs(fg - fo) <= 1e-4 * max(1.0, np.abs(fo).max())) >= 0.999
+    assert np.mean(np.abs(ag - ao) <= 1e-4) >= 0.999
+    return g, o
+
+
+# ---------------------------------------------------------------- primitives
+
+@pytest.mark.parametrize("n", [1, 2, 3, 10, 13, 18, 26, 42, 64])
+def test_wave_transposed_reduce(n):
+    L = _lib.load()
+    rng = np.random.default_rng(n)
+    x = rng.integers(-1000, 1000, size=(n, 64)).astype(np.float32)  # exact sums
+    xin = torch.from_numpy(x).cuda()
+    out = torch.full((n,), np.nan, device="cuda")
+    _lib.check(L.gs_test_wave_reduce(n, xin.data_ptr(), out.data_ptr(),
+                                     torch.cuda.current_stream().cuda_stream), "wave reduce")
+    np.testing.assert_array_equal(out.cpu().numpy(), x.sum(1))
+
+
+@pytest.mark.parametrize("n,end_bit", [(0, 40), (1, 40), (777, 40), (4096, 44), (100_000, 44),
+                                       (1_000_003, 45), (50_000, 13)])
+def test_radix_sort_stable(n, end_bit):
+    """Bit-exact against numpy's stable argsort on the sorted bit range,
+    with heavy key duplication (stability matters)."""
+    L = _lib.load()
+    rng = np.random.default_rng(n + end_bit)
+    tiles = rng.integers(0, 1 << max(end_bit - 32, 1), size=n, dtype=np.uint64)
+    depth = rng.integers(0x3f800000, 0x3f800000 + 5000, size=n, dtype=np.uint64)
+    keys = (tiles << np.uint64(32)) | depth if end_bit > 32 else depth & np.uint64((1 << end_bit) - 1)
+    vals = np.arange(n, dtype=np.uint32)
+    kd = torch.from_numpy(keys.view(np.int64).copy()).cuda()
+    vd = torch.from_numpy(vals.view(np.int32).copy()).cuda()
+    scratch = torch.empty(max(L.gs_sort_scratch_bytes(n), 1), dtype=torch.uint8, device="cuda")
+    _lib.check(L.gs_sort_pairs(n, kd.data_ptr(), vd.data_ptr(), end_bit, scratch.data_ptr(),
+                               torch.cuda.current_stream().cuda_stream), "sort")
+    torch.cuda.synchronize()
+    masked = keys & np.uint64((1 << end_bit) - 1) if end_bit < 64 else keys
+    order = np.argsort(masked, kind="stable")
+    np.testing.assert_array_equal(vd.cpu().numpy().view(np.uint32), vals[order])
+    np.testing.assert_array_equal(kd.cpu().numpy().view(np.uint64), keys[order])
+
+
+# ---------------------------------------------------------------- stages
+
+@pytest.mark.parametrize("kw", [
+    dict(), dict(use_sh=True, sh_degree=1), dict(use_sh=True, sh_degree=2),
+    dict(use_sh=True, sh_degree=3), dict(use_cov=True), dict(W=100, H=75, cam_index=5),
+    dict(cx=40.0, cy=70.0, W=128, H=96)])
+def test_preprocess_and_binning_bitexact(kw):
+    inp = H.scene(P=3000, **kw)
+    g = H.gpu_forward(inp)
+    o = H.oracle_forward(inp)
+    st_o = o[6]
+    P, W, Hh = inp["means3D"].shape[0], inp["image_width"], inp["image_height"]
+    st_g = H.export_state(P, W, Hh, g)
+    vis = st_o.radii > 0
+    np.testing.assert_array_equal(g[5].cpu().numpy(), st_o.radii)
+    np.testing.assert_array_equal(st_g["tiles"], st_o.tiles_touched)
+    np.testing.assert_array_equal(st_g["means2D"][vis], st_o.means2D[vis])
+    np.testing.assert_array_equal(st_g["depths"][vis], st_o.depths[vis])
+    np.testing.assert_array_equal(st_g["conic_opacity"][vis], st_o.conic_opacity[vis])
+    if kw.get("use_sh"):
+        np.testing.assert_array_equal(st_g["rgb"][vis], st_o.rgb[vis])
+    # binning (integer work) must be bit-exact
+    assert g[0] == o[0]
+    np.testing.assert_array_equal(st_g["point_list"], st_o.point_list)
+    np.testing.assert_array_equal(st_g["ranges"], st_o.ranges)
+    assert np.mean(st_g["n_contrib"] == st_o.n_contrib) >= 0.999
+
+
+# ---------------------------------------------------------------- forward
+
+@pytest.mark.parametrize("compat", ["reference", "fixed"])
+@pytest.mark.parametrize("kw", [
+    dict(), dict(F=32), dict(F=8, use_sh=True, sh_degree=3), dict(F=16, use_cov=True),
+    dict(F=64, W=80, H=48), dict(F=32, bg=(0.2, 0.5, 0.9)), dict(W=100, H=75, P=4000),
+    dict(F=32, cx=30.0, cy=60.0)])
+def test_forward_parity(compat, kw):
+    _cmp_forward(H.scene(**kw), compat, kw.get("F", 0))
+
+
+def test_forward_padded_feature_width():
+    """F = 5 is zero-padded to the 8-wide kernel; outputs keep 5 channels."""
+    inp = H.scene(P=1500, F=5)
+    g = H.gpu_forward(inp)
+    o = H.oracle_forward(inp)
+    assert g[2].shape == (5, 96, 128)
+    np.testing.assert_allclose(g[2].cpu().numpy(), o[2], atol=2e-4, rtol=0)
+
+
+# ---------------------------------------------------------------- backward
+
+GRAD_NAMES = ["dmeans2D", "dcolors", "dsemantic", "dopacity", "dmeans3D", "dcov3D", "dsh",
+              "dscales", "drotations"]
+
+
+@pytest.mark.parametrize("compat", ["reference", "fixed"])
+@pytest.mark.parametrize("kw", [
+    dict(), dict(F=32), dict(F=8, use_sh=True, sh_degree=3), dict(F=16, use_cov=True),
+    dict(F=32, bg=(0.3, 0.1, 0.7)), dict(W=100, H=75, P=4000, use_sh=True, sh_degree=1),
+    dict(F=32, cx=30.0, cy=60.0)])
+def test_backward_parity(compat, kw):
+    inp = H.scene(**kw)
+    F = kw.get("F", 0)
+    g = H.gpu_forward(inp, compat)
+    o = H.oracle_forward(inp, compat)
+    grads = H.upstream_grads(inp["image_height"], inp["image_width"], F)
+    gb = H.gpu_backward(inp, g, grads, compat)
+    ob = H.oracle_backward(inp, o, grads, compat)
+    for name, a, b in zip(GRAD_NAMES, gb, ob):
+        assert a.shape == b.shape, name
+        if b.size == 0 or not np.any(b):
+            assert not np.any(a) or np.abs(a).max() < 1e-6, name
+            continue
+        assert H.rel_l2(a, b) <= 1e-3, (name, H.rel_l2(a, b))
+
+
+def test_backward_reference_swap_matters():
+    """Q2: the reference's swapped camera arguments change dL/dscale a lot;
+    the HIP path follows whichever order it is given, like the oracle."""
+    inp = H.scene(F=0)
+    g = H.gpu_forward(inp)
+    o = H.oracle_forward(inp)
+    grads = H.upstream_grads(96, 128, 0)
+    a = H.gpu_backward(inp, g, grads, "reference", swap=True)
+    b = H.oracle_backward(inp, o, grads, "reference", swap=True)
+    c = H.gpu_backward(inp, g, grads, "reference", swap=False)
+    assert H.rel_l2(a[7], b[7]) <= 1e-3
+    assert H.rel_l2(a[7], c[7]) > 0.1
+
+
+# ---------------------------------------------------------------- edge cases
+
+def test_empty_and_culled():
+    inp = H.scene(P=0)
+    g = H.gpu_forward(inp)
+    assert g[0] == 0 and g[1].abs().sum().item() == 0  # P == 0: no background either
+    inp = H.scene(P=500, bg=(0.25, 0.5, 0.75))
+    fwd = inp["viewmatrix"][:3, 2]  # camera forward axis (row 2 of w2c)
+    inp["means3D"] = (inp["campos"] - 2.0 * fwd).expand(500, 3).contiguous()  # all behind camera
+    g = H.gpu_forward(inp)
+    o = H.oracle_forward(inp)
+    assert g[0] == 0 == o[0]
+    np.testing.assert_array_equal(g[1].cpu().numpy(), o[1])
+    grads = H.upstream_grads(96, 128, 0)
+    gb = H.gpu_backward(inp, g, grads)
+    for a in gb:
+        assert not np.any(a)
+
+
+def test_single_gaussian_known_answer():
+    """Closed form: isotropic s=0.05 at z=2, f=32, 32x32 image:
+    radius 4, centre (15.5, 15.5), conic (1/0.94, 0, 1/0.94)."""
+    from dynamic3dgaussians_amd.camera import setup_camera
+    cam = setup_camera(32, 32, np.array([[32, 0, 16], [0, 32, 16], [0, 0, 1.0]]), np.eye(4))
+    inp = dict(bg=torch.zeros(3), means3D=torch.tensor([[0.0, 0.0, 2.0]]),
+               colors=torch.tensor([[1.0, 0.5, 0.25]]), semantic_feature=None,
+               opacity=torch.tensor([[0.8]]), scales=torch.full((1, 3), 0.05),
+               rotations=torch.tensor([[1.0, 0, 0, 0]]), scale_modifier=1.0, cov3D_precomp=None,
+               viewmatrix=torch.from_numpy(cam.viewmatrix.copy()),
+               projmatrix=torch.from_numpy(cam.projmatrix.copy()), c_x=16.0, c_y=16.0,
+               tan_fovx=cam.tanfovx, tan_fovy=cam.tanfovy, image_height=32, image_width=32,
+               sh=None, degree=0, campos=torch.from_numpy(cam.campos.copy()))
+    g = H.gpu_forward(inp)
+    assert g[5].item() == 4 and g[0] == 4
+    st = H.export_state(1, 32, 32, g)
+    np.testing.assert_allclose(st["means2D"][0], [15.5, 15.5])
+    np.testing.assert_allclose(st["conic_opacity"][0, :3], [1 / 0.94, 0, 1 / 0.94], rtol=1e-6)
+    a = 0.8 * np.exp(-0.5 * (0.25 + 0.25) / 0.94)
+    np.testing.assert_allclose(g[1][:, 15, 15].cpu().numpy(), a * np.array([1, 0.5, 0.25]), rtol=1e-6)
+
+
+def test_huge_gaussian_and_odd_sizes():
+    inp = H.scene(P=50, W=37, H=29, scale_mult=40.0)
+    _cmp_forward(inp, "fixed", 0)
+
+
+def test_mark_visible():
+    from dynamic3dgaussians_amd import _C
+    inp = H.scene(P=5000)
+    m = inp["means3D"].clone()
+    m[::3, 2] += 5.0
+    vis = _C.mark_visible(m.cuda(), inp["viewmatrix"].cuda(), inp["projmatrix"].cuda())
+    ref = O.mark_visible(m, inp["viewmatrix"], inp["projmatrix"])
+    np.testing.assert_array_equal(vis.cpu().numpy(), ref)
+
+
+def test_prefiltered_error():
+    inp = H.scene(P=100)
+    inp["means3D"][0] = inp["campos"] - 2.0 * inp["viewmatrix"][:3, 2]  # behind the camera
+    args = H.fwd_args(inp, "cuda")
+    args[-2] = True  # prefiltered
+    with pytest.raises(_lib.GsplatError, match="prefiltered"):
+        from dynamic3dgaussians_amd import _C
+        _C.rasterize_gaussians(*args)
