@@ -1,0 +1,315 @@
+#!/usr/bin/env python3
+"""Benchmark: rendered Mpix/s of the differentiable Gaussian rasterizer, fwd+bwd.
+
+Workload (BASELINE.json configs[2], the north-star metric's config): a
+Panoptic-sized scene of 300k Gaussians rendered from a 27-camera rig at
+800x800, through the drop-in GaussianRasterizer (G3 call pattern of
+dyn_train.py:244: precomputed colours + 32-channel semantic features + label),
+forward AND backward for every camera, then ONE flat all-reduce of the
+per-Gaussian gradients (N > 1) and an Adam step -- one step of the
+per-timestep training loop.  Data is synthetic (no network): seeded Gaussians
+and cameras (dynamic3dgaussians_amd/scene.py, camera.py).
+
+Scaling is weak: every rank renders its own 27 cameras of a 27*N camera rig
+with the full Gaussian set replicated; value = all ranks' pixels / step time.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+        --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
+
+Prints ONE JSON line (rank 0).  Besides the contract fields it carries
+`roofline` (dominant kernel, live HIP-event timing over the timed region),
+`cpu_baseline` (the CPU oracle on a bounded sample, rank 0 at N=1 only) and
+`psnr_vs_oracle_db` (the rendered image of camera 0 vs the oracle's).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+from dynamic3dgaussians_amd import _lib  # noqa: E402
+from dynamic3dgaussians_amd.camera import camera_rig  # noqa: E402
+from dynamic3dgaussians_amd.distributed import GradBucket  # noqa: E402
+from dynamic3dgaussians_amd.rasterizer import (GaussianRasterizationSettings,  # noqa: E402
+                                               GaussianRasterizer)
+from dynamic3dgaussians_amd.scene import make_gaussians  # noqa: E402
+
+METRIC = "rendered Mpix/s fwd+bwd (1/8 GPU) at 300k Gaussians; PSNR vs ref"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--gaussians", type=int, default=300_000)
+    ap.add_argument("--cams", type=int, default=27, help="cameras per rank per step")
+    ap.add_argument("--width", type=int, default=800)
+    ap.add_argument("--height", type=int, default=800)
+    ap.add_argument("--features", type=int, default=32)
+    ap.add_argument("--compat", default="reference", choices=["reference", "fixed"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--seed", type=int, default=0)
+    return ap.parse_args()
+
+
+def setup_dist(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return world, rank, torch.device("cuda", local if world > 1 else 0)
+
+
+def make_params(args, dev):
+    """Dynamic3DGaussians parameterisation (dyn_train.py:117-129, helpers.py:98-107)."""
+    g = make_gaussians(args.gaussians, F=args.features, seed=args.seed)
+    params = {
+        "means3D": g["means3D"],
+        "rgb_colors": g["colors"],
+        "unnorm_rotations": g["rotations"],
+        "logit_opacities": torch.logit(g["opacities"]),
+        "log_scales": torch.log(g["scales"]),
+    }
+    if args.features:
+        params["semantic_feature"] = g["semantic_feature"]
+    params = {k: v.to(dev).requires_grad_(True) for k, v in params.items()}
+    label = torch.ones(args.gaussians, device=dev)
+    return params, label
+
+
+def params2rendervar(params, label):
+    rv = {
+        "means3D": params["means3D"],
+        "colors_precomp": params["rgb_colors"],
+        "rotations": torch.nn.functional.normalize(params["unnorm_rotations"]),
+        "opacities": torch.sigmoid(params["logit_opacities"]),
+        "scales": torch.exp(params["log_scales"]),
+        "means2D": torch.zeros_like(params["means3D"], requires_grad=True) + 0,
+        "label": label,
+    }
+    if "semantic_feature" in params:
+        rv["semantic_feature"] = params["semantic_feature"]
+    return rv
+
+
+def make_settings(cams, dev, compat):
+    out = []
+    for c in cams:
+        out.append(GaussianRasterizationSettings(
+            image_height=c.H, image_width=c.W, tanfovx=c.tanfovx, tanfovy=c.tanfovy,
+            c_x=c.c_x, c_y=c.c_y, bg=torch.zeros(3, device=dev), scale_modifier=1.0,
+            viewmatrix=torch.from_numpy(c.viewmatrix.copy()).to(dev),
+            projmatrix=torch.from_numpy(c.projmatrix.copy()).to(dev), sh_degree=0,
+            campos=torch.from_numpy(c.campos.copy()).to(dev), prefiltered=False, debug=False,
+            confidence=None, compat=compat))
+    return out
+
+
+def stage_bytes(L, Pv, P, npix, F, C=3):
+    """Algorithmic HBM bytes per launch; K=1 (precomputed colours)."""
+    return {
+        "preprocess": P * (12 + 12 + 16 + 4 + 12) + P * (4 + 8 + 4 + 16 + 4 + 24 + 12 + 3),
+        "scan": 8 * P,
+        "duplicate": 20 * Pv + 12 * L,
+        "sort": 24 * L,  # lower bound: one full pass
+        "ranges": 8 * L + 8 * ((npix + 255) // 256),
+        "render_fwd": L * (4 + 8 + 16 + 4 * C + 4 + 4 * F) + npix * 4 * (C + F + 2 + 1),
+        "render_bwd": L * (4 + 8 + 16 + 4 * C + 4 + 4 * F) + npix * 4 * (C + F + 4 + 1)
+        + Pv * 4 * (3 + 4 + 1 + C + F + 1),
+        "preprocess_bwd": P * (12 + 12 + 16 + 24 + 12 + 12) + P * 4 * (3 + 6 + 3 + 4 + 3),
+    }
+
+
+def load_pmc_traffic(stage):
+    """HBM bytes per launch from a committed rocprofv3 PMC summary, if any
+    (profiles/pmc_traffic.json, written by tools/pmc_traffic.py)."""
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get("bytes_per_launch", {}).get(stage)
+    except Exception:
+        return None
+
+
+def cpu_baseline(args, params, label, cam, settings, dev):
+    """The CPU oracle (plain C restatement, 1 thread) on one camera of the same
+    scene: forward + backward.  Also returns the PSNR of the HIP render of the
+    same camera against the oracle's."""
+    from oracle import oracle as O
+    with torch.no_grad():
+        rv = params2rendervar(params, label)
+        host = {k: v.detach().float().cpu() for k, v in rv.items() if isinstance(v, torch.Tensor)}
+    t0 = time.perf_counter()
+    L, color, feat, depth, alpha, radii, st = O.rasterize_gaussians(
+        np.zeros(3, np.float32), host["means3D"], host["colors_precomp"],
+        host.get("semantic_feature"), host["opacities"], host["scales"], host["rotations"], 1.0,
+        None, cam.viewmatrix, cam.projmatrix, cam.c_x, cam.c_y, cam.tanfovx, cam.tanfovy, cam.H,
+        cam.W, None, 0, cam.campos, compat=args.compat)
+    t1 = time.perf_counter()
+    rng = np.random.default_rng(1)
+    dc = rng.standard_normal((3, cam.H, cam.W), dtype=np.float32)
+    df = rng.standard_normal((args.features, cam.H, cam.W), dtype=np.float32)
+    dd = rng.standard_normal((1, cam.H, cam.W), dtype=np.float32)
+    da = np.zeros((1, cam.H, cam.W), np.float32)
+    cam4 = (cam.tanfovx, cam.tanfovy, cam.c_x, cam.c_y) if args.compat == "reference" else \
+        (cam.c_x, cam.c_y, cam.tanfovx, cam.tanfovy)
+    O.rasterize_gaussians_backward(
+        np.zeros(3, np.float32), host["means3D"], radii, host["colors_precomp"],
+        host.get("semantic_feature"), host["scales"], host["rotations"], 1.0, None, cam.viewmatrix,
+        cam.projmatrix, *cam4, dc, df, dd, da, None, 0, cam.campos, st, L, None, None, alpha,
+        compat=args.compat)
+    t2 = time.perf_counter()
+    # HIP render of the same camera
+    with torch.no_grad():
+        rv = params2rendervar(params, label)
+        out = GaussianRasterizer(settings)(**rv)
+        torch.cuda.synchronize()
+    img = out[0].float().cpu().numpy()
+    mse = float(np.mean((img.astype(np.float64) - color.astype(np.float64)) ** 2))
+    psnr = float("inf") if mse == 0 else 10 * np.log10(1.0 / mse)
+    mpix = cam.W * cam.H / 1e6
+    return {"value": round(mpix / (t2 - t0), 4), "unit": "Mpix/s", "cores": 1, "kind": "port",
+            "sample": f"1 of {args.cams} cameras ({cam.W}x{cam.H}, {args.gaussians} Gaussians, "
+                      f"F={args.features}), fwd {t1 - t0:.2f}s + bwd {t2 - t1:.2f}s, "
+                      "oracle/gs_oracle.c single thread"}, psnr
+
+
+def main():
+    args = parse()
+    world, rank, dev = setup_dist(args)
+    _lib.load()
+    torch.manual_seed(args.seed)
+
+    rig = camera_rig(args.cams * world, args.width, args.height, seed=args.seed)
+    my_cams = rig[rank * args.cams:(rank + 1) * args.cams]
+    settings = make_settings(my_cams, dev, args.compat)
+    params, label = make_params(args, dev)
+    opt = torch.optim.Adam([
+        {"params": [params["means3D"]], "lr": 1.6e-4},
+        {"params": [params["rgb_colors"]], "lr": 2.5e-3},
+        {"params": [params["unnorm_rotations"]], "lr": 1e-3},
+        {"params": [params["logit_opacities"]], "lr": 0.05},
+        {"params": [params["log_scales"]], "lr": 1e-3},
+    ] + ([{"params": [params["semantic_feature"]], "lr": 1e-3}] if args.features else []),
+        lr=0.0, eps=1e-15)
+    bucket = GradBucket(list(params.values()))
+    g = torch.Generator(device=dev).manual_seed(1 + rank)
+    H_, W_ = args.height, args.width
+    up_color = torch.randn(3, H_, W_, device=dev, generator=g)
+    up_depth = torch.randn(1, H_, W_, device=dev, generator=g) * 0.1
+    up_feat = torch.randn(args.features, H_, W_, device=dev, generator=g) if args.features else None
+
+    # per-camera instance counts for the algorithmic byte model
+    inst = []
+    with torch.no_grad():
+        rv = params2rendervar(params, label)
+        for s in settings:
+            from dynamic3dgaussians_amd import _C
+            out = _C.rasterize_gaussians(
+                s.bg, rv["means3D"], rv["colors_precomp"], rv.get("semantic_feature"),
+                rv["opacities"], rv["scales"], rv["rotations"], 1.0, torch.Tensor([]),
+                s.viewmatrix, s.projmatrix, s.c_x, s.c_y, s.tanfovx, s.tanfovy, H_, W_,
+                torch.Tensor([]), 0, s.campos, False, False, compat=args.compat)
+            inst.append((out[0], int((out[5] > 0).sum().item())))
+    del out
+
+    def step():
+        opt.zero_grad(set_to_none=False)
+        rv = params2rendervar(params, label)
+        for s in settings:
+            ras = GaussianRasterizer(s)
+            im, radius, feat, depth, _ = ras(**rv)
+            outs, grads = [im, depth], [up_color, up_depth]
+            if up_feat is not None:
+                outs.append(feat)
+                grads.append(up_feat)
+            torch.autograd.backward(outs, grads, retain_graph=True)
+        bucket.all_reduce()
+        opt.step()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    _lib.timing_enable(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    stages = _lib.timing_read()
+    _lib.timing_enable(False)
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    ms_per_step = elapsed / args.steps * 1e3
+    mpix_total = world * args.cams * W_ * H_ / 1e6
+    value = mpix_total / (ms_per_step / 1e3)
+
+    # roofline of the dominant stage (live HIP-event durations over the timed region)
+    per_cam_bytes = [stage_bytes(L, Pv, args.gaussians, W_ * H_, args.features) for L, Pv in inst]
+    stage_ms = {k: v[0] for k, v in stages.items()}
+    dom = max(stage_ms, key=stage_ms.get)
+    launches = stages[dom][1]
+    alg_bytes_total = sum(b[dom] for b in per_cam_bytes) * args.steps
+    avg_ms = stage_ms[dom] / max(launches, 1)
+    alg_per_launch = alg_bytes_total / max(launches, 1)
+    achieved = alg_per_launch / (avg_ms / 1e3) / 1e9 if avg_ms > 0 else 0.0
+    traffic = load_pmc_traffic(dom)
+    roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic, "kernel": dom, "avg_launch_ms": round(avg_ms, 4),
+                "alg_bytes_per_launch": int(alg_per_launch)}
+
+    result = {
+        "metric": METRIC, "value": round(value, 3), "unit": "Mpix/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic",
+        "config": {"workload": f"{args.gaussians // 1000}k Gaussians x {args.cams} cams/rank x "
+                               f"{W_}x{H_}, F={args.features} semantic channels, colors_precomp; "
+                               "fwd+bwd per camera + grad all-reduce + Adam",
+                   "gaussians": args.gaussians, "cams_per_rank": args.cams, "width": W_,
+                   "height": H_, "feature_channels": args.features, "compat": args.compat,
+                   "parallelism": f"camera-sharded dp{world}"},
+        "roofline": roofline,
+        "stages_ms_per_step": {k: round(v / args.steps, 4) for k, v in stage_ms.items()},
+        "instances_per_cam": int(np.mean([L for L, _ in inst])),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cb, psnr = cpu_baseline(args, params, label, my_cams[0], settings[0], dev)
+        result["cpu_baseline"] = cb
+        result["psnr_vs_oracle_db"] = round(psnr, 2) if np.isfinite(psnr) else "inf"
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

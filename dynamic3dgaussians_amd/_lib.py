@@ -64,7 +64,26 @@ PROTOTYPES = {
     "gs_sort_scratch_bytes": (c_size_t, [c_int64]),
     "gs_sort_pairs": (ctypes.c_int, [c_int64, c_void_p, c_void_p, ctypes.c_int, c_void_p, c_void_p]),
     "gs_test_wave_reduce": (ctypes.c_int, [ctypes.c_int, c_void_p, c_void_p, c_void_p]),
+    "gs_timing_enable": (ctypes.c_int, [ctypes.c_int]),
+    "gs_timing_read": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_int64),
+                                      ctypes.c_int]),
 }
+
+STAGES = ["preprocess", "scan", "duplicate", "sort", "ranges", "render_fwd", "render_bwd",
+          "preprocess_bwd"]
+
+
+def timing_enable(on: bool = True):
+    load().gs_timing_enable(1 if on else 0)
+
+
+def timing_read() -> dict:
+    """{stage: (total_ms, launches)} since the last timing_enable()."""
+    n = len(STAGES)
+    ms = (ctypes.c_double * n)()
+    cnt = (c_int64 * n)()
+    check(load().gs_timing_read(ms, cnt, n), "timing read")
+    return {s: (ms[i], cnt[i]) for i, s in enumerate(STAGES)}
 
 
 class GsplatError(RuntimeError):

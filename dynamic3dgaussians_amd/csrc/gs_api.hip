@@ -9,7 +9,9 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <mutex>
 #include <string>
+#include <vector>
 
 #include "../../include/gsplat_hip.h"
 #include "gs_common.h"
@@ -87,9 +89,73 @@ int check_gaussians(const gs_gaussians* g, const gs_camera* c, bool forward) {
   }
   return 0;
 }
+// ---- optional live kernel timing (bench instrumentation) ------------------
+// When enabled, an event pair is recorded on the launch stream around each
+// timed stage; gs_timing_read() resolves them.  Off by default (zero cost).
+struct TimedEvent {
+  hipEvent_t a, b;
+  int kind;
+};
+std::mutex g_tmu;
+bool g_timing = false;
+std::vector<TimedEvent> g_events;
+std::vector<hipEvent_t> g_pool;
+
+hipEvent_t pool_get() {
+  if (!g_pool.empty()) {
+    hipEvent_t e = g_pool.back();
+    g_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  (void)hipEventCreate(&e);
+  return e;
+}
+
+struct StageTimer {
+  hipStream_t s;
+  int kind;
+  hipEvent_t a = nullptr, b = nullptr;
+  StageTimer(hipStream_t s_, int kind_) : s(s_), kind(kind_) {
+    std::lock_guard<std::mutex> lk(g_tmu);
+    if (!g_timing) return;
+    a = pool_get();
+    b = pool_get();
+    (void)hipEventRecord(a, s);
+  }
+  ~StageTimer() {
+    if (!a) return;
+    (void)hipEventRecord(b, s);
+    std::lock_guard<std::mutex> lk(g_tmu);
+    g_events.push_back({a, b, kind});
+  }
+};
 }  // namespace
 
 extern "C" {
+
+int gs_timing_enable(int enable) {
+  std::lock_guard<std::mutex> lk(g_tmu);
+  for (auto& e : g_events) { g_pool.push_back(e.a); g_pool.push_back(e.b); }
+  g_events.clear();
+  g_timing = enable != 0;
+  return 0;
+}
+
+int gs_timing_read(double* ms, int64_t* count, int n_kinds) {
+  std::lock_guard<std::mutex> lk(g_tmu);
+  for (int k = 0; k < n_kinds; ++k) { ms[k] = 0.0; count[k] = 0; }
+  for (auto& e : g_events) {
+    if (e.kind < 0 || e.kind >= n_kinds) continue;
+    hipError_t r = hipEventSynchronize(e.b);
+    float t = 0.f;
+    if (r == hipSuccess) r = hipEventElapsedTime(&t, e.a, e.b);
+    if (r != hipSuccess) return fail((int)r, "timing read: %s", hipGetErrorString(r));
+    ms[e.kind] += t;
+    count[e.kind] += 1;
+  }
+  return 0;
+}
 
 int gs_version(void) { return GS_ABI_VERSION; }
 const char* gs_last_error(void) { return g_err.c_str(); }
@@ -130,10 +196,16 @@ int gs_forward_plan(const gs_gaussians* g, const gs_camera* cam, int prefiltered
   a.tiles = at<uint32_t>(geom, gl.tiles);
   a.status = at<int>(geom, gl.status);
   (void)hipMemsetAsync(a.status, 0, 16, s);
-  launch_preprocess_fwd(a, s);
+  {
+    StageTimer t(s, GS_STAGE_PREPROCESS);
+    launch_preprocess_fwd(a, s);
+  }
   if (int e = check("preprocess", debug, s)) return e;
   uint32_t* offsets = at<uint32_t>(geom, gl.offsets);
-  launch_scan(a.tiles, offsets, at<uint32_t>(geom, gl.blocksums), P, s);
+  {
+    StageTimer t(s, GS_STAGE_SCAN);
+    launch_scan(a.tiles, offsets, at<uint32_t>(geom, gl.blocksums), P, s);
+  }
   if (int e = check("scan", debug, s)) return e;
   // The one host read of the forward (CR/rasterizer_impl.cu:287): the total
   // instance count sizes the binning buffer.  The status word rides along.
@@ -172,17 +244,27 @@ int gs_forward_render(const gs_gaussians* g, const gs_camera* cam, int debug, in
     uint64_t* k1 = at<uint64_t>(binning, bl.keys1);
     uint32_t* v0 = at<uint32_t>(binning, bl.vals0);
     uint32_t* v1 = at<uint32_t>(binning, bl.vals1);
-    launch_duplicate(P, rec, at<uint32_t>(geom, gl.offsets), radii, gx, gy, k0, v0, s);
+    {
+      StageTimer t(s, GS_STAGE_DUPLICATE);
+      launch_duplicate(P, rec, at<uint32_t>(geom, gl.offsets), radii, gx, gy, k0, v0, s);
+    }
     if (int e = check("duplicateWithKeys", debug, s)) return e;
     const int bit = higher_msb((uint32_t)(gx * gy));
-    const int which = launch_radix_sort(L, k0, v0, k1, v1, at<uint32_t>(binning, bl.hist),
-                                        at<uint32_t>(binning, bl.rowtot), 32 + bit, s);
+    int which;
+    {
+      StageTimer t(s, GS_STAGE_SORT);
+      which = launch_radix_sort(L, k0, v0, k1, v1, at<uint32_t>(binning, bl.hist),
+                                at<uint32_t>(binning, bl.rowtot), 32 + bit, s);
+    }
     if (int e = check("radix sort", debug, s)) return e;
     if (which != sorted_slot(L, W, H)) return fail(-3, "internal: sort slot mismatch");
     sorted_keys = which ? k1 : k0;
     point_list = which ? v1 : v0;
   }
-  launch_tile_ranges(L, sorted_keys, ranges, gx * gy, s);
+  {
+    StageTimer t(s, GS_STAGE_RANGES);
+    launch_tile_ranges(L, sorted_keys, ranges, gx * gy, s);
+  }
   if (int e = check("identifyTileRanges", debug, s)) return e;
   RenderArgs ra{};
   ra.W = W; ra.H = H; ra.grid_x = gx; ra.num_tiles = gx * gy; ra.F = g->F; ra.compat = compat;
@@ -190,7 +272,10 @@ int gs_forward_render(const gs_gaussians* g, const gs_camera* cam, int debug, in
   ra.bg = cam->background;
   ra.out_color = out_color; ra.out_feature = out_feature; ra.out_depth = out_depth; ra.out_alpha = out_alpha;
   ra.n_contrib = at<uint32_t>(image, il.n_contrib);
-  if (!launch_render_fwd(ra, s)) return fail(-1, "unsupported feature width %d", g->F);
+  {
+    StageTimer t(s, GS_STAGE_RENDER_FWD);
+    if (!launch_render_fwd(ra, s)) return fail(-1, "unsupported feature width %d", g->F);
+  }
   return check("render", debug, s);
 }
 
@@ -228,7 +313,10 @@ int gs_backward(const gs_gaussians* g, const gs_camera* cam, const int32_t* radi
   ra.n_contrib = at<uint32_t>(image, il.n_contrib);
   ra.dL_dpix = dL_dout_color; ra.dL_dfeat = dL_dout_feature; ra.dL_ddepth = dL_dout_depth;
   ra.dL_dalpha = dL_dout_alpha; ra.acc = acc;
-  if (!launch_render_bwd(ra, s)) return fail(-1, "unsupported feature width %d", g->F);
+  {
+    StageTimer t(s, GS_STAGE_RENDER_BWD);
+    if (!launch_render_bwd(ra, s)) return fail(-1, "unsupported feature width %d", g->F);
+  }
   if (int e = check("render backward", debug, s)) return e;
   PreprocessBwdArgs b{};
   b.P = P; b.D = g->D; b.M = g->M; b.F = g->F; b.W = W; b.H = H; b.compat = compat;
@@ -244,7 +332,10 @@ int gs_backward(const gs_gaussians* g, const gs_camera* cam, const int32_t* radi
   b.dmeans2D = dL_dmeans2D; b.dcolors = dL_dcolors; b.dsemantic = dL_dsemantic; b.dopacity = dL_dopacity;
   b.dmeans3D = dL_dmeans3D; b.dcov3D = dL_dcov3D; b.dsh = dL_dsh; b.dscales = dL_dscales;
   b.drot = dL_drotations;
-  launch_preprocess_bwd(b, s);
+  {
+    StageTimer t(s, GS_STAGE_PREPROCESS_BWD);
+    launch_preprocess_bwd(b, s);
+  }
   return check("preprocess backward", debug, s);
 }
 

@@ -148,8 +148,10 @@ class _RasterizeGaussians(torch.autograd.Function):
             grad_scales = grad_scales * lab
             grad_rotations = grad_rotations * lab
             grad_cov3Ds_precomp = grad_cov3Ds_precomp * lab
-        return (grad_means3D, grad_means2D, grad_sh, grad_colors_precomp, grad_semantic_feature,
-                grad_opacities, grad_scales, grad_rotations, grad_cov3Ds_precomp, None, None)
+        grads = (grad_means3D, grad_means2D, grad_sh, grad_colors_precomp, grad_semantic_feature,
+                 grad_opacities, grad_scales, grad_rotations, grad_cov3Ds_precomp, None, None)
+        # inputs that were absent (None) or do not require grad get None
+        return tuple(g if need else None for g, need in zip(grads, ctx.needs_input_grad))
 
 
 class GaussianRasterizationSettings(NamedTuple):
@@ -198,6 +200,12 @@ class GaussianRasterizer(nn.Module):
                 ((scales is not None or rotations is not None) and cov3D_precomp is not None):
             raise Exception('Please provide exactly one of either scale/rotation pair or '
                             'precomputed 3D covariance!')
+        # __init__.py:218-230: absent inputs become empty tensors
+        shs = torch.Tensor([]) if shs is None else shs
+        colors_precomp = torch.Tensor([]) if colors_precomp is None else colors_precomp
+        scales = torch.Tensor([]) if scales is None else scales
+        rotations = torch.Tensor([]) if rotations is None else rotations
+        cov3D_precomp = torch.Tensor([]) if cov3D_precomp is None else cov3D_precomp
         has_label = label is not _UNSET
         lab = label if (has_label and isinstance(label, torch.Tensor)) else None
         color, radii, feature_map, depth, alpha = rasterize_gaussians(

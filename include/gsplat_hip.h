@@ -122,6 +122,23 @@ int gs_backward(const gs_gaussians *g, const gs_camera *cam, const int32_t *radi
 int gs_mark_visible(int64_t P, const float *means3D, const float *viewmatrix,
                     const float *projmatrix, uint8_t *present, gs_stream_t stream);
 
+/* ---- live stage timing (benchmark instrumentation; no reference analogue).
+ * When enabled, a hipEvent pair is recorded on the launch stream around each
+ * stage below; gs_timing_read() waits for them and returns, per stage, the
+ * summed elapsed milliseconds and the number of launches since the last
+ * gs_timing_enable().  Disabled by default. */
+#define GS_STAGE_PREPROCESS 0
+#define GS_STAGE_SCAN 1
+#define GS_STAGE_DUPLICATE 2
+#define GS_STAGE_SORT 3
+#define GS_STAGE_RANGES 4
+#define GS_STAGE_RENDER_FWD 5
+#define GS_STAGE_RENDER_BWD 6
+#define GS_STAGE_PREPROCESS_BWD 7
+#define GS_NUM_STAGES 8
+int gs_timing_enable(int enable);
+int gs_timing_read(double *ms, int64_t *count, int n_stages);
+
 /* ---- inspection entry points (tests and benchmarks; no reference analogue) */
 
 /* Copy the internal per-stage state of the last forward into host-visible
