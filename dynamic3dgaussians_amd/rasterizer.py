@@ -26,6 +26,7 @@ import torch
 import torch.nn as nn
 
 from . import _C
+from ._C import get_default_compat as _default_compat
 
 
 def cpu_deep_copy_tuple(input_tuple):
@@ -48,7 +49,7 @@ def _empty_like_none(t):
 
 def _compat_of(settings) -> str:
     mode = getattr(settings, "compat", None)
-    return _C.get_default_compat() if mode is None else mode
+    return _default_compat() if mode is None else mode
 
 
 def _principal_point(settings):

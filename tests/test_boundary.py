@@ -1,0 +1,168 @@
+"""CPU tests of the drop-in boundary (no GPU needed):
+  * the C ABI library loads and exports every symbol include/gsplat_hip.h declares;
+  * the autograd wrapper reproduces the reference wrapper's conventions exactly
+    (golden fixture recorded from DGR/diff_gaussian_rasterization/__init__.py);
+  * the caller-generation arity dispatch (G1..G4) and the settings superset;
+  * no CPU fallback: host tensors are rejected loudly.
+"""
+import json
+import os
+import re
+import subprocess
+
+import pytest
+import torch
+
+import dynamic3dgaussians_amd.rasterizer as R
+from dynamic3dgaussians_amd import _C, _lib
+from tests.golden.make_golden import Recorder, conventions_case, run_wrapper
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(REPO, "tests", "golden", "boundary_conventions.json")
+
+
+def _declared_symbols():
+    txt = open(os.path.join(REPO, "include", "gsplat_hip.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(gs_[a-z_0-9]+)\s*\(", txt)))
+
+
+def test_library_exports_every_declared_symbol():
+    L = _lib.load()
+    names = _declared_symbols()
+    assert len(names) >= 14
+    for n in names:
+        assert hasattr(L, n), n
+        assert n in _lib.PROTOTYPES, f"{n} has no ctypes prototype"
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.lib_path()], capture_output=True,
+                         text=True).stdout
+    exported = set(re.findall(r" T (gs_[a-z_0-9]+)", out))
+    assert set(names) <= exported
+
+
+def test_abi_version_and_sizes():
+    L = _lib.load()
+    assert L.gs_version() == 1
+    assert L.gs_geom_buffer_bytes(0) > 0
+    for a, b in [(1000, 2000), (10_000, 300_000)]:
+        assert L.gs_geom_buffer_bytes(b) > L.gs_geom_buffer_bytes(a)
+        assert L.gs_binning_buffer_bytes(b) > L.gs_binning_buffer_bytes(a)
+    assert L.gs_image_buffer_bytes(800, 800) >= 800 * 800 * 4
+    assert L.gs_backward_scratch_bytes(1000, 32) >= 1000 * 42 * 4
+
+
+def test_invalid_arguments_report_errors_without_gpu():
+    L = _lib.load()
+    g = _lib.GsGaussians(P=-1)
+    c = _lib.GsCamera(image_width=8, image_height=8)
+    import ctypes
+    n = ctypes.c_int64(0)
+    code = L.gs_forward_plan(ctypes.byref(g), ctypes.byref(c), 0, 0, 0, None, None,
+                             ctypes.byref(n), None)
+    assert code < 0 and b"P must be" in L.gs_last_error()
+    g = _lib.GsGaussians(P=10, F=7)
+    code = L.gs_forward_plan(ctypes.byref(g), ctypes.byref(c), 0, 0, 0, None, None,
+                             ctypes.byref(n), None)
+    assert code < 0 and b"feature width" in L.gs_last_error()
+
+
+def test_conventions_match_reference_wrapper(monkeypatch):
+    """Golden: positional packing of _C.rasterize_gaussians / _backward
+    (including Q2's swapped camera scalars), the returned 5-tuple and the
+    label masking (Q12) are identical to the reference wrapper's."""
+    gold = json.load(open(GOLD))
+    rec = Recorder()
+    monkeypatch.setattr(R, "_C", rec)
+    tensors, settings = conventions_case()
+    ours = run_wrapper(R, rec, tensors, settings)
+    assert ours["n_outputs"] == gold["n_outputs"] == 5
+    assert ours["radii"] == gold["radii"]
+    assert len(ours["forward_args"]) == len(gold["forward_args"]) == 22
+    assert ours["forward_args"] == gold["forward_args"]
+    assert len(ours["backward_args"]) == len(gold["backward_args"]) == 28
+    assert ours["backward_args"] == gold["backward_args"]
+    assert ours["grads"].keys() == gold["grads"].keys()
+    for k in gold["grads"]:
+        assert ours["grads"][k] == pytest.approx(gold["grads"][k], rel=1e-12, abs=1e-12), k
+    # the reference's settings fields are a prefix of ours (superset)
+    assert list(R.GaussianRasterizationSettings._fields[:15]) == gold["settings_fields"]
+
+
+def test_fixed_mode_passes_camera_scalars_in_binding_order(monkeypatch):
+    rec = Recorder()
+    monkeypatch.setattr(R, "_C", rec)
+    tensors, settings = conventions_case()
+    settings = dict(settings, compat="fixed")
+    run_wrapper(R, rec, tensors, settings)
+    assert rec.bwd_args[11:15] == [2.25, 1.75, 0.61, 0.47]
+
+
+def _stub_call(monkeypatch, **kw):
+    rec = Recorder()
+    monkeypatch.setattr(R, "_C", rec)
+    tensors, settings = conventions_case()
+    s = R.GaussianRasterizationSettings(**settings)
+    t = tensors
+    return R.GaussianRasterizer(s)(means3D=t["means3D"], means2D=torch.zeros_like(t["means3D"]),
+                                   opacities=t["opacities"], colors_precomp=t["colors_precomp"],
+                                   scales=t["scales"], rotations=t["rotations"], **kw)
+
+
+def test_arity_dispatch_g1_to_g4(monkeypatch):
+    t, _ = conventions_case()
+    g1 = _stub_call(monkeypatch)
+    assert len(g1) == 3 and g1[1].dtype == torch.int32               # color, radii, depth
+    g2 = _stub_call(monkeypatch, label=t["label"])
+    assert len(g2) == 4 and g2[1].dtype == torch.int32               # + alpha
+    g3 = _stub_call(monkeypatch, label=t["label"], semantic_feature=t["semantic_feature"])
+    assert len(g3) == 5 and g3[2].shape[0] == 32                     # color, radii, feat, depth, alpha
+    g4 = _stub_call(monkeypatch, semantic_feature=t["semantic_feature"])
+    assert len(g4) == 4 and g4[2].dtype == torch.int32 and g4[1].shape[0] == 32
+
+
+def test_settings_superset_defaults():
+    s = R.GaussianRasterizationSettings(image_height=10, image_width=20, tanfovx=0.5, tanfovy=0.4,
+                                        bg=torch.zeros(3), viewmatrix=torch.eye(4),
+                                        projmatrix=torch.eye(4), sh_degree=0,
+                                        campos=torch.zeros(3), prefiltered=False, debug=False)
+    assert s.c_x is None and s.confidence is None and s.compat is None
+    assert R._principal_point(s) == (10.0, 5.0)
+
+
+def test_input_validation_messages(monkeypatch):
+    rec = Recorder()
+    monkeypatch.setattr(R, "_C", rec)
+    t, settings = conventions_case()
+    ras = R.GaussianRasterizer(R.GaussianRasterizationSettings(**settings))
+    with pytest.raises(Exception, match="exactly one of either SHs or precomputed colors|excatly"):
+        ras(means3D=t["means3D"], means2D=t["means3D"], opacities=t["opacities"],
+            scales=t["scales"], rotations=t["rotations"])
+    with pytest.raises(Exception, match="scale/rotation pair"):
+        ras(means3D=t["means3D"], means2D=t["means3D"], opacities=t["opacities"],
+            colors_precomp=t["colors_precomp"], scales=t["scales"])
+
+
+def test_no_cpu_fallback():
+    t, settings = conventions_case()
+    with pytest.raises(_lib.GsplatError, match="device tensors"):
+        _C.rasterize_gaussians(settings["bg"], t["means3D"], t["colors_precomp"], None,
+                               t["opacities"], t["scales"], t["rotations"], 1.0, torch.Tensor([]),
+                               settings["viewmatrix"], settings["projmatrix"], 1.0, 1.0, 0.5, 0.5,
+                               4, 5, torch.Tensor([]), 0, settings["campos"], False, False)
+    with pytest.raises(RuntimeError, match=r"means3D must have dimensions \(num_points, 3\)"):
+        _C.rasterize_gaussians(settings["bg"], t["means3D"][:, :2], None, None, None, None, None,
+                               1.0, None, None, None, 1, 1, 1, 1, 4, 5, None, 0, None, False, False)
+
+
+def test_compat_validation():
+    with pytest.raises(ValueError):
+        _C.set_default_compat("nope")
+    _C.set_default_compat("fixed")
+    assert _C.get_default_compat() == "fixed"
+    _C.set_default_compat("reference")
+
+
+def test_drop_in_import_name():
+    import diff_gaussian_rasterization as d
+    from diff_gaussian_rasterization import _C as c2
+    assert d.GaussianRasterizer is R.GaussianRasterizer and c2 is _C
