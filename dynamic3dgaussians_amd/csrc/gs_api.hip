@@ -53,14 +53,17 @@ int higher_msb(uint32_t n) {  // getHigherMsb, CR/rasterizer_impl.cu:35-50
   return (int)msb;
 }
 
-// Which ping-pong slot holds the sorted (key, id) pairs after the radix sort:
-// every 8-bit pass swaps the slots (see launch_radix_sort).
-int sorted_slot(int64_t L, int W, int H) {
-  if (L <= 1) return 0;
+// Sort bit ranges: the depth sort uses the 31 bits of a positive float; the
+// instance sort only the tile id (getHigherMsb(tiles) bits, the reference's
+// 32 + msb minus the depth bits already ordered by the depth sort).
+constexpr int DEPTH_BITS = 31;
+int tile_bits(int W, int H) {
   const int gx = (W + TILE - 1) / TILE, gy = (H + TILE - 1) / TILE;
-  const int end_bit = 32 + higher_msb((uint32_t)(gx * gy));
-  return ((end_bit + 7) / 8) & 1;
+  return higher_msb((uint32_t)(gx * gy));
 }
+// Which ping-pong slot holds the sorted pairs: every 8-bit pass swaps slots.
+int slot_after(int64_t n, int end_bit) { return n <= 1 ? 0 : ((end_bit + 7) / 8) & 1; }
+int sorted_slot(int64_t L, int W, int H) { return slot_after(L, tile_bits(W, H)); }
 
 template <class T>
 T* at(void* base, size_t off) { return reinterpret_cast<T*>(static_cast<char*>(base) + off); }
@@ -164,7 +167,8 @@ size_t gs_geom_buffer_bytes(int64_t P) { return GeomLayout(P > 0 ? P : 0).total;
 size_t gs_binning_buffer_bytes(int64_t L) { return BinLayout(L > 0 ? L : 0).total; }
 size_t gs_image_buffer_bytes(int32_t W, int32_t H) { return ImgLayout(W, H).total; }
 size_t gs_backward_scratch_bytes(int64_t P, int32_t F) {
-  return align_up(sizeof(float) * (size_t)(A_FEAT + F) * (size_t)(P > 0 ? P : 0), 256) + 256;
+  (void)F;
+  return align_up(sizeof(float) * (size_t)A_FEAT * (size_t)(P > 0 ? P : 0), 256) + 256;
 }
 
 int gs_forward_plan(const gs_gaussians* g, const gs_camera* cam, int prefiltered, int debug, int compat,
@@ -203,8 +207,20 @@ int gs_forward_plan(const gs_gaussians* g, const gs_camera* cam, int prefiltered
   if (int e = check("preprocess", debug, s)) return e;
   uint32_t* offsets = at<uint32_t>(geom, gl.offsets);
   {
+    // stable depth order of the Gaussians (ties: index order)
+    StageTimer t(s, GS_STAGE_SORT);
+    uint32_t* dk0 = at<uint32_t>(geom, gl.dkeys0);
+    uint32_t* dk1 = at<uint32_t>(geom, gl.dkeys1);
+    uint32_t* o0 = at<uint32_t>(geom, gl.order0);
+    uint32_t* o1 = at<uint32_t>(geom, gl.order1);
+    launch_depth_keys(P, a.rec, radii, dk0, o0, s);
+    launch_radix_sort32(P, dk0, o0, dk1, o1, at<uint32_t>(geom, gl.dhist), at<uint32_t>(geom, gl.drowtot),
+                        DEPTH_BITS, s);
+  }
+  const uint32_t* order = at<uint32_t>(geom, slot_after(P, DEPTH_BITS) ? gl.order1 : gl.order0);
+  {
     StageTimer t(s, GS_STAGE_SCAN);
-    launch_scan(a.tiles, offsets, at<uint32_t>(geom, gl.blocksums), P, s);
+    launch_scan(a.tiles, order, offsets, at<uint32_t>(geom, gl.blocksums), P, s);
   }
   if (int e = check("scan", debug, s)) return e;
   // The one host read of the forward (CR/rasterizer_impl.cu:287): the total
@@ -238,23 +254,23 @@ int gs_forward_render(const gs_gaussians* g, const gs_camera* cam, int debug, in
   const float* rec = at<float>(geom, gl.rec);
   uint2* ranges = at<uint2>(image, il.ranges);
   const uint32_t* point_list = nullptr;
-  const uint64_t* sorted_keys = nullptr;
+  const uint32_t* sorted_keys = nullptr;
   if (L > 0) {
-    uint64_t* k0 = at<uint64_t>(binning, bl.keys0);
-    uint64_t* k1 = at<uint64_t>(binning, bl.keys1);
+    uint32_t* k0 = at<uint32_t>(binning, bl.keys0);
+    uint32_t* k1 = at<uint32_t>(binning, bl.keys1);
     uint32_t* v0 = at<uint32_t>(binning, bl.vals0);
     uint32_t* v1 = at<uint32_t>(binning, bl.vals1);
+    const uint32_t* order = at<uint32_t>(geom, slot_after(P, DEPTH_BITS) ? gl.order1 : gl.order0);
     {
       StageTimer t(s, GS_STAGE_DUPLICATE);
-      launch_duplicate(P, rec, at<uint32_t>(geom, gl.offsets), radii, gx, gy, k0, v0, s);
+      launch_duplicate_sorted(P, order, rec, at<uint32_t>(geom, gl.offsets), radii, gx, gy, k0, v0, s);
     }
     if (int e = check("duplicateWithKeys", debug, s)) return e;
-    const int bit = higher_msb((uint32_t)(gx * gy));
     int which;
     {
       StageTimer t(s, GS_STAGE_SORT);
-      which = launch_radix_sort(L, k0, v0, k1, v1, at<uint32_t>(binning, bl.hist),
-                                at<uint32_t>(binning, bl.rowtot), 32 + bit, s);
+      which = launch_radix_sort32(L, k0, v0, k1, v1, at<uint32_t>(binning, bl.hist),
+                                  at<uint32_t>(binning, bl.rowtot), tile_bits(W, H), s);
     }
     if (int e = check("radix sort", debug, s)) return e;
     if (which != sorted_slot(L, W, H)) return fail(-3, "internal: sort slot mismatch");
@@ -301,7 +317,8 @@ int gs_backward(const gs_gaussians* g, const gs_camera* cam, const int32_t* radi
   const BinLayout bl(L);
   const ImgLayout il(W, H);
   float* acc = static_cast<float*>(scratch);
-  (void)hipMemsetAsync(acc, 0, sizeof(float) * (size_t)(A_FEAT + g->F) * P, s);
+  (void)hipMemsetAsync(acc, 0, sizeof(float) * (size_t)A_FEAT * P, s);
+  if (g->F > 0) (void)hipMemsetAsync(dL_dsemantic, 0, sizeof(float) * (size_t)g->F * P, s);
   RenderBwdArgs ra{};
   ra.W = W; ra.H = H; ra.grid_x = gx; ra.num_tiles = gx * gy; ra.F = g->F; ra.compat = compat;
   ra.ranges = at<uint2>(image, il.ranges);
@@ -312,7 +329,7 @@ int gs_backward(const gs_gaussians* g, const gs_camera* cam, const int32_t* radi
   ra.alphas = alphas;
   ra.n_contrib = at<uint32_t>(image, il.n_contrib);
   ra.dL_dpix = dL_dout_color; ra.dL_dfeat = dL_dout_feature; ra.dL_ddepth = dL_dout_depth;
-  ra.dL_dalpha = dL_dout_alpha; ra.acc = acc;
+  ra.dL_dalpha = dL_dout_alpha; ra.acc = acc; ra.dsem = dL_dsemantic;
   {
     StageTimer t(s, GS_STAGE_RENDER_BWD);
     if (!launch_render_bwd(ra, s)) return fail(-1, "unsupported feature width %d", g->F);
@@ -386,7 +403,7 @@ int gs_debug_export(int64_t P, int32_t W, int32_t H, const void* geom, const voi
 }
 
 size_t gs_sort_scratch_bytes(int64_t n) {
-  const BinLayout bl(n);
+  const BinLayout bl(n, 8);
   return bl.total;
 }
 
@@ -394,7 +411,7 @@ int gs_sort_pairs(int64_t n, uint64_t* keys, uint32_t* vals, int end_bit, void* 
   if (n < 0 || end_bit < 0 || end_bit > 64) return fail(-1, "bad sort arguments");
   if (n <= 1) return 0;
   hipStream_t s = (hipStream_t)stream;
-  const BinLayout bl(n);
+  const BinLayout bl(n, 8);
   uint64_t* k1 = at<uint64_t>(scratch, bl.keys1);
   uint32_t* v1 = at<uint32_t>(scratch, bl.vals1);
   const int which = launch_radix_sort(n, keys, vals, k1, v1, at<uint32_t>(scratch, bl.hist),

@@ -1,6 +1,7 @@
-// gs_binning.hip -- tile binning: inclusive scan of per-Gaussian tile
-// counts, duplicate-with-keys, a stable LSD radix sort of (tile|depth, id)
-// pairs and per-tile ranges.  All HBM-bound integer work.
+// gs_binning.hip -- tile binning: a stable depth sort of the Gaussians, an
+// inclusive scan of their tile counts in depth order, duplicate-with-keys,
+// a stable LSD radix sort of the (tile, id) instances and per-tile ranges.
+// All HBM-bound integer work.
 //
 // Reference: DGR/cuda_rasterizer/rasterizer_impl.cu:70-138 (duplicateWithKeys,
 // identifyTileRanges), :283 (cub::DeviceScan::InclusiveSum), :306-314
@@ -44,13 +45,18 @@ __device__ inline uint32_t block_excl_scan(uint32_t x, uint32_t* sh /*[4]*/, uin
   return woff + inc - x;
 }
 
-__global__ __launch_bounds__(SCAN_T) void scan_reduce_kernel(const uint32_t* __restrict__ in, int P,
+__device__ inline uint32_t scan_in(const uint32_t* __restrict__ in, const uint32_t* __restrict__ perm, int i) {
+  return in[perm ? perm[i] : (uint32_t)i];
+}
+
+__global__ __launch_bounds__(SCAN_T) void scan_reduce_kernel(const uint32_t* __restrict__ in,
+                                                            const uint32_t* __restrict__ perm, int P,
                                                             uint32_t* __restrict__ sums) {
   __shared__ uint32_t sh[4];
   const int base = blockIdx.x * (SCAN_T * SCAN_I) + threadIdx.x * SCAN_I;
   uint32_t s = 0;
 #pragma unroll
-  for (int k = 0; k < SCAN_I; ++k) s += (base + k < P) ? in[base + k] : 0u;
+  for (int k = 0; k < SCAN_I; ++k) s += (base + k < P) ? scan_in(in, perm, base + k) : 0u;
   uint32_t tot;
   block_excl_scan(s, sh, &tot);
   if (threadIdx.x == 0) sums[blockIdx.x] = tot;
@@ -70,14 +76,15 @@ __global__ __launch_bounds__(SCAN_T) void scan_sums_kernel(uint32_t* __restrict_
   }
 }
 
-__global__ __launch_bounds__(SCAN_T) void scan_apply_kernel(const uint32_t* __restrict__ in, int P,
+__global__ __launch_bounds__(SCAN_T) void scan_apply_kernel(const uint32_t* __restrict__ in,
+                                                           const uint32_t* __restrict__ perm, int P,
                                                            const uint32_t* __restrict__ sums,
                                                            uint32_t* __restrict__ out) {
   __shared__ uint32_t sh[4];
   const int base = blockIdx.x * (SCAN_T * SCAN_I) + threadIdx.x * SCAN_I;
   uint32_t v[SCAN_I], s = 0;
 #pragma unroll
-  for (int k = 0; k < SCAN_I; ++k) { v[k] = (base + k < P) ? in[base + k] : 0u; s += v[k]; }
+  for (int k = 0; k < SCAN_I; ++k) { v[k] = (base + k < P) ? scan_in(in, perm, base + k) : 0u; s += v[k]; }
   uint32_t tot;
   uint32_t run = block_excl_scan(s, sh, &tot) + sums[blockIdx.x];
 #pragma unroll
@@ -87,53 +94,17 @@ __global__ __launch_bounds__(SCAN_T) void scan_apply_kernel(const uint32_t* __re
   }
 }
 
-void launch_scan(const uint32_t* in, uint32_t* out, uint32_t* tmp, int P, hipStream_t s) {
+void launch_scan(const uint32_t* in, const uint32_t* perm, uint32_t* out, uint32_t* tmp, int P, hipStream_t s) {
   if (P <= 0) return;
   const int nb = (P + SCAN_T * SCAN_I - 1) / (SCAN_T * SCAN_I);
-  hipLaunchKernelGGL(scan_reduce_kernel, dim3(nb), dim3(SCAN_T), 0, s, in, P, tmp);
+  hipLaunchKernelGGL(scan_reduce_kernel, dim3(nb), dim3(SCAN_T), 0, s, in, perm, P, tmp);
   hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(SCAN_T), 0, s, tmp, nb);
-  hipLaunchKernelGGL(scan_apply_kernel, dim3(nb), dim3(SCAN_T), 0, s, in, P, tmp, out);
-}
-
-// ------------------------------------------------------------------ duplicate
-
-__global__ __launch_bounds__(256) void duplicate_kernel(int P, const float* __restrict__ rec,
-                                                        const uint32_t* __restrict__ offsets,
-                                                        const int* __restrict__ radii, int gx, int gy,
-                                                        uint64_t* __restrict__ keys,
-                                                        uint32_t* __restrict__ vals) {
-  const int g = blockIdx.x * 256 + threadIdx.x;
-  if (g >= P) return;
-  const int r = radii[g];
-  if (!(r > 0)) return;
-  uint32_t off = (g == 0) ? 0u : offsets[g - 1];
-  const float px = rec[(size_t)REC * g + R_X], py = rec[(size_t)REC * g + R_Y];
-  const uint32_t dbits = __float_as_uint(rec[(size_t)REC * g + R_DEPTH]);
-  // getRect (auxiliary.h:46-56), same float expression order as preprocess
-  int a;
-  int x0, y0, x1, y1;
-  a = (int)((px - (float)r) / (float)TILE); a = a > 0 ? a : 0; x0 = a < gx ? a : gx;
-  a = (int)((py - (float)r) / (float)TILE); a = a > 0 ? a : 0; y0 = a < gy ? a : gy;
-  a = (int)((((px + (float)r) + (float)TILE) - 1.0f) / (float)TILE); a = a > 0 ? a : 0; x1 = a < gx ? a : gx;
-  a = (int)((((py + (float)r) + (float)TILE) - 1.0f) / (float)TILE); a = a > 0 ? a : 0; y1 = a < gy ? a : gy;
-  for (int y = y0; y < y1; ++y)
-    for (int x = x0; x < x1; ++x) {
-      keys[off] = ((uint64_t)(uint32_t)(y * gx + x) << 32) | dbits;
-      vals[off] = (uint32_t)g;
-      ++off;
-    }
-}
-
-void launch_duplicate(int P, const float* rec, const uint32_t* offsets, const int* radii, int grid_x,
-                      int grid_y, uint64_t* keys, uint32_t* vals, hipStream_t s) {
-  if (P <= 0) return;
-  hipLaunchKernelGGL(duplicate_kernel, dim3((P + 255) / 256), dim3(256), 0, s, P, rec, offsets, radii,
-                     grid_x, grid_y, keys, vals);
+  hipLaunchKernelGGL(scan_apply_kernel, dim3(nb), dim3(SCAN_T), 0, s, in, perm, P, tmp, out);
 }
 
 // ------------------------------------------------------------------ radix sort
 
-constexpr int RS_T = BinLayout::SORT_THREADS, RS_I = BinLayout::SORT_ITEMS, RS_TILE = BinLayout::SORT_TILE;
+constexpr int RS_T = SORT_THREADS;
 
 // Lanes of the wave holding the same 8-bit digit (valid lanes only).
 __device__ inline uint64_t match_digit(uint32_t d, uint64_t valid) {
@@ -147,16 +118,16 @@ __device__ inline uint64_t match_digit(uint32_t d, uint64_t valid) {
   return peers;
 }
 
-__global__ __launch_bounds__(RS_T) void radix_hist_kernel(const uint64_t* __restrict__ keys, int64_t n,
+template <class K>
+__global__ __launch_bounds__(RS_T) void radix_hist_kernel(const K* __restrict__ keys, int64_t n,
                                                           int shift, uint32_t* __restrict__ hist,
-                                                          int64_t nblk) {
+                                                          int64_t nblk, int rounds) {
   __shared__ uint32_t cnt[256];
   cnt[threadIdx.x] = 0;
   __syncthreads();
   const int lane = threadIdx.x & 63;
-  const int64_t base = (int64_t)blockIdx.x * RS_TILE;
-#pragma unroll 4
-  for (int r = 0; r < RS_I; ++r) {
+  const int64_t base = (int64_t)blockIdx.x * RS_T * rounds;
+  for (int r = 0; r < rounds; ++r) {
     const int64_t i = base + r * RS_T + threadIdx.x;
     const bool valid = i < n;
     const uint32_t d = valid ? (uint32_t)(keys[i] >> shift) & 255u : 0u;
@@ -185,10 +156,13 @@ __global__ __launch_bounds__(RS_T) void radix_rowscan_kernel(uint32_t* __restric
   if (threadIdx.x == 0) rowtot[blockIdx.x] = carry;
 }
 
+// Stable scatter of one 8-bit digit: items are ranked in block order (rounds
+// of 256, waves in order, lanes in order) with ballot-matched peer masks.
+template <class K>
 __global__ __launch_bounds__(RS_T) void radix_scatter_kernel(
-    const uint64_t* __restrict__ kin, const uint32_t* __restrict__ vin, uint64_t* __restrict__ kout,
+    const K* __restrict__ kin, const uint32_t* __restrict__ vin, K* __restrict__ kout,
     uint32_t* __restrict__ vout, int64_t n, int shift, const uint32_t* __restrict__ hist,
-    const uint32_t* __restrict__ rowtot, int64_t nblk) {
+    const uint32_t* __restrict__ rowtot, int64_t nblk, int rounds) {
   __shared__ uint32_t base[256];
   __shared__ uint32_t wcnt[4][256];
   __shared__ uint32_t sh[4];
@@ -200,11 +174,11 @@ __global__ __launch_bounds__(RS_T) void radix_scatter_kernel(
     wcnt[0][tid] = 0; wcnt[1][tid] = 0; wcnt[2][tid] = 0; wcnt[3][tid] = 0;
   }
   __syncthreads();
-  const int64_t b0 = (int64_t)blockIdx.x * RS_TILE;
-  for (int r = 0; r < RS_I; ++r) {
+  const int64_t b0 = (int64_t)blockIdx.x * RS_T * rounds;
+  for (int r = 0; r < rounds; ++r) {
     const int64_t i = b0 + r * RS_T + tid;
     const bool valid = i < n;
-    uint64_t k = 0;
+    K k = 0;
     uint32_t v = 0, d = 0;
     if (valid) { k = kin[i]; v = vin[i]; d = (uint32_t)(k >> shift) & 255u; }
     const uint64_t peers = match_digit(d, __ballot(valid));
@@ -225,39 +199,115 @@ __global__ __launch_bounds__(RS_T) void radix_scatter_kernel(
   }
 }
 
-int launch_radix_sort(int64_t n, uint64_t* keys0, uint32_t* vals0, uint64_t* keys1, uint32_t* vals1,
-                      uint32_t* hist, uint32_t* rowtot, int end_bit, hipStream_t s) {
+template <class K>
+int radix_sort_impl(int64_t n, K* keys0, uint32_t* vals0, K* keys1, uint32_t* vals1, uint32_t* hist,
+                    uint32_t* rowtot, int end_bit, hipStream_t s) {
   if (n <= 1) return 0;
-  const int64_t nblk = (n + RS_TILE - 1) / RS_TILE;
+  const int64_t nblk = sort_blocks(n);
+  const int rounds = sort_rounds(n);
   int cur = 0;
-  uint64_t* kb[2] = {keys0, keys1};
+  K* kb[2] = {keys0, keys1};
   uint32_t* vb[2] = {vals0, vals1};
   for (int shift = 0; shift < end_bit; shift += 8) {
-    hipLaunchKernelGGL(radix_hist_kernel, dim3((unsigned)nblk), dim3(RS_T), 0, s, kb[cur], n, shift, hist, nblk);
+    hipLaunchKernelGGL(radix_hist_kernel<K>, dim3((unsigned)nblk), dim3(RS_T), 0, s, kb[cur], n, shift, hist, nblk,
+                       rounds);
     hipLaunchKernelGGL(radix_rowscan_kernel, dim3(256), dim3(RS_T), 0, s, hist, nblk, rowtot);
-    hipLaunchKernelGGL(radix_scatter_kernel, dim3((unsigned)nblk), dim3(RS_T), 0, s, kb[cur], vb[cur],
-                       kb[cur ^ 1], vb[cur ^ 1], n, shift, hist, rowtot, nblk);
+    hipLaunchKernelGGL(radix_scatter_kernel<K>, dim3((unsigned)nblk), dim3(RS_T), 0, s, kb[cur], vb[cur],
+                       kb[cur ^ 1], vb[cur ^ 1], n, shift, hist, rowtot, nblk, rounds);
     cur ^= 1;
   }
   return cur;
 }
 
+int launch_radix_sort(int64_t n, uint64_t* keys0, uint32_t* vals0, uint64_t* keys1, uint32_t* vals1,
+                      uint32_t* hist, uint32_t* rowtot, int end_bit, hipStream_t s) {
+  return radix_sort_impl<uint64_t>(n, keys0, vals0, keys1, vals1, hist, rowtot, end_bit, s);
+}
+
+int launch_radix_sort32(int64_t n, uint32_t* keys0, uint32_t* vals0, uint32_t* keys1, uint32_t* vals1,
+                        uint32_t* hist, uint32_t* rowtot, int end_bit, hipStream_t s) {
+  return radix_sort_impl<uint32_t>(n, keys0, vals0, keys1, vals1, hist, rowtot, end_bit, s);
+}
+
+// ------------------------------------------------------------------ depth-first binning
+//
+// The reference sorts (tile << 32 | depth bits) pairs, stable in Gaussian
+// index, over 32 + msb(tiles) bits (6 passes of the L instances at 800x800).
+// Equivalent order with less work: sort the P Gaussians once by depth bits
+// (stable, so ties keep index order), emit each Gaussian's instances in that
+// order, then stably sort the instances by tile id alone (msb(tiles) bits: 2
+// passes of 4-byte keys).  Within a tile the result is (depth bits, index)
+// order -- identical to the reference's list.
+
+__global__ __launch_bounds__(256) void depth_keys_kernel(int P, const float* __restrict__ rec,
+                                                         const int* __restrict__ radii,
+                                                         uint32_t* __restrict__ keys,
+                                                         uint32_t* __restrict__ vals) {
+  const int g = blockIdx.x * 256 + threadIdx.x;
+  if (g >= P) return;
+  // positive depths order like their bit patterns; culled Gaussians have no
+  // instances, park them at the end
+  keys[g] = radii[g] > 0 ? __float_as_uint(rec[(size_t)REC * g + R_DEPTH]) : 0x7FFFFFFFu;
+  vals[g] = (uint32_t)g;
+}
+
+void launch_depth_keys(int P, const float* rec, const int* radii, uint32_t* keys, uint32_t* vals,
+                       hipStream_t s) {
+  if (P <= 0) return;
+  hipLaunchKernelGGL(depth_keys_kernel, dim3((P + 255) / 256), dim3(256), 0, s, P, rec, radii, keys, vals);
+}
+
+__global__ __launch_bounds__(256) void duplicate_sorted_kernel(int P, const uint32_t* __restrict__ order,
+                                                               const float* __restrict__ rec,
+                                                               const uint32_t* __restrict__ offsets,
+                                                               const int* __restrict__ radii, int gx, int gy,
+                                                               uint32_t* __restrict__ keys,
+                                                               uint32_t* __restrict__ vals) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= P) return;
+  const uint32_t g = order[i];
+  const int r = radii[g];
+  if (!(r > 0)) return;
+  uint32_t off = (i == 0) ? 0u : offsets[i - 1];
+  const float px = rec[(size_t)REC * g + R_X], py = rec[(size_t)REC * g + R_Y];
+  // getRect (auxiliary.h:46-56), same float expression order as preprocess
+  int a, x0, y0, x1, y1;
+  a = (int)((px - (float)r) / (float)TILE); a = a > 0 ? a : 0; x0 = a < gx ? a : gx;
+  a = (int)((py - (float)r) / (float)TILE); a = a > 0 ? a : 0; y0 = a < gy ? a : gy;
+  a = (int)((((px + (float)r) + (float)TILE) - 1.0f) / (float)TILE); a = a > 0 ? a : 0; x1 = a < gx ? a : gx;
+  a = (int)((((py + (float)r) + (float)TILE) - 1.0f) / (float)TILE); a = a > 0 ? a : 0; y1 = a < gy ? a : gy;
+  for (int y = y0; y < y1; ++y)
+    for (int x = x0; x < x1; ++x) {
+      keys[off] = (uint32_t)(y * gx + x);
+      vals[off] = g;
+      ++off;
+    }
+}
+
+void launch_duplicate_sorted(int P, const uint32_t* order, const float* rec, const uint32_t* offsets,
+                             const int* radii, int grid_x, int grid_y, uint32_t* keys, uint32_t* vals,
+                             hipStream_t s) {
+  if (P <= 0) return;
+  hipLaunchKernelGGL(duplicate_sorted_kernel, dim3((P + 255) / 256), dim3(256), 0, s, P, order, rec, offsets,
+                     radii, grid_x, grid_y, keys, vals);
+}
+
 // ------------------------------------------------------------------ ranges
 
-__global__ __launch_bounds__(256) void tile_ranges_kernel(int64_t L, const uint64_t* __restrict__ keys,
+__global__ __launch_bounds__(256) void tile_ranges_kernel(int64_t L, const uint32_t* __restrict__ keys,
                                                           uint2* __restrict__ ranges) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= L) return;
-  const uint32_t cur = (uint32_t)(keys[i] >> 32);
+  const uint32_t cur = keys[i];
   if (i == 0) ranges[cur].x = 0;
   else {
-    const uint32_t prev = (uint32_t)(keys[i - 1] >> 32);
+    const uint32_t prev = keys[i - 1];
     if (cur != prev) { ranges[prev].y = (uint32_t)i; ranges[cur].x = (uint32_t)i; }
   }
   if (i == L - 1) ranges[cur].y = (uint32_t)L;
 }
 
-void launch_tile_ranges(int64_t L, const uint64_t* keys, uint2* ranges, int num_tiles, hipStream_t s) {
+void launch_tile_ranges(int64_t L, const uint32_t* keys, uint2* ranges, int num_tiles, hipStream_t s) {
   (void)hipMemsetAsync(ranges, 0, sizeof(uint2) * (size_t)num_tiles, s);
   if (L <= 0) return;
   hipLaunchKernelGGL(tile_ranges_kernel, dim3((unsigned)((L + 255) / 256)), dim3(256), 0, s, L, keys, ranges);

@@ -40,11 +40,26 @@ constexpr int COMPAT_FIXED = 1;
 __host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 // ---------------------------------------------------------------- layouts
+// Radix-sort geometry: 256 threads per block, `rounds` items per thread,
+// chosen so that a pass has ~2048 blocks (>= 8 per CU) for any n; small
+// sorts (the per-Gaussian depth sort) would otherwise run on a few dozen
+// latency-bound blocks.
+constexpr int SORT_THREADS = 256;
+__host__ __device__ inline int sort_rounds(int64_t n) {
+  int64_t r = (n + (int64_t)SORT_THREADS * 2048 - 1) / ((int64_t)SORT_THREADS * 2048);
+  return (int)(r < 1 ? 1 : (r > 16 ? 16 : r));
+}
+__host__ __device__ inline int64_t sort_blocks(int64_t n) {
+  const int64_t tile = (int64_t)SORT_THREADS * sort_rounds(n);
+  return (n + tile - 1) / tile;
+}
 // Geometry buffer (per-Gaussian state kept from forward to backward).
 struct GeomLayout {
-  size_t rec, cov3D, clamped, tiles, offsets, blocksums, status, total;
   static constexpr int SCAN_ITEMS = 2048;  // items per scan block
+  size_t rec, cov3D, clamped, tiles, offsets, blocksums, status;
+  size_t dkeys0, dkeys1, order0, order1, dhist, drowtot, total;
   __host__ __device__ GeomLayout(int64_t P) {
+    const int64_t nblk = sort_blocks(P);
     size_t o = 0;
     rec = o;       o = align_up(o + sizeof(float) * REC * P, 256);
     cov3D = o;     o = align_up(o + sizeof(float) * 6 * P, 256);
@@ -53,22 +68,27 @@ struct GeomLayout {
     offsets = o;   o = align_up(o + sizeof(uint32_t) * P, 256);
     blocksums = o; o = align_up(o + sizeof(uint32_t) * ((P + SCAN_ITEMS - 1) / SCAN_ITEMS + 1), 256);
     status = o;    o = align_up(o + 64, 256);
+    dkeys0 = o;    o = align_up(o + sizeof(uint32_t) * P, 256);
+    dkeys1 = o;    o = align_up(o + sizeof(uint32_t) * P, 256);
+    order0 = o;    o = align_up(o + sizeof(uint32_t) * P, 256);
+    order1 = o;    o = align_up(o + sizeof(uint32_t) * P, 256);
+    dhist = o;     o = align_up(o + sizeof(uint32_t) * 256 * (nblk > 0 ? nblk : 1), 256);
+    drowtot = o;   o = align_up(o + sizeof(uint32_t) * 256, 256);
     total = o;
   }
 };
 
-// Binning buffer (per tile/Gaussian instance).
+// Binning buffer (per tile/Gaussian instance): ping-pong (tile key, id)
+// arrays of the radix sort.  key_bytes = 4 for the binning (tile ids), 8 for
+// the standalone 64-bit sort entry point.
 struct BinLayout {
-  static constexpr int SORT_THREADS = 256;
-  static constexpr int SORT_ITEMS = 16;  // per thread per block
-  static constexpr int SORT_TILE = SORT_THREADS * SORT_ITEMS;
   size_t keys0, keys1, vals0, vals1, hist, rowtot, total;
   int64_t nblk;
-  __host__ __device__ BinLayout(int64_t L) {
-    nblk = (L + SORT_TILE - 1) / SORT_TILE;
+  __host__ __device__ BinLayout(int64_t L, int key_bytes = 4) {
+    nblk = sort_blocks(L);
     size_t o = 0;
-    keys0 = o; o = align_up(o + sizeof(uint64_t) * L, 256);
-    keys1 = o; o = align_up(o + sizeof(uint64_t) * L, 256);
+    keys0 = o; o = align_up(o + (size_t)key_bytes * L, 256);
+    keys1 = o; o = align_up(o + (size_t)key_bytes * L, 256);
     vals0 = o; o = align_up(o + sizeof(uint32_t) * L, 256);
     vals1 = o; o = align_up(o + sizeof(uint32_t) * L, 256);
     hist = o;  o = align_up(o + sizeof(uint32_t) * 256 * (nblk > 0 ? nblk : 1), 256);

@@ -40,7 +40,7 @@ struct PreprocessBwdArgs {
   const float* proj;
   const float* campos;
   float scale_modifier, c_x, c_y, tan_fovx, tan_fovy, focal_x, focal_y;
-  const float* acc;  // P x (10+F) blend gradients
+  const float* acc;  // P x 10 blend gradients (A_MX..A_DEPTH)
   float* dmeans2D;
   float* dcolors;
   float* dsemantic;
@@ -79,22 +79,28 @@ struct RenderBwdArgs {
   const float* dL_dfeat;
   const float* dL_ddepth;
   const float* dL_dalpha;
-  float* acc;  // P x (10+F), zeroed by the caller
+  float* acc;   // P x 10 blend gradients, zeroed by the caller
+  float* dsem;  // P x F semantic-feature gradients (the output), zeroed by the caller
 };
 
 void launch_preprocess_fwd(const PreprocessArgs& a, hipStream_t s);
 void launch_preprocess_bwd(const PreprocessBwdArgs& a, hipStream_t s);
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t s);
 
-// Binning: inclusive scan of tiles_touched (P) into offsets, block sums in tmp.
-void launch_scan(const uint32_t* in, uint32_t* out, uint32_t* tmp, int P, hipStream_t s);
-void launch_duplicate(int P, const float* rec, const uint32_t* offsets, const int* radii, int grid_x,
-                      int grid_y, uint64_t* keys, uint32_t* vals, hipStream_t s);
-// Stable LSD radix sort on bits [0, end_bit); the result ends in keys0/vals0
-// or keys1/vals1 -- returns 0 or 1 for which.
+// Binning: inclusive scan of in[perm[i]] (perm may be null) into out, block sums in tmp.
+void launch_scan(const uint32_t* in, const uint32_t* perm, uint32_t* out, uint32_t* tmp, int P, hipStream_t s);
+// Stable LSD radix sorts on bits [0, end_bit); the result ends in keys0/vals0
+// or keys1/vals1 -- returns 0 or 1 for which (passes of 8 bits swap slots).
 int launch_radix_sort(int64_t n, uint64_t* keys0, uint32_t* vals0, uint64_t* keys1, uint32_t* vals1,
                       uint32_t* hist, uint32_t* rowtot, int end_bit, hipStream_t s);
-void launch_tile_ranges(int64_t L, const uint64_t* keys, uint2* ranges, int num_tiles, hipStream_t s);
+int launch_radix_sort32(int64_t n, uint32_t* keys0, uint32_t* vals0, uint32_t* keys1, uint32_t* vals1,
+                        uint32_t* hist, uint32_t* rowtot, int end_bit, hipStream_t s);
+void launch_depth_keys(int P, const float* rec, const int* radii, uint32_t* keys, uint32_t* vals,
+                       hipStream_t s);
+void launch_duplicate_sorted(int P, const uint32_t* order, const float* rec, const uint32_t* offsets,
+                             const int* radii, int grid_x, int grid_y, uint32_t* keys, uint32_t* vals,
+                             hipStream_t s);
+void launch_tile_ranges(int64_t L, const uint32_t* keys, uint2* ranges, int num_tiles, hipStream_t s);
 
 bool launch_render_fwd(const RenderArgs& a, hipStream_t s);
 bool launch_render_bwd(const RenderBwdArgs& a, hipStream_t s);

@@ -356,8 +356,7 @@ __device__ inline void cov3d_bwd(V3 scale, float mod, float4 rot, const float d[
 __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdArgs a) {
   const int g = blockIdx.x * 256 + threadIdx.x;
   if (g >= a.P) return;
-  const int CS = A_FEAT + a.F;
-  const float* acc = a.acc + (size_t)CS * g;
+  const float* acc = a.acc + (size_t)A_FEAT * g;
   const bool vis = a.radii[g] > 0;
   // blend gradients -> output tensors (zero for culled Gaussians: never touched)
   const float am0 = acc[A_MX], am1 = acc[A_MY];
@@ -365,7 +364,6 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdArgs a
   const float dcol[3] = {acc[A_R], acc[A_G], acc[A_B]};
   a.dcolors[3 * g] = dcol[0]; a.dcolors[3 * g + 1] = dcol[1]; a.dcolors[3 * g + 2] = dcol[2];
   a.dopacity[g] = acc[A_OP];
-  for (int ch = 0; ch < a.F; ++ch) a.dsemantic[(size_t)a.F * g + ch] = acc[A_FEAT + ch];
   float dm[3] = {0.f, 0.f, 0.f};
   float dcov[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   float dscale[3] = {0.f, 0.f, 0.f}, drot[4] = {0.f, 0.f, 0.f, 0.f};

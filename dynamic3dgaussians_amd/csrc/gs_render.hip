@@ -3,29 +3,77 @@
 // Reference: DGR/cuda_rasterizer/forward.cu:274-408 (renderCUDA) and
 // backward.cu:432-652 (renderCUDA backward).
 //
-// MI355X design (no LDS staging, no block barriers):
+// MI355X design:
 //  * A 16x16 binning tile is one 256-thread workgroup; each of its 4 waves
 //    owns a 16x4 pixel strip and walks the tile's depth-sorted list on its
-//    own.  The Gaussian index and its 64-B render record are wave-uniform,
-//    so they arrive through the scalar unit (s_load_dwordx16) and feed the
-//    VALU as SGPR operands -- no per-lane gather, no LDS round trip.
-//  * Wave-level culling: a wave skips a Gaussian whose alpha >= 1/255 region
-//    (precomputed half extents) misses its 16x4 strip -- exactly the
-//    Gaussians every one of its pixels would skip in the reference loop.
-//  * Forward early exit is a wave vote (the reference votes per 256-thread
-//    block); the backward starts each wave at its own max n_contrib.
-//  * Backward: per-pixel contributions are summed over the wave with a
-//    transposed reduction (permlane32/16 swaps + DPP), then ONE atomic
-//    wave-instruction commits all 10+F per-Gaussian sums, instead of the
-//    reference's 10+F atomics per pixel.
+//    own -- no block barriers, every wave exits when its own pixels are done.
+//  * The list is consumed in chunks of 64: lane j gathers the 48-B render
+//    record of the chunk's j-th Gaussian (prefetched one chunk ahead), tests
+//    it against the wave's strip (the Gaussian's alpha >= 1/255 extent) and
+//    parks it in a wave-private LDS slot.  A ballot leaves the Gaussians the
+//    strip can see; the inner loop visits only those, reading each record
+//    back with broadcast ds_read_b128.  Culled Gaussians are exactly the ones
+//    every pixel of the strip skips in the reference loop.
+//  * Semantic features (F = 32/64) are a dense contraction and go to the fp32
+//    matrix cores (v_mfma_f32_32x32x2_f32, an exact k-ordered fma chain):
+//      forward   out_feat^T[ch][pix] += f[g][ch] * w[g][pix]  over Gaussian pairs
+//      backward  dL/df[g][ch]        += w[g][pix] * dL/dfeat[pix][ch] over 32-Gaussian batches
+//    Colour, depth and the geometric gradients stay on the VALU.
+//  * Backward per-Gaussian sums (mean2D, conic, opacity, colour, depth) are
+//    reduced over the wave with permlane32/16 swaps + DPP and committed with
+//    ONE atomic wave-instruction; feature gradients leave the MFMA
+//    accumulator as 2 x 128-B rows per atomic instruction.
 #include "gs_common.h"
 #include "gs_kernels.h"
 
 namespace gs {
 
 constexpr float ALPHA_MIN = 1.0f / 255.0f;
+constexpr int CHUNK = 64;
+typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 __device__ inline bool wave_any(bool p) { return __ballot(p) != 0ull; }
+
+// exp(x) as one v_exp_f32 (2^x) on x*log2(e): ~3 ulp instead of libm's
+// correctly-rounded-ish 14-instruction sequence.  Forward and backward use
+// the same function, so their alpha decisions agree bit for bit.
+__device__ inline float fast_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
+// 1/x as one v_rcp_f32 (1 ulp).
+__device__ inline float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+
+__device__ inline f32x16 mfma32(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+// Swap the upper half of `a` with the lower half of `b`:
+// lo = [a_lo, b_lo], hi = [a_hi, b_hi].
+__device__ inline void swap32(float a, float b, float& lo, float& hi) {
+  auto r = __builtin_amdgcn_permlane32_swap(f_bits(a), f_bits(b), false, false);
+  lo = bits_f(r[0]);
+  hi = bits_f(r[1]);
+}
+
+// Gather the record of the chunk's lane-th Gaussian (rec fields 0..11).
+struct RecRegs {
+  float4 q0, q1, q2;
+  uint32_t gid;
+};
+__device__ inline RecRegs load_rec(const uint32_t* __restrict__ point_list, const float* __restrict__ rec,
+                                   uint32_t i, bool ok, const RecRegs& prev) {
+  RecRegs r = prev;
+  if (ok) {
+    r.gid = point_list[i];
+    const float4* p = reinterpret_cast<const float4*>(rec + (size_t)r.gid * REC);
+    r.q0 = p[0];  // x, y, conic a, conic b
+    r.q1 = p[1];  // conic c, opacity, r, g
+    r.q2 = p[2];  // b, depth, ext x, ext y
+  }
+  return r;
+}
+
+__device__ inline bool strip_culled(const RecRegs& q, float sx0, float sx1, float sy0, float sy1) {
+  return q.q0.x + q.q2.z < sx0 || q.q0.x - q.q2.z > sx1 || q.q0.y + q.q2.w < sy0 || q.q0.y - q.q2.w > sy1;
+}
 
 // ------------------------------------------------------------------ forward
 
@@ -36,6 +84,12 @@ __global__ __launch_bounds__(256) void render_fwd_kernel(
     const float* __restrict__ feats, const float* __restrict__ bg, float* __restrict__ out_color,
     float* __restrict__ out_feature, float* __restrict__ out_depth, float* __restrict__ out_alpha,
     uint32_t* __restrict__ n_contrib) {
+  constexpr bool MF = (F == 32 || F == 64);  // features on the matrix cores
+  constexpr int FB = MF ? F / 32 : 1;        // 32-channel blocks
+  constexpr int NSF = (!MF && F > 0) ? F : 1;
+  __shared__ float4 s_rec[4][CHUNK][3];
+  __shared__ uint32_t s_gid[4][CHUNK];
+
   const int tile = xcd_remap(blockIdx.x, num_tiles);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int tx = tile % grid_x, ty = tile / grid_x;
@@ -47,73 +101,173 @@ __global__ __launch_bounds__(256) void render_fwd_kernel(
   const uint2 range = ranges[tile];
 
   float T = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f, Dp = 0.f;
-  float SF[F > 0 ? F : 1];
+  float SF[NSF];
 #pragma unroll
-  for (int c = 0; c < F; ++c) SF[c] = 0.f;
+  for (int c = 0; c < NSF; ++c) SF[c] = 0.f;
+  f32x16 acc[2 * FB];
+#pragma unroll
+  for (int i = 0; i < 2 * FB; ++i) acc[i] = f32x16{0};
   uint32_t last = 0;
   bool done = !inside;
-
-  for (uint32_t i = range.x; i < range.y; ++i) {
-    if (!wave_any(!done)) break;
-    const uint32_t g = point_list[i];
-    const float* r = rec + (size_t)g * REC;
-    const float gx = r[R_X], gy = r[R_Y], ex = r[R_EX], ey = r[R_EY];
-    if (gx + ex < sx0 || gx - ex > sx1 || gy + ey < sy0 || gy - ey > sy1) continue;
-    const float ca = r[R_CA], cb = r[R_CB], cc = r[R_CC], op = r[R_OP];
-    const float dx = gx - pfx, dy = gy - pfy;
-    const float power = -0.5f * (ca * dx * dx + cc * dy * dy) - cb * dx * dy;
-    const float alpha = fminf(0.99f, op * expf(power));
-    const float test_T = T * (1 - alpha);
-    bool blend = !done && !(power > 0.0f) && !(alpha < ALPHA_MIN);
-    if (blend && test_T < 0.0001f) { done = true; blend = false; }
-    if (!wave_any(blend)) continue;
-    if (blend) {
-      const float w = alpha * T;
-      C0 += r[R_R] * w;
-      C1 += r[R_G] * w;
-      C2 += r[R_B] * w;
-      Dp += r[R_DEPTH] * w;
-      if constexpr (F > 0) {
-        const float* f = feats + (size_t)g * F;
+  // MFMA pairing: a blended Gaussian waits for a partner; a completed pair's
+  // feature rows are loaded one pair ahead of its MFMAs (latency hiding).
+  int pend = 0;
+  uint32_t pend_gid = 0;
+  float pend_w = 0.f;
+  int have_prev = 0;
+  float pa[FB], pb0 = 0.f, pb1 = 0.f;
 #pragma unroll
-        for (int c = 0; c < F; ++c) SF[c] += f[c] * w;
+  for (int fb = 0; fb < FB; ++fb) pa[fb] = 0.f;
+  auto push_pair = [&](float b0, float b1, const float (&an)[FB]) {
+    if (have_prev) {
+#pragma unroll
+      for (int fb = 0; fb < FB; ++fb) {
+        acc[2 * fb] = mfma32(pa[fb], pb0, acc[2 * fb]);
+        acc[2 * fb + 1] = mfma32(pa[fb], pb1, acc[2 * fb + 1]);
       }
-      T = test_T;
-      last = i - range.x + 1;
+    }
+#pragma unroll
+    for (int fb = 0; fb < FB; ++fb) pa[fb] = an[fb];
+    pb0 = b0;
+    pb1 = b1;
+    have_prev = 1;
+  };
+
+  RecRegs q{};
+  q = load_rec(point_list, rec, range.x + lane, range.x + lane < range.y, q);
+  bool all_done = !wave_any(!done);
+  for (uint32_t c0 = range.x; c0 < range.y && !all_done; c0 += CHUNK) {
+    const bool keep = (c0 + lane < range.y) && !strip_culled(q, sx0, sx1, sy0, sy1);
+    s_rec[wave][lane][0] = q.q0;
+    s_rec[wave][lane][1] = q.q1;
+    s_rec[wave][lane][2] = q.q2;
+    s_gid[wave][lane] = q.gid;
+    uint64_t mask = __ballot(keep);
+    q = load_rec(point_list, rec, c0 + CHUNK + lane, c0 + CHUNK + lane < range.y, q);  // prefetch
+    while (mask) {
+      const int j = __builtin_ctzll(mask);
+      mask &= mask - 1;
+      const float4 r0 = s_rec[wave][j][0];
+      const float4 r1 = s_rec[wave][j][1];
+      const float4 r2 = s_rec[wave][j][2];
+      const float dx = r0.x - pfx, dy = r0.y - pfy;
+      const float power = -0.5f * (r0.z * dx * dx + r1.x * dy * dy) - r0.w * dx * dy;
+      const float alpha = fminf(0.99f, r1.y * fast_exp(power));
+      const float test_T = T * (1 - alpha);
+      bool blend = !done && !(power > 0.0f) && !(alpha < ALPHA_MIN);
+      if (blend && test_T < 0.0001f) { done = true; blend = false; }
+      if (wave_any(blend)) {
+        const float w = blend ? alpha * T : 0.0f;
+        if (blend) {
+          C0 += r1.z * w;
+          C1 += r1.w * w;
+          C2 += r2.x * w;
+          Dp += r2.y * w;
+          T = test_T;
+          last = c0 + j - range.x + 1;
+        }
+        if constexpr (F > 0) {
+          const uint32_t gid = __builtin_amdgcn_readfirstlane(s_gid[wave][j]);
+          if constexpr (MF) {
+            if (pend == 0) {
+              pend = 1;
+              pend_gid = gid;
+              pend_w = w;
+            } else {
+              const uint32_t ga = lane < 32 ? pend_gid : gid;
+              float b0, b1, an[FB];
+              swap32(pend_w, w, b0, b1);
+#pragma unroll
+              for (int fb = 0; fb < FB; ++fb) an[fb] = feats[(size_t)ga * F + fb * 32 + (lane & 31)];
+              push_pair(b0, b1, an);
+              pend = 0;
+            }
+          } else if (blend) {
+            const float* f = feats + (size_t)gid * F;
+#pragma unroll
+            for (int c = 0; c < NSF; ++c) SF[c] += f[c] * w;
+          }
+        }
+      }
+      if (!wave_any(!done)) { all_done = true; break; }
     }
   }
+  if constexpr (MF) {
+    if (pend) {
+      float b0, b1, an[FB];
+      swap32(pend_w, 0.0f, b0, b1);
+#pragma unroll
+      for (int fb = 0; fb < FB; ++fb) an[fb] = lane < 32 ? feats[(size_t)pend_gid * F + fb * 32 + lane] : 0.0f;
+      push_pair(b0, b1, an);
+    }
+    if (have_prev) {
+#pragma unroll
+      for (int fb = 0; fb < FB; ++fb) {
+        acc[2 * fb] = mfma32(pa[fb], pb0, acc[2 * fb]);
+        acc[2 * fb + 1] = mfma32(pa[fb], pb1, acc[2 * fb + 1]);
+      }
+    }
+  }
+  const size_t HW = (size_t)H * W;
   if (inside) {
-    const size_t HW = (size_t)H * W, pix = (size_t)py * W + px;
+    const size_t pix = (size_t)py * W + px;
     n_contrib[pix] = last;
     out_color[pix] = C0 + T * bg[0];
     out_color[HW + pix] = C1 + T * bg[1];
     out_color[2 * HW + pix] = C2 + T * bg[2];
     out_depth[pix] = Dp;
+    if constexpr (!MF && F > 0) {
 #pragma unroll
-    for (int c = 0; c < F; ++c) {
-      // Q4: the reference adds bg[ch] (an out-of-bounds read for ch >= 3;
-      // zero here); the fixed mode adds no background to features.
-      const float b = (COMPAT == COMPAT_REFERENCE && c < 3) ? bg[c] : 0.0f;
-      out_feature[c * HW + pix] = SF[c] + T * b;
+      for (int c = 0; c < F; ++c) {
+        // Q4: the reference adds bg[ch] (an out-of-bounds read for ch >= 3;
+        // zero here); the fixed mode adds no background to features.
+        const float b = (COMPAT == COMPAT_REFERENCE && c < 3) ? bg[c] : 0.0f;
+        out_feature[c * HW + pix] = SF[c] + T * b;
+      }
     }
     if (COMPAT != COMPAT_REFERENCE) out_alpha[pix] = 1.0f - T;  // Q1
+  }
+  if constexpr (MF) {
+    // acc[2*fb + blk] holds out_feat^T: lane l, register r ->
+    // channel fb*32 + (r&3) + 8(r>>2) + 4(l>>5), strip pixel (l&31) + 32 blk.
+    float t_lo, t_hi;
+    swap32(T, T, t_lo, t_hi);  // T of strip pixel (l&31) and (l&31)+32
+#pragma unroll
+    for (int blk = 0; blk < 2; ++blk) {
+      const int p = (lane & 31) + 32 * blk;
+      const int qx = tx * TILE + (p & 15), qy = ty * TILE + wave * WAVE_ROWS + (p >> 4);
+      if (qx < W && qy < H) {
+        const size_t pix = (size_t)qy * W + qx;
+        const float Tp = blk ? t_hi : t_lo;
+#pragma unroll
+        for (int fb = 0; fb < FB; ++fb)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int ch = fb * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+            const float b = (COMPAT == COMPAT_REFERENCE && ch < 3) ? bg[ch < 3 ? ch : 0] : 0.0f;
+            out_feature[ch * HW + pix] = acc[2 * fb + blk][r] + Tp * b;
+          }
+      }
+    }
   }
 }
 
 // ------------------------------------------------------------------ backward
 
-// Reduce N per-lane components over the wave and add them to dst[0..N) with
-// one atomic wave-instruction per 64 components.
+// Reduce N per-lane components over the wave and add them with one atomic
+// wave-instruction per 64 components: components [0, A_FEAT) go to the
+// per-Gaussian record acc[g][0..A_FEAT), features to dsem[g][0..F).
 template <int N, int OFF = 0>
-__device__ inline void commit(const float (&v)[N], float* __restrict__ dst, int lane) {
+__device__ inline void commit(const float (&v)[N], float* __restrict__ acc_g, float* __restrict__ dsem_g,
+                              int lane) {
   constexpr int n = (N - OFF) < 64 ? (N - OFF) : 64;
   float t[64];
 #pragma unroll
   for (int c = 0; c < n; ++c) t[c] = v[OFF + c];
   const float s = wave_reduce_transposed<n>(t, lane);
-  const int comp = bitrev6(lane);
-  if (comp < n) atomicAdd(dst + OFF + comp, s);
-  if constexpr (OFF + 64 < N) commit<N, OFF + 64>(v, dst, lane);
+  const int comp = OFF + bitrev6(lane);
+  if (comp < OFF + n) atomicAdd(comp < A_FEAT ? acc_g + comp : dsem_g + (comp - A_FEAT), s);
+  if constexpr (OFF + 64 < N) commit<N, OFF + 64>(v, acc_g, dsem_g, lane);
 }
 
 template <int F, int COMPAT>
@@ -123,8 +277,18 @@ __global__ __launch_bounds__(256) void render_bwd_kernel(
     const float* __restrict__ feats, const float* __restrict__ bg, const float* __restrict__ alphas,
     const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dpix,
     const float* __restrict__ dL_dfeat, const float* __restrict__ dL_ddepth,
-    const float* __restrict__ dL_dalpha, float* __restrict__ acc) {
-  constexpr int N = A_FEAT + F;
+    const float* __restrict__ dL_dalpha, float* __restrict__ acc, float* __restrict__ dsem) {
+  constexpr bool MF = (F == 32 || F == 64);
+  constexpr int FB = MF ? F / 32 : 1;
+  constexpr int NV = MF ? A_FEAT : A_FEAT + F;  // components reduced on the VALU
+  constexpr int WB = 32;                        // Gaussians per MFMA batch
+  constexpr bool FIXED_FEAT = (COMPAT != COMPAT_REFERENCE) && F > 0;
+  constexpr int NF_REG = (!MF && F > 0) ? F : 1;
+  __shared__ float4 s_rec[4][CHUNK][3];
+  __shared__ uint32_t s_gid[4][CHUNK];
+  __shared__ float s_w[MF ? 4 : 1][MF ? WB : 1][65];
+  __shared__ uint32_t s_bgid[MF ? 4 : 1][WB];
+
   const int tile = xcd_remap(blockIdx.x, num_tiles);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int tx = tile % grid_x, ty = tile / grid_x;
@@ -139,82 +303,169 @@ __global__ __launch_bounds__(256) void render_bwd_kernel(
   const float T_final = inside ? 1 - alphas[pix] : 0.0f;
   float T = T_final;
   const uint32_t last = inside ? n_contrib[pix] : 0u;
-  float dLp[3], dLf[F > 0 ? F : 1];
+  float dLp[3];
   dLp[0] = inside ? dL_dpix[pix] : 0.f;
   dLp[1] = inside ? dL_dpix[HW + pix] : 0.f;
   dLp[2] = inside ? dL_dpix[2 * HW + pix] : 0.f;
-#pragma unroll
-  for (int c = 0; c < F; ++c) dLf[c] = inside ? dL_dfeat[c * HW + pix] : 0.f;
   const float dLd = inside ? dL_ddepth[pix] : 0.f;
   const float dLa = inside ? dL_dalpha[pix] : 0.f;
   const float bg_dot = bg[0] * dLp[0] + bg[1] * dLp[1] + bg[2] * dLp[2];
   const float ddelx_dx = 0.5f * (float)W, ddely_dy = 0.5f * (float)H;
 
+  // Upstream feature gradients.  VALU path: one register per channel.
+  // MFMA path: the B operands of dL/df = W . dLf, lane l / step s holding
+  // dLf[pixel 2s + (l>>5)][channel fb*32 + (l&31)], transposed through LDS.
+  float dLf[NF_REG];
+  float Bs[MF ? FB : 1][MF ? 32 : 1];
+  float dLf_own[FIXED_FEAT && MF ? F : 1];  // fixed mode also needs f . dLf per pixel
+  if constexpr (MF) {
+#pragma unroll
+    for (int fb = 0; fb < FB; ++fb) {
+#pragma unroll
+      for (int c = 0; c < 32; ++c) {
+        const float v = inside ? dL_dfeat[(size_t)(fb * 32 + c) * HW + pix] : 0.f;
+        s_w[wave][c][lane] = v;
+        if constexpr (FIXED_FEAT) dLf_own[fb * 32 + c] = v;
+      }
+#pragma unroll
+      for (int s = 0; s < 32; ++s) Bs[fb][s] = s_w[wave][lane & 31][2 * s + (lane >> 5)];
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < NF_REG; ++c) dLf[c] = (F > 0 && inside) ? dL_dfeat[c * HW + pix] : 0.f;
+  }
+
   float ar0 = 0.f, ar1 = 0.f, ar2 = 0.f, lc0 = 0.f, lc1 = 0.f, lc2 = 0.f;
   float ad = 0.f, ld = 0.f, aa = 0.f, la = 0.f;
   float af = 0.f, lfd = 0.f;  // fixed mode: feature accum . dL/dfeature
+  int nb = 0;                 // MFMA batch fill
 
   const uint32_t wmax = __builtin_amdgcn_readfirstlane(wave_max_u(last));
-  for (uint32_t k = wmax; k-- > 0;) {
-    const uint32_t g = point_list[range.x + k];
-    const float* r = rec + (size_t)g * REC;
-    const float gx = r[R_X], gy = r[R_Y], ex = r[R_EX], ey = r[R_EY];
-    if (gx + ex < sx0 || gx - ex > sx1 || gy + ey < sy0 || gy - ey > sy1) continue;
-    const float ca = r[R_CA], cb = r[R_CB], cc = r[R_CC], op = r[R_OP];
-    const float dx = gx - pfx, dy = gy - pfy;
-    const float power = -0.5f * (ca * dx * dx + cc * dy * dy) - cb * dx * dy;
-    const float G = expf(power);
-    const float alpha = fminf(0.99f, op * G);
-    const bool valid = (k < last) && !(power > 0.0f) && !(alpha < ALPHA_MIN);
-    if (!wave_any(valid)) continue;
-    float v[N];
+  const uint32_t top = range.x + wmax;  // exclusive end of this wave's walk
+  RecRegs q{};
+  {
+    const uint32_t c0 = top > range.x + CHUNK ? top - CHUNK : range.x;
+    q = load_rec(point_list, rec, c0 + lane, c0 + lane < top, q);
+  }
+  for (uint32_t hi = top; hi > range.x;) {
+    const uint32_t c0 = hi > range.x + CHUNK ? hi - CHUNK : range.x;
+    const bool keep = (c0 + lane < hi) && !strip_culled(q, sx0, sx1, sy0, sy1);
+    s_rec[wave][lane][0] = q.q0;
+    s_rec[wave][lane][1] = q.q1;
+    s_rec[wave][lane][2] = q.q2;
+    s_gid[wave][lane] = q.gid;
+    uint64_t mask = __ballot(keep);
+    {
+      const uint32_t n0 = c0 > range.x + CHUNK ? c0 - CHUNK : range.x;
+      q = load_rec(point_list, rec, n0 + lane, n0 + lane < c0, q);  // prefetch the next (lower) chunk
+    }
+    while (mask) {
+      const int j = 63 - __builtin_clzll(mask);
+      mask &= ~(1ull << j);
+      const uint32_t k = c0 + j - range.x;  // position in the tile list
+      const float4 r0 = s_rec[wave][j][0];
+      const float4 r1 = s_rec[wave][j][1];
+      const float4 r2 = s_rec[wave][j][2];
+      const float dx = r0.x - pfx, dy = r0.y - pfy;
+      const float ca = r0.z, cb = r0.w, cc = r1.x, op = r1.y;
+      const float power = -0.5f * (ca * dx * dx + cc * dy * dy) - cb * dx * dy;
+      const float G = fast_exp(power);
+      const float alpha = fminf(0.99f, op * G);
+      const bool valid = (k < last) && !(power > 0.0f) && !(alpha < ALPHA_MIN);
+      if (!wave_any(valid)) continue;
+      const uint32_t gid = __builtin_amdgcn_readfirstlane(s_gid[wave][j]);
+      float v[NV];
 #pragma unroll
-    for (int c = 0; c < N; ++c) v[c] = 0.f;
-    if (valid) {
-      T = T / (1.f - alpha);
-      const float dch = alpha * T;
-      float dL_dopa = 0.f;
-      const float c0 = r[R_R], c1 = r[R_G], c2 = r[R_B];
-      ar0 = la * lc0 + (1.f - la) * ar0; lc0 = c0; dL_dopa += (c0 - ar0) * dLp[0];
-      ar1 = la * lc1 + (1.f - la) * ar1; lc1 = c1; dL_dopa += (c1 - ar1) * dLp[1];
-      ar2 = la * lc2 + (1.f - la) * ar2; lc2 = c2; dL_dopa += (c2 - ar2) * dLp[2];
-      v[A_R] = dch * dLp[0]; v[A_G] = dch * dLp[1]; v[A_B] = dch * dLp[2];
-      const float cd = r[R_DEPTH];
-      ad = la * ld + (1.f - la) * ad; ld = cd; dL_dopa += (cd - ad) * dLd;
-      if constexpr (F > 0) {
-        const float* f = feats + (size_t)g * F;
-        float fd = 0.f;
+      for (int c = 0; c < NV; ++c) v[c] = 0.f;
+      float dch = 0.f;
+      if (valid) {
+        const float rinv = fast_rcp(1.f - alpha);
+        T = T * rinv;
+        dch = alpha * T;
+        float dL_dopa = 0.f;
+        const float c0v = r1.z, c1v = r1.w, c2v = r2.x;
+        ar0 = la * lc0 + (1.f - la) * ar0; lc0 = c0v; dL_dopa += (c0v - ar0) * dLp[0];
+        ar1 = la * lc1 + (1.f - la) * ar1; lc1 = c1v; dL_dopa += (c1v - ar1) * dLp[1];
+        ar2 = la * lc2 + (1.f - la) * ar2; lc2 = c2v; dL_dopa += (c2v - ar2) * dLp[2];
+        v[A_R] = dch * dLp[0]; v[A_G] = dch * dLp[1]; v[A_B] = dch * dLp[2];
+        const float cd = r2.y;
+        ad = la * ld + (1.f - la) * ad; ld = cd; dL_dopa += (cd - ad) * dLd;
+        if constexpr (F > 0) {
+          const float* f = feats + (size_t)gid * F;
+          float fd = 0.f;
+          if constexpr (!MF) {
 #pragma unroll
-        for (int c = 0; c < F; ++c) {
-          v[A_FEAT + c] = dch * dLf[c];
-          if constexpr (COMPAT != COMPAT_REFERENCE) fd += f[c] * dLf[c];
+            for (int c = 0; c < NF_REG; ++c) {
+              v[A_FEAT + c] = dch * dLf[c];
+              if constexpr (FIXED_FEAT) fd += f[c] * dLf[c];
+            }
+          } else if constexpr (FIXED_FEAT) {
+#pragma unroll
+            for (int c = 0; c < F; ++c) fd += f[c] * dLf_own[c];
+          }
+          // Q5: in the reference the feature term reads a never-written
+          // (zero) scratch and contributes nothing to dL/dalpha.
+          if constexpr (FIXED_FEAT) {
+            af = la * lfd + (1.f - la) * af;
+            lfd = fd;
+            dL_dopa += fd - af;
+          }
         }
-        // Q5: in the reference the feature term reads a never-written
-        // (zero) scratch and contributes nothing to dL/dalpha.
-        if constexpr (COMPAT != COMPAT_REFERENCE) {
-          af = la * lfd + (1.f - la) * af;
-          lfd = fd;
-          dL_dopa += fd - af;
+        v[A_DEPTH] = dch * dLd;
+        aa = la + (1.f - la) * aa;
+        dL_dopa += (1 - aa) * dLa;
+        dL_dopa *= T;
+        la = alpha;
+        dL_dopa += (-T_final * rinv) * bg_dot;
+        const float dL_dG = op * dL_dopa;
+        const float gdx = G * dx, gdy = G * dy;
+        const float dG_ddelx = -gdx * ca - gdy * cb;
+        const float dG_ddely = -gdy * cc - gdx * cb;
+        v[A_MX] = dL_dG * dG_ddelx * ddelx_dx;
+        v[A_MY] = dL_dG * dG_ddely * ddely_dy;
+        v[A_CA] = -0.5f * gdx * dx * dL_dG;
+        v[A_CB] = -0.5f * gdx * dy * dL_dG;
+        v[A_CC] = -0.5f * gdy * dy * dL_dG;
+        v[A_OP] = G * dL_dopa;
+      }
+      commit<NV>(v, acc + (size_t)A_FEAT * gid, dsem + (size_t)F * gid, lane);
+      if constexpr (MF) {
+        s_w[wave][nb][lane] = dch;
+        if (lane == 0) s_bgid[wave][nb] = gid;
+        if (++nb == WB) {
+#pragma unroll
+          for (int fb = 0; fb < FB; ++fb) {
+            f32x16 c = f32x16{0};
+#pragma unroll
+            for (int s = 0; s < 32; ++s) c = mfma32(s_w[wave][lane & 31][2 * s + (lane >> 5)], Bs[fb][s], c);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+              atomicAdd(dsem + (size_t)s_bgid[wave][row] * F + fb * 32 + (lane & 31), c[r]);
+            }
+          }
+          nb = 0;
         }
       }
-      v[A_DEPTH] = dch * dLd;
-      aa = la + (1.f - la) * aa;
-      dL_dopa += (1 - aa) * dLa;
-      dL_dopa *= T;
-      la = alpha;
-      dL_dopa += (-T_final / (1.f - alpha)) * bg_dot;
-      const float dL_dG = op * dL_dopa;
-      const float gdx = G * dx, gdy = G * dy;
-      const float dG_ddelx = -gdx * ca - gdy * cb;
-      const float dG_ddely = -gdy * cc - gdx * cb;
-      v[A_MX] = dL_dG * dG_ddelx * ddelx_dx;
-      v[A_MY] = dL_dG * dG_ddely * ddely_dy;
-      v[A_CA] = -0.5f * gdx * dx * dL_dG;
-      v[A_CB] = -0.5f * gdx * dy * dL_dG;
-      v[A_CC] = -0.5f * gdy * dy * dL_dG;
-      v[A_OP] = G * dL_dopa;
     }
-    commit<N>(v, acc + (size_t)N * g, lane);
+    hi = c0;
+  }
+  if constexpr (MF) {
+    if (nb > 0) {
+      // rows >= nb hold stale weights; MFMA rows are independent, so they
+      // only produce results that are not committed
+#pragma unroll
+      for (int fb = 0; fb < FB; ++fb) {
+        f32x16 c = f32x16{0};
+#pragma unroll
+        for (int s = 0; s < 32; ++s) c = mfma32(s_w[wave][lane & 31][2 * s + (lane >> 5)], Bs[fb][s], c);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          if (row < nb) atomicAdd(dsem + (size_t)s_bgid[wave][row] * F + fb * 32 + (lane & 31), c[r]);
+        }
+      }
+    }
   }
 }
 
@@ -239,11 +490,11 @@ static void bwd_f(const RenderBwdArgs& a, hipStream_t s) {
   if (a.compat == COMPAT_REFERENCE)
     hipLaunchKernelGGL((render_bwd_kernel<F, COMPAT_REFERENCE>), grid, block, 0, s, a.W, a.H, a.grid_x,
                        a.num_tiles, a.ranges, a.point_list, a.rec, a.feats, a.bg, a.alphas, a.n_contrib,
-                       a.dL_dpix, a.dL_dfeat, a.dL_ddepth, a.dL_dalpha, a.acc);
+                       a.dL_dpix, a.dL_dfeat, a.dL_ddepth, a.dL_dalpha, a.acc, a.dsem);
   else
     hipLaunchKernelGGL((render_bwd_kernel<F, COMPAT_FIXED>), grid, block, 0, s, a.W, a.H, a.grid_x,
                        a.num_tiles, a.ranges, a.point_list, a.rec, a.feats, a.bg, a.alphas, a.n_contrib,
-                       a.dL_dpix, a.dL_dfeat, a.dL_ddepth, a.dL_dalpha, a.acc);
+                       a.dL_dpix, a.dL_dfeat, a.dL_ddepth, a.dL_dalpha, a.acc, a.dsem);
 }
 
 bool launch_render_fwd(const RenderArgs& a, hipStream_t s) {

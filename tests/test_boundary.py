@@ -48,7 +48,7 @@ def test_abi_version_and_sizes():
         assert L.gs_geom_buffer_bytes(b) > L.gs_geom_buffer_bytes(a)
         assert L.gs_binning_buffer_bytes(b) > L.gs_binning_buffer_bytes(a)
     assert L.gs_image_buffer_bytes(800, 800) >= 800 * 800 * 4
-    assert L.gs_backward_scratch_bytes(1000, 32) >= 1000 * 42 * 4
+    assert L.gs_backward_scratch_bytes(1000, 32) >= 1000 * 10 * 4  # feature grads go to the output
 
 
 def test_invalid_arguments_report_errors_without_gpu():
