@@ -233,14 +233,23 @@ def main():
     def step():
         opt.zero_grad(set_to_none=False)
         rv = params2rendervar(params, label)
+        # The activations are shared by all cameras of the step: render from
+        # detached leaves, let autograd sum the per-camera gradients on them,
+        # then run the activation backward once (same gradients as
+        # back-propagating every camera through the activations).
+        leaves = {k: v.detach().requires_grad_(True) for k, v in rv.items()
+                  if isinstance(v, torch.Tensor) and v.requires_grad}
+        rvl = dict(rv, **leaves)
         for s in settings:
             ras = GaussianRasterizer(s)
-            im, radius, feat, depth, _ = ras(**rv)
+            im, radius, feat, depth, _ = ras(**rvl)
             outs, grads = [im, depth], [up_color, up_depth]
             if up_feat is not None:
                 outs.append(feat)
                 grads.append(up_feat)
-            torch.autograd.backward(outs, grads, retain_graph=True)
+            torch.autograd.backward(outs, grads)
+        keys = [k for k in leaves if k != "means2D" and leaves[k].grad is not None]
+        torch.autograd.backward([rv[k] for k in keys], [leaves[k].grad for k in keys])
         bucket.all_reduce()
         opt.step()
 

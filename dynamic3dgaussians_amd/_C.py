@@ -111,7 +111,7 @@ class _Inputs:
                            colors_precomp=_ptr(self.colors), semantic_feature=_ptr(self.sem),
                            opacities=_ptr(self.opacity), scales=_ptr(self.scales),
                            rotations=_ptr(self.rotations), cov3D_precomp=_ptr(self.cov3D),
-                           scale_modifier=self.scale_modifier, _pad=0)
+                           scale_modifier=self.scale_modifier, _pad=0, grad_mask=None)
 
 
 def _camera(dev, background, viewmatrix, projmatrix, campos, c_x, c_y, tan_fovx, tan_fovy, W, H):
@@ -152,8 +152,9 @@ def rasterize_gaussians(background, means3D, colors, semantic_feature, opacity, 
     out_color = torch.empty(3, H, W, **f32)
     out_feature = torch.empty(inp.F, H, W, **f32)
     out_depth = torch.empty(1, H, W, **f32)
-    # Q1: the reference never writes out_alpha (it stays 0); "fixed" writes 1 - T.
-    out_alpha = torch.zeros(1, H, W, **f32) if cm == 0 else torch.empty(1, H, W, **f32)
+    # Q1: the reference never writes out_alpha (it stays 0; the kernel stores
+    # those zeros); "fixed" writes 1 - T.
+    out_alpha = torch.empty(1, H, W, **f32)
     radii = torch.empty(P, dtype=torch.int32, device=dev)
     geom = torch.empty(L_.gs_geom_buffer_bytes(P), **u8)
     img = torch.empty(L_.gs_image_buffer_bytes(W, H), **u8)
@@ -178,13 +179,19 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, semantic_fe
                                  rotations, scale_modifier, cov3D_precomp, viewmatrix, projmatrix,
                                  c_x, c_y, tan_fovx, tan_fovy, dL_dout_color, dL_dout_feature,
                                  dL_dout_depth, dL_dout_alpha, sh, degree, campos, geomBuffer, R,
-                                 binningBuffer, imageBuffer, alphas, debug, *, compat=None):
+                                 binningBuffer, imageBuffer, alphas, debug, *, compat=None,
+                                 grad_mask=None):
     """RasterizeGaussiansBackwardCUDA (DGR/rasterize_points.cu:128-225).
 
     Camera scalars are consumed in this positional order, exactly as the
     reference binding consumes them.  Returns (dL_dmeans2D[P,3],
     dL_dcolors[P,3], dL_dsemantic[P,F], dL_dopacity[P,1], dL_dmeans3D[P,3],
     dL_dcov3D[P,6], dL_dsh[P,M,3], dL_dscales[P,3], dL_drotations[P,4]).
+
+    `grad_mask` (keyword-only, no reference analogue in the binding): an
+    optional per-Gaussian [P] mask fused into the kernel, equal to the
+    reference wrapper's `grad * label` (__init__.py:159-173) on every returned
+    gradient except dL_dmeans2D and dL_dsemantic.
     """
     L_ = _lib.load()
     cm = _compat_code(compat)
@@ -200,6 +207,11 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, semantic_fe
     cam, keep = _camera(dev, background, viewmatrix, projmatrix, campos, c_x, c_y, tan_fovx,
                         tan_fovy, W, H)
     g = inp.struct()
+    if grad_mask is not None:
+        gm = grad_mask.to(device=dev, dtype=torch.float32).reshape(-1).contiguous()
+        if gm.numel() != P:
+            raise RuntimeError(f"grad_mask must have {P} elements, got {gm.numel()}")
+        g.grad_mask = gm.data_ptr()
     dLc = _dev(dL_dout_color, dev, "dL_dout_color")
     dLd = _dev(dL_dout_depth, dev, "dL_dout_depth")
     dLa = _dev(dL_dout_alpha, dev, "dL_dout_alpha")

@@ -16,6 +16,7 @@ _lock = threading.Lock()
 _lib = None
 
 c_void_p = ctypes.c_void_p
+ABI_VERSION = 2  # include/gsplat_hip.h GS_ABI_VERSION
 c_int32, c_int64, c_float, c_size_t = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_size_t
 
 GS_COMPAT = {"reference": 0, "fixed": 1}
@@ -27,7 +28,8 @@ class GsGaussians(ctypes.Structure):
                 ("means3D", c_void_p), ("shs", c_void_p), ("colors_precomp", c_void_p),
                 ("semantic_feature", c_void_p), ("opacities", c_void_p), ("scales", c_void_p),
                 ("rotations", c_void_p), ("cov3D_precomp", c_void_p),
-                ("scale_modifier", c_float), ("_pad", c_int32)]
+                ("scale_modifier", c_float), ("_pad", c_int32),
+                ("grad_mask", c_void_p)]
 
 
 class GsCamera(ctypes.Structure):
@@ -118,7 +120,7 @@ def load(auto_build: bool = True):
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        if L.gs_version() != 1:
+        if L.gs_version() != ABI_VERSION:
             raise GsplatError(f"ABI version mismatch: library reports {L.gs_version()}")
         _lib = L
         return L

@@ -362,8 +362,12 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdArgs a
   const float am0 = acc[A_MX], am1 = acc[A_MY];
   a.dmeans2D[3 * g] = am0; a.dmeans2D[3 * g + 1] = am1; a.dmeans2D[3 * g + 2] = 0.f;
   const float dcol[3] = {acc[A_R], acc[A_G], acc[A_B]};
-  a.dcolors[3 * g] = dcol[0]; a.dcolors[3 * g + 1] = dcol[1]; a.dcolors[3 * g + 2] = dcol[2];
-  a.dopacity[g] = acc[A_OP];
+  // Q12 label mask (DGR/__init__.py:159-173), applied at store time exactly as
+  // the reference's elementwise `grad * label` (the chain rule uses unmasked dcol).
+  const bool masked = a.grad_mask != nullptr;
+  const float mk = masked ? a.grad_mask[g] : 1.f;
+  a.dcolors[3 * g] = dcol[0] * mk; a.dcolors[3 * g + 1] = dcol[1] * mk; a.dcolors[3 * g + 2] = dcol[2] * mk;
+  a.dopacity[g] = acc[A_OP] * mk;
   float dm[3] = {0.f, 0.f, 0.f};
   float dcov[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   float dscale[3] = {0.f, 0.f, 0.f}, drot[4] = {0.f, 0.f, 0.f, 0.f};
@@ -449,11 +453,17 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdArgs a
     float* ds = a.dsh + (size_t)g * a.M * 3;
     for (int i = 0; i < 3 * a.M; ++i) ds[i] = 0.f;
   }
-  a.dmeans3D[3 * g] = dm[0]; a.dmeans3D[3 * g + 1] = dm[1]; a.dmeans3D[3 * g + 2] = dm[2];
+  if (masked && a.M > 0) {
+    float* ds = a.dsh + (size_t)g * a.M * 3;
+    for (int i = 0; i < 3 * a.M; ++i) ds[i] *= mk;
+  }
+  a.dmeans3D[3 * g] = dm[0] * mk; a.dmeans3D[3 * g + 1] = dm[1] * mk; a.dmeans3D[3 * g + 2] = dm[2] * mk;
 #pragma unroll
-  for (int i = 0; i < 6; ++i) a.dcov3D[6 * g + i] = dcov[i];
-  a.dscales[3 * g] = dscale[0]; a.dscales[3 * g + 1] = dscale[1]; a.dscales[3 * g + 2] = dscale[2];
-  reinterpret_cast<float4*>(a.drot)[g] = make_float4(drot[0], drot[1], drot[2], drot[3]);
+  for (int i = 0; i < 6; ++i) a.dcov3D[6 * g + i] = dcov[i] * mk;
+  a.dscales[3 * g] = dscale[0] * mk; a.dscales[3 * g + 1] = dscale[1] * mk;
+  a.dscales[3 * g + 2] = dscale[2] * mk;
+  reinterpret_cast<float4*>(a.drot)[g] =
+      make_float4(drot[0] * mk, drot[1] * mk, drot[2] * mk, drot[3] * mk);
 }
 
 void launch_preprocess_bwd(const PreprocessBwdArgs& a, hipStream_t s) {

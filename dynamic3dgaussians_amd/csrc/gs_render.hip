@@ -225,7 +225,10 @@ __global__ __launch_bounds__(256) void render_fwd_kernel(
         out_feature[c * HW + pix] = SF[c] + T * b;
       }
     }
-    if (COMPAT != COMPAT_REFERENCE) out_alpha[pix] = 1.0f - T;  // Q1
+    // Q1: the reference never writes out_alpha (torch::full -> 0 stays 0);
+    // we store that 0 here instead of a separate fill launch.
+    if (COMPAT != COMPAT_REFERENCE) out_alpha[pix] = 1.0f - T;
+    else if (out_alpha) out_alpha[pix] = 0.0f;
   }
   if constexpr (MF) {
     // acc[2*fb + blk] holds out_feat^T: lane l, register r ->

@@ -58,6 +58,10 @@ def _principal_point(settings):
     return float(cx), float(cy)
 
 
+_FUSABLE_LABEL_DTYPES = (torch.float32, torch.float16, torch.bfloat16, torch.bool, torch.uint8,
+                         torch.int8, torch.int16, torch.int32, torch.int64)
+
+
 class _RasterizeGaussians(torch.autograd.Function):
     """__init__.py:48-174."""
 
@@ -122,23 +126,30 @@ class _RasterizeGaussians(torch.autograd.Function):
                 rs.scale_modifier, cov3Ds_precomp, rs.viewmatrix, rs.projmatrix, *cam4,
                 grad_color, grad_out_feature, grad_depth, grad_alpha, sh, rs.sh_degree, rs.campos,
                 geomBuffer, num_rendered, binningBuffer, imgBuffer, alpha, rs.debug)
+        # The label mask is fused into the backward kernel when that is
+        # bit-identical to the wrapper's `grad * label.unsqueeze(1)` (a [P]
+        # label whose dtype does not promote fp32); otherwise it is applied
+        # below exactly as the reference does.
+        fuse = (label is not None and label.dim() == 1 and label.numel() == means3D.size(0)
+                and label.dtype in _FUSABLE_LABEL_DTYPES)
+        kw = dict(compat=ctx.compat, grad_mask=label if fuse else None)
         if rs.debug:
             cpu_args = cpu_deep_copy_tuple(args)
             try:
-                grads = _C.rasterize_gaussians_backward(*args, compat=ctx.compat)
+                grads = _C.rasterize_gaussians_backward(*args, **kw)
             except Exception as ex:
                 torch.save(cpu_args, "snapshot_bw.dump")
                 print("\nAn error occured in backward. Writing snapshot_bw.dump for debugging.\n")
                 raise ex
         else:
-            grads = _C.rasterize_gaussians_backward(*args, compat=ctx.compat)
+            grads = _C.rasterize_gaussians_backward(*args, **kw)
         (grad_means2D, grad_colors_precomp, grad_semantic_feature, grad_opacities, grad_means3D,
          grad_cov3Ds_precomp, grad_sh, grad_scales, grad_rotations) = grads
         if ctx.sem_shape is not None:
             grad_semantic_feature = grad_semantic_feature.reshape(ctx.sem_shape)
         else:
             grad_semantic_feature = None
-        if label is not None:
+        if label is not None and not fuse:
             # __init__.py:159-173: every Gaussian-parameter gradient except
             # means2D and the semantic feature is masked by `label` (Q12).
             lab = label.unsqueeze(1)

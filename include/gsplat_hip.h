@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 1
+#define GS_ABI_VERSION 2
 
 /* compat modes: numerics of the as-shipped reference vs corrected ones */
 #define GS_COMPAT_REFERENCE 0
@@ -60,6 +60,13 @@ typedef struct gs_gaussians {
   const float *cov3D_precomp;     /* P x 6 or NULL */
   float scale_modifier;
   int32_t _pad;
+  /* Optional per-Gaussian gradient mask (P floats or NULL), used by
+   * gs_backward only: dL/d{means3D, sh, colors, opacity, scales, rotations,
+   * cov3D} are multiplied by it, exactly as the reference's Python autograd
+   * wrapper does with `label` after the binding returns
+   * (DGR/diff_gaussian_rasterization/__init__.py:159-173).  dL/dmeans2D and
+   * dL/dsemantic are not masked (Q12). */
+  const float *grad_mask;
 } gs_gaussians;
 
 /* Camera / raster settings (GaussianRasterizationSettings,
@@ -93,7 +100,9 @@ int gs_forward_plan(const gs_gaussians *g, const gs_camera *cam, int prefiltered
 /* Forward, phase 2 -- replaces CR/rasterizer_impl.cu:289-345 (duplicateWithKeys,
  * radix sort, identifyTileRanges, render).  Outputs are planar CHW:
  * out_color 3xHxW, out_feature FxHxW (may be NULL if F==0), out_depth HxW,
- * out_alpha HxW.  Every output pixel is written. */
+ * out_alpha HxW.  Every output pixel is written.  In GS_COMPAT_REFERENCE mode
+ * out_alpha receives zeros (the reference never writes it, Q1) and may be NULL;
+ * in GS_COMPAT_FIXED mode it receives 1 - T_final. */
 int gs_forward_render(const gs_gaussians *g, const gs_camera *cam, int debug,
                       int compat, void *geom_buffer, void *binning_buffer,
                       void *image_buffer, int64_t num_rendered, const int32_t *radii,

@@ -96,7 +96,14 @@ class Recorder(types.ModuleType):
         M = args[19].shape[1] if args[19].numel() else 0
         g = torch.Generator().manual_seed(12)
         r = lambda *s: torch.randn(*s, generator=g)  # noqa: E731
-        return (r(P, 3), r(P, 3), r(P, 32), r(P, 1), r(P, 3), r(P, 6), r(P, M, 3), r(P, 3), r(P, 4))
+        out = [r(P, 3), r(P, 3), r(P, 32), r(P, 1), r(P, 3), r(P, 6), r(P, M, 3), r(P, 3), r(P, 4)]
+        m = kw.get("grad_mask")  # our binding's fused label mask (never passed by the reference)
+        if m is not None:
+            m = m.float().reshape(-1)
+            for i in (1, 3, 4, 5, 7, 8):
+                out[i] = out[i] * m[:, None]
+            out[6] = out[6] * m[:, None, None]
+        return tuple(out)
 
     def mark_visible(self, *args):
         return torch.ones(args[0].shape[0], dtype=torch.bool)

@@ -42,7 +42,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_sizes():
     L = _lib.load()
-    assert L.gs_version() == 1
+    assert L.gs_version() == _lib.ABI_VERSION == 2
     assert L.gs_geom_buffer_bytes(0) > 0
     for a, b in [(1000, 2000), (10_000, 300_000)]:
         assert L.gs_geom_buffer_bytes(b) > L.gs_geom_buffer_bytes(a)

@@ -16,7 +16,7 @@ import pytest
 import torch
 
 from tests import _harness as H
-from dynamic3dgaussians_amd import _lib
+from dynamic3dgaussians_amd import _C, _lib
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -230,3 +230,52 @@ def test_prefiltered_error():
     with pytest.raises(_lib.GsplatError, match="prefiltered"):
         from dynamic3dgaussians_amd import _C
         _C.rasterize_gaussians(*args)
+
+
+# ------------------------------------------------------- fused label mask (Q12)
+
+@pytest.mark.parametrize("use_sh", [False, True])
+def test_fused_label_mask_matches_wrapper_mask(use_sh):
+    """The label mask fused into preprocess_bwd equals the reference
+    wrapper's `grad * label.unsqueeze(1)` (__init__.py:159-173): a single fp32
+    multiply of the same value, so bit-identical up to backward's atomic order."""
+    inp = H.scene(F=32, use_sh=use_sh, sh_degree=2 if use_sh else 0)
+    P = inp["means3D"].size(0)
+    g = torch.Generator().manual_seed(3)
+    label = (torch.rand(P, generator=g) > 0.3).float() * torch.rand(P, generator=g).add(0.5)
+    fwd = H.gpu_forward(inp)
+    grads = H.upstream_grads(inp["image_height"], inp["image_width"], 32)
+    plain = H.gpu_backward(inp, fwd, grads)
+    num_rendered, color, feat, depth, alpha, radii, geom, binning, img = fwd
+    dc, df, dd, da = [t.to(H.DEV) for t in grads]
+    d = lambda k: H._to(inp[k], H.DEV)  # noqa: E731
+    fused = _C.rasterize_gaussians_backward(
+        d("bg"), d("means3D"), radii, d("colors"), d("semantic_feature"), d("scales"),
+        d("rotations"), 1.0, d("cov3D_precomp"), d("viewmatrix"), d("projmatrix"),
+        *H.bwd_cam4(inp, True), dc, df, dd, da, d("sh"), inp["degree"], d("campos"), geom,
+        num_rendered, binning, img, alpha, False, grad_mask=label.to(H.DEV))
+    fused = [t.cpu() for t in fused]
+    # The two backward runs differ only by fp32 atomic ordering, so compare at
+    # that tolerance; rows with label 0 must be exactly zero.
+    zero = label == 0
+    for i, name in enumerate(GRAD_NAMES):
+        ref = torch.from_numpy(plain[i])
+        if name not in ("dmeans2D", "dsemantic"):
+            ref = ref * (label[:, None, None] if ref.dim() == 3 else label[:, None])
+            if fused[i].numel():
+                assert fused[i][zero].abs().max().item() == 0.0, name
+        if ref.abs().max().item() > 0:
+            assert H.rel_l2(fused[i].numpy(), ref.numpy()) <= 1e-5, name
+        else:
+            assert fused[i].abs().max().item() == 0.0, name
+
+
+def test_reference_mode_alpha_is_zero():
+    """Q1: out_alpha of the reference is never written -> zeros (the kernel
+    stores them, so a recycled allocation cannot leak through)."""
+    inp = H.scene(F=0)
+    junk = torch.full((1, 96, 128), 7.0, device=H.DEV)  # dirty the caching allocator
+    del junk
+    assert H.gpu_forward(inp, "reference")[4].abs().sum().item() == 0
+    a = H.gpu_forward(inp, "fixed")[4]
+    assert a.max().item() > 0.5
