@@ -161,7 +161,8 @@ def rasterize_gaussians(background, means3D, colors, semantic_feature, opacity, 
     stream = _stream(dev)
     L = ctypes.c_int64(0)
     check(L_.gs_forward_plan(ctypes.byref(g), ctypes.byref(cam), int(bool(prefiltered)),
-                             int(bool(debug)), cm, geom.data_ptr(), radii.data_ptr(), ctypes.byref(L),
+                             int(bool(debug)), cm, geom.data_ptr(), img.data_ptr(), radii.data_ptr(),
+                             ctypes.byref(L),
                              stream), "rasterize_gaussians (preprocess)")
     num_rendered = int(L.value)
     binning = torch.empty(L_.gs_binning_buffer_bytes(num_rendered), **u8)

@@ -24,6 +24,13 @@ INCLUDE = os.path.join(REPO, "include")
 OUT_DIR = os.path.join(PKG, "lib")
 BUILD_DIR = os.path.join(OUT_DIR, "obj")
 LIB = os.path.join(OUT_DIR, "libgsplat_hip.so")
+# Build variants: "" = the product library; "stats" adds the blend kernels'
+# work counters (-DGS_STATS, tools/render_stats.py only).
+VARIANT = os.environ.get("GSPLAT_VARIANT", "")
+if VARIANT:
+    LIB = os.path.join(OUT_DIR, f"libgsplat_hip_{VARIANT}.so")
+    BUILD_DIR = os.path.join(OUT_DIR, f"obj_{VARIANT}")
+VARIANT_FLAGS = {"": [], "stats": ["-DGS_STATS"]}
 ARCH = os.environ.get("GSPLAT_OFFLOAD_ARCH", "gfx950")
 
 # Per-file flags.  The preprocess kernels are compiled without FMA
@@ -31,6 +38,7 @@ ARCH = os.environ.get("GSPLAT_OFFLOAD_ARCH", "gfx950")
 SOURCES = {
     "gs_preprocess.hip": ["-ffp-contract=off"],
     "gs_binning.hip": [],
+    "gs_tiles.hip": [],
     "gs_render.hip": [],
     "gs_api.hip": [],
 }
@@ -68,7 +76,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     def compile_one(item):
         src, extra = item
         obj = os.path.join(BUILD_DIR, src.replace(".hip", ".o"))
-        cmd = [cc, *COMMON, *extra, "-c", os.path.join(CSRC, src), "-o", obj]
+        cmd = [cc, *COMMON, *VARIANT_FLAGS[VARIANT], *extra, "-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)

@@ -53,18 +53,6 @@ int higher_msb(uint32_t n) {  // getHigherMsb, CR/rasterizer_impl.cu:35-50
   return (int)msb;
 }
 
-// Sort bit ranges: the depth sort uses the 31 bits of a positive float; the
-// instance sort only the tile id (getHigherMsb(tiles) bits, the reference's
-// 32 + msb minus the depth bits already ordered by the depth sort).
-constexpr int DEPTH_BITS = 31;
-int tile_bits(int W, int H) {
-  const int gx = (W + TILE - 1) / TILE, gy = (H + TILE - 1) / TILE;
-  return higher_msb((uint32_t)(gx * gy));
-}
-// Which ping-pong slot holds the sorted pairs: every 8-bit pass swaps slots.
-int slot_after(int64_t n, int end_bit) { return n <= 1 ? 0 : ((end_bit + 7) / 8) & 1; }
-int sorted_slot(int64_t L, int W, int H) { return slot_after(L, tile_bits(W, H)); }
-
 template <class T>
 T* at(void* base, size_t off) { return reinterpret_cast<T*>(static_cast<char*>(base) + off); }
 template <class T>
@@ -133,6 +121,30 @@ struct StageTimer {
     g_events.push_back({a, b, kind});
   }
 };
+// The plan's header as read back by gs_forward_plan, remembered per thread so
+// that gs_forward_render can size its sort launch without another readback.
+struct PlanInfo {
+  const void* image = nullptr;
+  int64_t L = -1;
+  int64_t max_len = -1;
+};
+thread_local PlanInfo g_plan;
+
+TileArgs tile_args(int P, int W, int H, void* geom, void* image) {
+  TileArgs t{};
+  const GeomLayout gl(P);
+  const ImgLayout il(W, H);
+  t.P = P; t.W = W; t.H = H;
+  t.grid_x = (W + TILE - 1) / TILE; t.grid_y = (H + TILE - 1) / TILE;
+  t.num_tiles = (int)il.tiles;
+  t.rect = at<uint16_t>(geom, gl.rect);
+  t.rec = at<float>(geom, gl.rec);
+  t.thist = at<uint32_t>(image, il.thist);
+  t.ttotal = at<uint32_t>(image, il.ttotal);
+  t.meta = at<uint32_t>(image, il.meta);
+  t.ranges = at<uint2>(image, il.ranges);
+  return t;
+}
 }  // namespace
 
 extern "C" {
@@ -172,19 +184,21 @@ size_t gs_backward_scratch_bytes(int64_t P, int32_t F) {
 }
 
 int gs_forward_plan(const gs_gaussians* g, const gs_camera* cam, int prefiltered, int debug, int compat,
-                    void* geom, int32_t* radii, int64_t* num_rendered, gs_stream_t stream) {
+                    void* geom, void* image, int32_t* radii, int64_t* num_rendered, gs_stream_t stream) {
   if (int e = check_gaussians(g, cam, true)) return e;
   if (!num_rendered) return fail(-1, "num_rendered is null");
   *num_rendered = 0;
+  g_plan = PlanInfo{};
   const int P = g->P;
   if (P == 0) return 0;
-  if (!geom || !radii) return fail(-1, "geom buffer and radii are required");
+  if (!geom || !image || !radii) return fail(-1, "geom buffer, image buffer and radii are required");
   hipStream_t s = (hipStream_t)stream;
   const GeomLayout gl(P);
   const int W = cam->image_width, H = cam->image_height;
+  const TileArgs ta = tile_args(P, W, H, geom, image);
   PreprocessArgs a{};
   a.P = P; a.D = g->D; a.M = g->M; a.W = W; a.H = H;
-  a.grid_x = (W + TILE - 1) / TILE; a.grid_y = (H + TILE - 1) / TILE;
+  a.grid_x = ta.grid_x; a.grid_y = ta.grid_y;
   a.prefiltered = prefiltered;
   a.means3D = g->means3D; a.scales = g->scales; a.rotations = g->rotations; a.opacities = g->opacities;
   a.shs = g->shs; a.cov3D_precomp = g->cov3D_precomp; a.colors_precomp = g->colors_precomp;
@@ -198,40 +212,32 @@ int gs_forward_plan(const gs_gaussians* g, const gs_camera* cam, int prefiltered
   a.cov3D = at<float>(geom, gl.cov3D);
   a.clamped = at<uint8_t>(geom, gl.clamped);
   a.tiles = at<uint32_t>(geom, gl.tiles);
-  a.status = at<int>(geom, gl.status);
-  (void)hipMemsetAsync(a.status, 0, 16, s);
+  a.rect = at<uint16_t>(geom, gl.rect);
+  a.status = reinterpret_cast<int*>(ta.meta + M_STATUS);
+  if (prefiltered) (void)hipMemsetAsync(a.status, 0, 4, s);  // culled-but-prefiltered flag
   {
     StageTimer t(s, GS_STAGE_PREPROCESS);
     launch_preprocess_fwd(a, s);
   }
   if (int e = check("preprocess", debug, s)) return e;
-  uint32_t* offsets = at<uint32_t>(geom, gl.offsets);
-  {
-    // stable depth order of the Gaussians (ties: index order)
-    StageTimer t(s, GS_STAGE_SORT);
-    uint32_t* dk0 = at<uint32_t>(geom, gl.dkeys0);
-    uint32_t* dk1 = at<uint32_t>(geom, gl.dkeys1);
-    uint32_t* o0 = at<uint32_t>(geom, gl.order0);
-    uint32_t* o1 = at<uint32_t>(geom, gl.order1);
-    launch_depth_keys(P, a.rec, radii, dk0, o0, s);
-    launch_radix_sort32(P, dk0, o0, dk1, o1, at<uint32_t>(geom, gl.dhist), at<uint32_t>(geom, gl.drowtot),
-                        DEPTH_BITS, s);
-  }
-  const uint32_t* order = at<uint32_t>(geom, slot_after(P, DEPTH_BITS) ? gl.order1 : gl.order0);
   {
     StageTimer t(s, GS_STAGE_SCAN);
-    launch_scan(a.tiles, order, offsets, at<uint32_t>(geom, gl.blocksums), P, s);
+    launch_tile_plan(ta, prefiltered, s);
   }
-  if (int e = check("scan", debug, s)) return e;
+  if (int e = check("tile plan", debug, s)) return e;
   // The one host read of the forward (CR/rasterizer_impl.cu:287): the total
-  // instance count sizes the binning buffer.  The status word rides along.
-  uint32_t host[2] = {0, 0};
-  hipError_t he = hipMemcpyAsync(&host[0], offsets + P - 1, 4, hipMemcpyDeviceToHost, s);
-  if (he == hipSuccess) he = hipMemcpyAsync(&host[1], a.status, 4, hipMemcpyDeviceToHost, s);
+  // instance count sizes the binning buffer; the rest of the header rides along.
+  uint32_t host[4] = {0, 0, 0, 0};
+  hipError_t he = hipMemcpyAsync(host, ta.meta, sizeof(host), hipMemcpyDeviceToHost, s);
   if (he == hipSuccess) he = hipStreamSynchronize(s);
   if (he != hipSuccess) return fail((int)he, "num_rendered readback: %s", hipGetErrorString(he));
-  if (host[1]) return fail(-2, "Point is filtered although prefiltered is set. This shouldn't happen!");
-  *num_rendered = host[0];
+  if (prefiltered && (host[M_STATUS] & 1u))
+    return fail(-2, "Point is filtered although prefiltered is set. This shouldn't happen!");
+  if (host[M_STATUS] & 2u) return fail(-1, "more than 2^32 tile instances");
+  *num_rendered = host[M_L];
+  g_plan.image = image;
+  g_plan.L = host[M_L];
+  g_plan.max_len = host[M_MAXN];
   (void)compat;
   return 0;
 }
@@ -252,36 +258,25 @@ int gs_forward_render(const gs_gaussians* g, const gs_camera* cam, int debug, in
   const BinLayout bl(L);
   const ImgLayout il(W, H);
   const float* rec = at<float>(geom, gl.rec);
-  uint2* ranges = at<uint2>(image, il.ranges);
-  const uint32_t* point_list = nullptr;
-  const uint32_t* sorted_keys = nullptr;
+  TileArgs ta = tile_args(P, W, H, geom, image);
+  ta.keys = L > 0 ? at<uint64_t>(binning, bl.keys) : nullptr;
+  ta.keys2 = L > 0 ? at<uint64_t>(binning, bl.keys2) : nullptr;
+  ta.plist = L > 0 ? at<uint32_t>(binning, bl.plist) : nullptr;
+  const uint2* ranges = ta.ranges;
+  const uint32_t* point_list = ta.plist;
   if (L > 0) {
-    uint32_t* k0 = at<uint32_t>(binning, bl.keys0);
-    uint32_t* k1 = at<uint32_t>(binning, bl.keys1);
-    uint32_t* v0 = at<uint32_t>(binning, bl.vals0);
-    uint32_t* v1 = at<uint32_t>(binning, bl.vals1);
-    const uint32_t* order = at<uint32_t>(geom, slot_after(P, DEPTH_BITS) ? gl.order1 : gl.order0);
     {
       StageTimer t(s, GS_STAGE_DUPLICATE);
-      launch_duplicate_sorted(P, order, rec, at<uint32_t>(geom, gl.offsets), radii, gx, gy, k0, v0, s);
+      launch_tile_bucket(ta, s);
     }
     if (int e = check("duplicateWithKeys", debug, s)) return e;
-    int which;
+    const bool known = g_plan.image == image && g_plan.L == L;
     {
       StageTimer t(s, GS_STAGE_SORT);
-      which = launch_radix_sort32(L, k0, v0, k1, v1, at<uint32_t>(binning, bl.hist),
-                                  at<uint32_t>(binning, bl.rowtot), tile_bits(W, H), s);
+      launch_tile_sort(ta, known ? g_plan.max_len : -1, s);
     }
-    if (int e = check("radix sort", debug, s)) return e;
-    if (which != sorted_slot(L, W, H)) return fail(-3, "internal: sort slot mismatch");
-    sorted_keys = which ? k1 : k0;
-    point_list = which ? v1 : v0;
+    if (int e = check("tile sort", debug, s)) return e;
   }
-  {
-    StageTimer t(s, GS_STAGE_RANGES);
-    launch_tile_ranges(L, sorted_keys, ranges, gx * gy, s);
-  }
-  if (int e = check("identifyTileRanges", debug, s)) return e;
   RenderArgs ra{};
   ra.W = W; ra.H = H; ra.grid_x = gx; ra.num_tiles = gx * gy; ra.F = g->F; ra.compat = compat;
   ra.ranges = ranges; ra.point_list = point_list; ra.rec = rec; ra.feats = g->semantic_feature;
@@ -322,7 +317,7 @@ int gs_backward(const gs_gaussians* g, const gs_camera* cam, const int32_t* radi
   RenderBwdArgs ra{};
   ra.W = W; ra.H = H; ra.grid_x = gx; ra.num_tiles = gx * gy; ra.F = g->F; ra.compat = compat;
   ra.ranges = at<uint2>(image, il.ranges);
-  ra.point_list = L > 0 ? at<uint32_t>(binning, sorted_slot(L, W, H) ? bl.vals1 : bl.vals0) : nullptr;
+  ra.point_list = L > 0 ? at<uint32_t>(binning, bl.plist) : nullptr;
   ra.rec = at<float>(geom, gl.rec);
   ra.feats = g->semantic_feature;
   ra.bg = cam->background;
@@ -392,7 +387,7 @@ int gs_debug_export(int64_t P, int32_t W, int32_t H, const void* geom, const voi
   if (tiles_touched && P > 0 && e == hipSuccess)
     e = hipMemcpyAsync(tiles_touched, at<uint32_t>(geom, gl.tiles), 4 * P, hipMemcpyDeviceToDevice, s);
   if (point_list && L > 0 && e == hipSuccess)
-    e = hipMemcpyAsync(point_list, at<uint32_t>(binning, sorted_slot(L, W, H) ? bl.vals1 : bl.vals0), 4 * L,
+    e = hipMemcpyAsync(point_list, at<uint32_t>(binning, bl.plist), 4 * L,
                        hipMemcpyDeviceToDevice, s);
   const int64_t tiles = (int64_t)((W + TILE - 1) / TILE) * ((H + TILE - 1) / TILE);
   if (ranges && e == hipSuccess)
@@ -403,20 +398,17 @@ int gs_debug_export(int64_t P, int32_t W, int32_t H, const void* geom, const voi
   return 0;
 }
 
-size_t gs_sort_scratch_bytes(int64_t n) {
-  const BinLayout bl(n, 8);
-  return bl.total;
-}
+size_t gs_sort_scratch_bytes(int64_t n) { return SortLayout(n > 0 ? n : 0).total; }
 
 int gs_sort_pairs(int64_t n, uint64_t* keys, uint32_t* vals, int end_bit, void* scratch, gs_stream_t stream) {
   if (n < 0 || end_bit < 0 || end_bit > 64) return fail(-1, "bad sort arguments");
   if (n <= 1) return 0;
   hipStream_t s = (hipStream_t)stream;
-  const BinLayout bl(n, 8);
-  uint64_t* k1 = at<uint64_t>(scratch, bl.keys1);
-  uint32_t* v1 = at<uint32_t>(scratch, bl.vals1);
-  const int which = launch_radix_sort(n, keys, vals, k1, v1, at<uint32_t>(scratch, bl.hist),
-                                      at<uint32_t>(scratch, bl.rowtot), end_bit, s);
+  const SortLayout sl(n);
+  uint64_t* k1 = at<uint64_t>(scratch, sl.keys1);
+  uint32_t* v1 = at<uint32_t>(scratch, sl.vals1);
+  const int which = launch_radix_sort(n, keys, vals, k1, v1, at<uint32_t>(scratch, sl.hist),
+                                      at<uint32_t>(scratch, sl.rowtot), end_bit, s);
   if (which) {
     (void)hipMemcpyAsync(keys, k1, 8 * n, hipMemcpyDeviceToDevice, s);
     (void)hipMemcpyAsync(vals, v1, 4 * n, hipMemcpyDeviceToDevice, s);

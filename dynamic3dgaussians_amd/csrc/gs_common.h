@@ -53,58 +53,72 @@ __host__ __device__ inline int64_t sort_blocks(int64_t n) {
   const int64_t tile = (int64_t)SORT_THREADS * sort_rounds(n);
   return (n + tile - 1) / tile;
 }
+// Tile bucketing geometry (gs_tiles.hip): TB_BLOCKS workgroups each own a
+// contiguous slice of the Gaussians and histogram their instances over (a
+// range of at most TB_BINS) tiles in LDS.
+constexpr int TB_BLOCKS = 256;
+constexpr int TB_THREADS = 512;
+constexpr int TB_BINS = 16384;    // LDS tile bins per pass (64 KiB)
+constexpr int TS_CAP = 3584;      // per-tile LDS sort capacity (2 x 28 KiB of u64 keys)
+constexpr int TS_THREADS = 256;
+
 // Geometry buffer (per-Gaussian state kept from forward to backward).
 struct GeomLayout {
-  static constexpr int SCAN_ITEMS = 2048;  // items per scan block
-  size_t rec, cov3D, clamped, tiles, offsets, blocksums, status;
-  size_t dkeys0, dkeys1, order0, order1, dhist, drowtot, total;
+  size_t rec, cov3D, clamped, tiles, rect, total;
   __host__ __device__ GeomLayout(int64_t P) {
-    const int64_t nblk = sort_blocks(P);
     size_t o = 0;
     rec = o;       o = align_up(o + sizeof(float) * REC * P, 256);
     cov3D = o;     o = align_up(o + sizeof(float) * 6 * P, 256);
     clamped = o;   o = align_up(o + P, 256);
     tiles = o;     o = align_up(o + sizeof(uint32_t) * P, 256);
-    offsets = o;   o = align_up(o + sizeof(uint32_t) * P, 256);
-    blocksums = o; o = align_up(o + sizeof(uint32_t) * ((P + SCAN_ITEMS - 1) / SCAN_ITEMS + 1), 256);
-    status = o;    o = align_up(o + 64, 256);
-    dkeys0 = o;    o = align_up(o + sizeof(uint32_t) * P, 256);
-    dkeys1 = o;    o = align_up(o + sizeof(uint32_t) * P, 256);
-    order0 = o;    o = align_up(o + sizeof(uint32_t) * P, 256);
-    order1 = o;    o = align_up(o + sizeof(uint32_t) * P, 256);
-    dhist = o;     o = align_up(o + sizeof(uint32_t) * 256 * (nblk > 0 ? nblk : 1), 256);
-    drowtot = o;   o = align_up(o + sizeof(uint32_t) * 256, 256);
+    rect = o;      o = align_up(o + sizeof(uint16_t) * 4 * P, 256);  // tile rect x0,y0,x1,y1
     total = o;
   }
 };
 
-// Binning buffer (per tile/Gaussian instance): ping-pong (tile key, id)
-// arrays of the radix sort.  key_bytes = 4 for the binning (tile ids), 8 for
-// the standalone 64-bit sort entry point.
+// Binning buffer (per tile/Gaussian instance): the (depth bits, id) keys in
+// tile-bucket order and the per-tile sorted id list the blend kernels read.
 struct BinLayout {
-  size_t keys0, keys1, vals0, vals1, hist, rowtot, total;
-  int64_t nblk;
-  __host__ __device__ BinLayout(int64_t L, int key_bytes = 4) {
-    nblk = sort_blocks(L);
+  size_t keys, keys2, plist, total;
+  __host__ __device__ BinLayout(int64_t L) {
     size_t o = 0;
-    keys0 = o; o = align_up(o + (size_t)key_bytes * L, 256);
-    keys1 = o; o = align_up(o + (size_t)key_bytes * L, 256);
-    vals0 = o; o = align_up(o + sizeof(uint32_t) * L, 256);
-    vals1 = o; o = align_up(o + sizeof(uint32_t) * L, 256);
+    keys = o;  o = align_up(o + sizeof(uint64_t) * L, 256);
+    keys2 = o; o = align_up(o + sizeof(uint64_t) * L, 256);  // radix twin of long tiles
+    plist = o; o = align_up(o + sizeof(uint32_t) * L, 256);
+    total = o;
+  }
+};
+
+// Scratch of the standalone radix sort entry point (gs_sort_pairs).
+struct SortLayout {
+  size_t keys1, vals1, hist, rowtot, total;
+  __host__ __device__ SortLayout(int64_t n) {
+    const int64_t nblk = sort_blocks(n);
+    size_t o = 0;
+    keys1 = o; o = align_up(o + sizeof(uint64_t) * n, 256);
+    vals1 = o; o = align_up(o + sizeof(uint32_t) * n, 256);
     hist = o;  o = align_up(o + sizeof(uint32_t) * 256 * (nblk > 0 ? nblk : 1), 256);
     rowtot = o; o = align_up(o + sizeof(uint32_t) * 256, 256);
     total = o;
   }
 };
 
-// Image buffer (per pixel / per tile).
+// Image buffer (per pixel / per tile), also the binning plan: per-block tile
+// histograms (turned into per-block offsets), tile totals and a 4-word
+// header {L, max tile length, -, status}.
+enum ImgMeta { M_L = 0, M_MAXN = 1, M_RSVD = 2, M_STATUS = 3 };
 struct ImgLayout {
-  size_t ranges, n_contrib, total;
+  size_t ranges, n_contrib, thist, ttotal, meta, total;
+  int64_t tiles;
   __host__ __device__ ImgLayout(int W, int H) {
-    const int64_t tiles = (int64_t)((W + TILE - 1) / TILE) * ((H + TILE - 1) / TILE);
+    tiles = (int64_t)((W + TILE - 1) / TILE) * ((H + TILE - 1) / TILE);
+    const int64_t t = tiles > 0 ? tiles : 1;
     size_t o = 0;
-    ranges = o;    o = align_up(o + sizeof(uint32_t) * 2 * (tiles > 0 ? tiles : 1), 256);
+    ranges = o;    o = align_up(o + sizeof(uint32_t) * 2 * t, 256);
     n_contrib = o; o = align_up(o + sizeof(uint32_t) * (int64_t)W * H, 256);
+    thist = o;     o = align_up(o + sizeof(uint32_t) * TB_BLOCKS * t, 256);
+    ttotal = o;    o = align_up(o + sizeof(uint32_t) * t, 256);
+    meta = o;      o = align_up(o + sizeof(uint32_t) * 4, 256);
     total = o;
   }
 };

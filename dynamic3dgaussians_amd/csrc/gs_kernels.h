@@ -24,6 +24,7 @@ struct PreprocessArgs {
   float* cov3D;
   uint8_t* clamped;
   uint32_t* tiles;
+  uint16_t* rect;  // P x 4: tile rect [x0, x1) x [y0, y1) (empty when culled)
   int* status;
 };
 
@@ -88,20 +89,31 @@ void launch_preprocess_fwd(const PreprocessArgs& a, hipStream_t s);
 void launch_preprocess_bwd(const PreprocessBwdArgs& a, hipStream_t s);
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t s);
 
-// Binning: inclusive scan of in[perm[i]] (perm may be null) into out, block sums in tmp.
-void launch_scan(const uint32_t* in, const uint32_t* perm, uint32_t* out, uint32_t* tmp, int P, hipStream_t s);
-// Stable LSD radix sorts on bits [0, end_bit); the result ends in keys0/vals0
-// or keys1/vals1 -- returns 0 or 1 for which (passes of 8 bits swap slots).
+// Stable LSD radix sort on bits [0, end_bit) (the standalone gs_sort_pairs
+// entry point); the result ends in keys0/vals0 or keys1/vals1 -- returns 0
+// or 1 for which (passes of 8 bits swap slots).
 int launch_radix_sort(int64_t n, uint64_t* keys0, uint32_t* vals0, uint64_t* keys1, uint32_t* vals1,
                       uint32_t* hist, uint32_t* rowtot, int end_bit, hipStream_t s);
-int launch_radix_sort32(int64_t n, uint32_t* keys0, uint32_t* vals0, uint32_t* keys1, uint32_t* vals1,
-                        uint32_t* hist, uint32_t* rowtot, int end_bit, hipStream_t s);
-void launch_depth_keys(int P, const float* rec, const int* radii, uint32_t* keys, uint32_t* vals,
-                       hipStream_t s);
-void launch_duplicate_sorted(int P, const uint32_t* order, const float* rec, const uint32_t* offsets,
-                             const int* radii, int grid_x, int grid_y, uint32_t* keys, uint32_t* vals,
-                             hipStream_t s);
-void launch_tile_ranges(int64_t L, const uint32_t* keys, uint2* ranges, int num_tiles, hipStream_t s);
+
+// Tile binning (gs_tiles.hip).
+struct TileArgs {
+  int P, W, H, grid_x, grid_y, num_tiles;
+  const uint16_t* rect;  // P x 4
+  const float* rec;      // P x REC (depth)
+  uint32_t* thist;       // TB_BLOCKS x num_tiles
+  uint32_t* ttotal;      // num_tiles
+  uint32_t* meta;        // 4
+  uint2* ranges;         // num_tiles
+  uint64_t* keys;        // L
+  uint64_t* keys2;       // L (sort twin for long tiles)
+  uint32_t* plist;       // L
+};
+// plan: per-block tile histograms, tile totals and offsets, ranges, header
+void launch_tile_plan(const TileArgs& a, int prefiltered, hipStream_t s);
+// render: bucket the instances by tile, then sort every tile by (depth, id).
+// max_len = the plan header's longest tile (host copy), or -1 if unknown.
+void launch_tile_bucket(const TileArgs& a, hipStream_t s);
+void launch_tile_sort(const TileArgs& a, int64_t max_len, hipStream_t s);
 
 bool launch_render_fwd(const RenderArgs& a, hipStream_t s);
 bool launch_render_bwd(const RenderBwdArgs& a, hipStream_t s);

@@ -166,6 +166,7 @@ __global__ __launch_bounds__(256) void preprocess_fwd_kernel(PreprocessArgs a) {
   if (g >= a.P) return;
   a.radii[g] = 0;
   a.tiles[g] = 0;
+  reinterpret_cast<ushort4*>(a.rect)[g] = make_ushort4(0, 0, 0, 0);
   const V3 p = ld3(a.means3D + 3 * g);
   const V3 pv = xf43(a.view, p);
   if (pv.z <= 0.0f) {  // in_frustum, Q8
@@ -231,6 +232,8 @@ __global__ __launch_bounds__(256) void preprocess_fwd_kernel(PreprocessArgs a) {
   rec[3] = make_float4((float)rad, 0.f, 0.f, 0.f);
   a.radii[g] = (int)rad;
   a.tiles[g] = (uint32_t)((rmax.y - rmin.y) * (rmax.x - rmin.x));
+  reinterpret_cast<ushort4*>(a.rect)[g] =
+      make_ushort4((uint16_t)rmin.x, (uint16_t)rmin.y, (uint16_t)rmax.x, (uint16_t)rmax.y);
 }
 
 void launch_preprocess_fwd(const PreprocessArgs& a, hipStream_t s) {
@@ -359,7 +362,9 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdArgs a
   const float* acc = a.acc + (size_t)A_FEAT * g;
   const bool vis = a.radii[g] > 0;
   // blend gradients -> output tensors (zero for culled Gaussians: never touched)
-  const float am0 = acc[A_MX], am1 = acc[A_MY];
+  // the blend kernel accumulates dL/d(pixel offset); the ndc scale
+  // ddelx_dx = 0.5 W, ddely_dy = 0.5 H (CR/backward.cu:520-521) is applied once here
+  const float am0 = acc[A_MX] * (0.5f * (float)a.W), am1 = acc[A_MY] * (0.5f * (float)a.H);
   a.dmeans2D[3 * g] = am0; a.dmeans2D[3 * g + 1] = am1; a.dmeans2D[3 * g + 2] = 0.f;
   const float dcol[3] = {acc[A_R], acc[A_G], acc[A_B]};
   // Q12 label mask (DGR/__init__.py:159-173), applied at store time exactly as

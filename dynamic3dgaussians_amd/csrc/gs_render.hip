@@ -34,6 +34,32 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 __device__ inline bool wave_any(bool p) { return __ballot(p) != 0ull; }
 
+// Work counters for kernel tuning (tools/render_stats.py); compiled only into
+// the "stats" build variant (-DGS_STATS), never into the product library.
+#ifdef GS_STATS
+__device__ unsigned long long g_stats[32];
+#define STAT(i, n)                                                               \
+  do {                                                                           \
+    const unsigned long long n_ = (unsigned long long)(n);                       \
+    if ((threadIdx.x & 63) == 0) atomicAdd(&g_stats[i], n_);                     \
+  } while (0)
+#define STAT_DECL(v) unsigned long long v = 0
+#define STAT_INC(v) (++v)
+#define STAT_WAVE(i_max, i_hist, v)                                              \
+  do {                                                                           \
+    if ((threadIdx.x & 63) == 0) {                                               \
+      atomicMax(&g_stats[i_max], v);                                             \
+      const int b_ = v < 256 ? 0 : v < 512 ? 1 : v < 1024 ? 2 : v < 2048 ? 3 : 4; \
+      atomicAdd(&g_stats[i_hist + b_], 1ull);                                    \
+    }                                                                            \
+  } while (0)
+#else
+#define STAT(i, n) ((void)0)
+#define STAT_DECL(v) ((void)0)
+#define STAT_INC(v) ((void)0)
+#define STAT_WAVE(i_max, i_hist, v) ((void)0)
+#endif
+
 // exp(x) as one v_exp_f32 (2^x) on x*log2(e): ~3 ulp instead of libm's
 // correctly-rounded-ish 14-instruction sequence.  Forward and backward use
 // the same function, so their alpha decisions agree bit for bit.
@@ -53,21 +79,23 @@ __device__ inline void swap32(float a, float b, float& lo, float& hi) {
   hi = bits_f(r[1]);
 }
 
-// Gather the record of the chunk's lane-th Gaussian (rec fields 0..11).
+// Gather the record of list entry i (fields 0..11).  The index is clamped to
+// the last entry of the (non-empty) range, so the loads are unconditional:
+// lanes past the end re-read a valid record and are masked out by the caller.
+// (A conditional update of a register struct made the compiler keep it in
+// scratch memory.)
 struct RecRegs {
   float4 q0, q1, q2;
   uint32_t gid;
 };
 __device__ inline RecRegs load_rec(const uint32_t* __restrict__ point_list, const float* __restrict__ rec,
-                                   uint32_t i, bool ok, const RecRegs& prev) {
-  RecRegs r = prev;
-  if (ok) {
-    r.gid = point_list[i];
-    const float4* p = reinterpret_cast<const float4*>(rec + (size_t)r.gid * REC);
-    r.q0 = p[0];  // x, y, conic a, conic b
-    r.q1 = p[1];  // conic c, opacity, r, g
-    r.q2 = p[2];  // b, depth, ext x, ext y
-  }
+                                   uint32_t i, uint32_t last_valid) {
+  RecRegs r;
+  r.gid = point_list[i < last_valid ? i : last_valid];
+  const float4* p = reinterpret_cast<const float4*>(rec + (size_t)r.gid * REC);
+  r.q0 = p[0];  // x, y, conic a, conic b
+  r.q1 = p[1];  // conic c, opacity, r, g
+  r.q2 = p[2];  // b, depth, ext x, ext y
   return r;
 }
 
@@ -133,9 +161,13 @@ __global__ __launch_bounds__(256) void render_fwd_kernel(
     have_prev = 1;
   };
 
-  RecRegs q{};
-  q = load_rec(point_list, rec, range.x + lane, range.x + lane < range.y, q);
+  const uint32_t lastv = range.y > range.x ? range.y - 1 : range.x;
+  RecRegs q;
+  if (range.y > range.x) q = load_rec(point_list, rec, range.x + lane, lastv);
   bool all_done = !wave_any(!done);
+  STAT(6, 1);
+  STAT(7, range.y - range.x);
+  STAT_DECL(st_it);
   for (uint32_t c0 = range.x; c0 < range.y && !all_done; c0 += CHUNK) {
     const bool keep = (c0 + lane < range.y) && !strip_culled(q, sx0, sx1, sy0, sy1);
     s_rec[wave][lane][0] = q.q0;
@@ -143,10 +175,15 @@ __global__ __launch_bounds__(256) void render_fwd_kernel(
     s_rec[wave][lane][2] = q.q2;
     s_gid[wave][lane] = q.gid;
     uint64_t mask = __ballot(keep);
-    q = load_rec(point_list, rec, c0 + CHUNK + lane, c0 + CHUNK + lane < range.y, q);  // prefetch
+    STAT(0, 1);
+    STAT(1, range.y - c0 < CHUNK ? range.y - c0 : CHUNK);
+    STAT(2, __builtin_popcountll(mask));
+    q = load_rec(point_list, rec, c0 + CHUNK + lane, lastv);  // prefetch (clamped)
     while (mask) {
       const int j = __builtin_ctzll(mask);
       mask &= mask - 1;
+      STAT(3, 1);
+      STAT_INC(st_it);
       const float4 r0 = s_rec[wave][j][0];
       const float4 r1 = s_rec[wave][j][1];
       const float4 r2 = s_rec[wave][j][2];
@@ -156,6 +193,8 @@ __global__ __launch_bounds__(256) void render_fwd_kernel(
       const float test_T = T * (1 - alpha);
       bool blend = !done && !(power > 0.0f) && !(alpha < ALPHA_MIN);
       if (blend && test_T < 0.0001f) { done = true; blend = false; }
+      STAT(4, wave_any(blend));
+      STAT(5, __builtin_popcountll(__ballot(blend)));
       if (wave_any(blend)) {
         const float w = blend ? alpha * T : 0.0f;
         if (blend) {
@@ -192,6 +231,7 @@ __global__ __launch_bounds__(256) void render_fwd_kernel(
       if (!wave_any(!done)) { all_done = true; break; }
     }
   }
+  STAT_WAVE(16, 20, st_it);
   if constexpr (MF) {
     if (pend) {
       float b0, b1, an[FB];
@@ -313,7 +353,6 @@ __global__ __launch_bounds__(256) void render_bwd_kernel(
   const float dLd = inside ? dL_ddepth[pix] : 0.f;
   const float dLa = inside ? dL_dalpha[pix] : 0.f;
   const float bg_dot = bg[0] * dLp[0] + bg[1] * dLp[1] + bg[2] * dLp[2];
-  const float ddelx_dx = 0.5f * (float)W, ddely_dy = 0.5f * (float)H;
 
   // Upstream feature gradients.  VALU path: one register per channel.
   // MFMA path: the B operands of dL/df = W . dLf, lane l / step s holding
@@ -338,17 +377,26 @@ __global__ __launch_bounds__(256) void render_bwd_kernel(
     for (int c = 0; c < NF_REG; ++c) dLf[c] = (F > 0 && inside) ? dL_dfeat[c * HW + pix] : 0.f;
   }
 
-  float ar0 = 0.f, ar1 = 0.f, ar2 = 0.f, lc0 = 0.f, lc1 = 0.f, lc2 = 0.f;
-  float ad = 0.f, ld = 0.f, aa = 0.f, la = 0.f;
-  float af = 0.f, lfd = 0.f;  // fixed mode: feature accum . dL/dfeature
-  int nb = 0;                 // MFMA batch fill
+  // The reference carries per-channel "accum_rec" recurrences
+  // (CR/backward.cu:560-615): for every channel k with colour c_k and upstream
+  // gradient g_k,  rec_k <- la*last_k + (1-la)*rec_k  and  dL/dalpha += (c_k -
+  // rec_k)*g_k.  Since g_k is fixed per pixel, only the dot products matter:
+  // with  cdot = sum_k c_k g_k  (colour, depth, alpha with c = 1, and in fixed
+  // mode the features) and  Q = sum_k rec_k g_k  the recurrence is
+  //   Q <- Q + la*(last_cdot - Q),   dL/dalpha = cdot - Q  -- the same value
+  // with fewer operations (fp32 reassociation only).
+  float Q = 0.f, lcd = 0.f, la = 0.f;
+  int nb = 0;  // MFMA batch fill
 
   const uint32_t wmax = __builtin_amdgcn_readfirstlane(wave_max_u(last));
   const uint32_t top = range.x + wmax;  // exclusive end of this wave's walk
-  RecRegs q{};
-  {
+  STAT(14, 1);
+  STAT(15, wmax);
+  STAT_DECL(st_it);
+  RecRegs q;
+  if (top > range.x) {
     const uint32_t c0 = top > range.x + CHUNK ? top - CHUNK : range.x;
-    q = load_rec(point_list, rec, c0 + lane, c0 + lane < top, q);
+    q = load_rec(point_list, rec, c0 + lane, top - 1);
   }
   for (uint32_t hi = top; hi > range.x;) {
     const uint32_t c0 = hi > range.x + CHUNK ? hi - CHUNK : range.x;
@@ -358,9 +406,12 @@ __global__ __launch_bounds__(256) void render_bwd_kernel(
     s_rec[wave][lane][2] = q.q2;
     s_gid[wave][lane] = q.gid;
     uint64_t mask = __ballot(keep);
+    STAT(8, 1);
+    STAT(9, hi - c0);
+    STAT(10, __builtin_popcountll(mask));
     {
       const uint32_t n0 = c0 > range.x + CHUNK ? c0 - CHUNK : range.x;
-      q = load_rec(point_list, rec, n0 + lane, n0 + lane < c0, q);  // prefetch the next (lower) chunk
+      q = load_rec(point_list, rec, n0 + lane, top - 1);  // prefetch the next (lower) chunk
     }
     while (mask) {
       const int j = 63 - __builtin_clzll(mask);
@@ -375,62 +426,58 @@ __global__ __launch_bounds__(256) void render_bwd_kernel(
       const float G = fast_exp(power);
       const float alpha = fminf(0.99f, op * G);
       const bool valid = (k < last) && !(power > 0.0f) && !(alpha < ALPHA_MIN);
+      STAT(11, 1);
+      STAT_INC(st_it);
+      STAT(12, wave_any(valid));
+      STAT(13, __builtin_popcountll(__ballot(valid)));
       if (!wave_any(valid)) continue;
       const uint32_t gid = __builtin_amdgcn_readfirstlane(s_gid[wave][j]);
-      float v[NV];
-#pragma unroll
-      for (int c = 0; c < NV; ++c) v[c] = 0.f;
-      float dch = 0.f;
+      // Invalid lanes keep dch = dL_dopa = Gv = 0, which zeroes every
+      // contribution below without per-component selects.
+      float dch = 0.f, dL_dopa = 0.f, Gv = 0.f;
       if (valid) {
         const float rinv = fast_rcp(1.f - alpha);
         T = T * rinv;
         dch = alpha * T;
-        float dL_dopa = 0.f;
-        const float c0v = r1.z, c1v = r1.w, c2v = r2.x;
-        ar0 = la * lc0 + (1.f - la) * ar0; lc0 = c0v; dL_dopa += (c0v - ar0) * dLp[0];
-        ar1 = la * lc1 + (1.f - la) * ar1; lc1 = c1v; dL_dopa += (c1v - ar1) * dLp[1];
-        ar2 = la * lc2 + (1.f - la) * ar2; lc2 = c2v; dL_dopa += (c2v - ar2) * dLp[2];
-        v[A_R] = dch * dLp[0]; v[A_G] = dch * dLp[1]; v[A_B] = dch * dLp[2];
-        const float cd = r2.y;
-        ad = la * ld + (1.f - la) * ad; ld = cd; dL_dopa += (cd - ad) * dLd;
-        if constexpr (F > 0) {
+        float cdot = fmaf(r2.y, dLd, fmaf(r2.x, dLp[2], fmaf(r1.w, dLp[1], r1.z * dLp[0]))) + dLa;
+        if constexpr (FIXED_FEAT) {
+          // fixed mode: the features feed dL/dalpha (Q5 fixed)
           const float* f = feats + (size_t)gid * F;
           float fd = 0.f;
-          if constexpr (!MF) {
+          if constexpr (MF) {
 #pragma unroll
-            for (int c = 0; c < NF_REG; ++c) {
-              v[A_FEAT + c] = dch * dLf[c];
-              if constexpr (FIXED_FEAT) fd += f[c] * dLf[c];
-            }
-          } else if constexpr (FIXED_FEAT) {
+            for (int c = 0; c < F; ++c) fd = fmaf(f[c], dLf_own[c], fd);
+          } else {
 #pragma unroll
-            for (int c = 0; c < F; ++c) fd += f[c] * dLf_own[c];
+            for (int c = 0; c < NF_REG; ++c) fd = fmaf(f[c], dLf[c], fd);
           }
-          // Q5: in the reference the feature term reads a never-written
-          // (zero) scratch and contributes nothing to dL/dalpha.
-          if constexpr (FIXED_FEAT) {
-            af = la * lfd + (1.f - la) * af;
-            lfd = fd;
-            dL_dopa += fd - af;
-          }
+          cdot += fd;
         }
-        v[A_DEPTH] = dch * dLd;
-        aa = la + (1.f - la) * aa;
-        dL_dopa += (1 - aa) * dLa;
-        dL_dopa *= T;
+        Q = fmaf(la, lcd - Q, Q);
+        dL_dopa = fmaf(-T_final * rinv, bg_dot, (cdot - Q) * T);
+        lcd = cdot;
         la = alpha;
-        dL_dopa += (-T_final * rinv) * bg_dot;
-        const float dL_dG = op * dL_dopa;
-        const float gdx = G * dx, gdy = G * dy;
-        const float dG_ddelx = -gdx * ca - gdy * cb;
-        const float dG_ddely = -gdy * cc - gdx * cb;
-        v[A_MX] = dL_dG * dG_ddelx * ddelx_dx;
-        v[A_MY] = dL_dG * dG_ddely * ddely_dy;
-        v[A_CA] = -0.5f * gdx * dx * dL_dG;
-        v[A_CB] = -0.5f * gdx * dy * dL_dG;
-        v[A_CC] = -0.5f * gdy * dy * dL_dG;
-        v[A_OP] = G * dL_dopa;
+        Gv = G;
       }
+      float v[NV];
+      v[A_R] = dch * dLp[0];
+      v[A_G] = dch * dLp[1];
+      v[A_B] = dch * dLp[2];
+      v[A_DEPTH] = dch * dLd;
+      if constexpr (!MF) {
+#pragma unroll
+        for (int c = 0; c < NF_REG; ++c) if (A_FEAT + c < NV) v[A_FEAT + c] = dch * dLf[c];
+      }
+      // dL/dG -> mean2D (scaled by 0.5W, 0.5H in preprocess_bwd) and conic
+      const float dL_dG = op * dL_dopa;
+      const float gdx = Gv * dx, gdy = Gv * dy;
+      v[A_MX] = dL_dG * fmaf(-gdx, ca, -gdy * cb);
+      v[A_MY] = dL_dG * fmaf(-gdy, cc, -gdx * cb);
+      const float hx = -0.5f * dL_dG * gdx, hy = -0.5f * dL_dG * gdy;
+      v[A_CA] = hx * dx;
+      v[A_CB] = hx * dy;
+      v[A_CC] = hy * dy;
+      v[A_OP] = Gv * dL_dopa;
       commit<NV>(v, acc + (size_t)A_FEAT * gid, dsem + (size_t)F * gid, lane);
       if constexpr (MF) {
         s_w[wave][nb][lane] = dch;
@@ -453,6 +500,7 @@ __global__ __launch_bounds__(256) void render_bwd_kernel(
     }
     hi = c0;
   }
+  STAT_WAVE(17, 25, st_it);
   if constexpr (MF) {
     if (nb > 0) {
       // rows >= nb hold stale weights; MFMA rows are independent, so they
@@ -523,6 +571,18 @@ bool launch_render_bwd(const RenderBwdArgs& a, hipStream_t s) {
     default: return false;
   }
 }
+
+#ifdef GS_STATS
+extern "C" int gs_stats_read(unsigned long long* out, int n) {
+  if (n > 32) n = 32;
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stats), sizeof(unsigned long long) * n, 0,
+                                  hipMemcpyDeviceToHost);
+}
+extern "C" int gs_stats_reset(void) {
+  static const unsigned long long z[32] = {0};
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_stats), z, sizeof(z), 0, hipMemcpyHostToDevice);
+}
+#endif
 
 // ------------------------------------------------------------------ self-test
 

@@ -1,0 +1,333 @@
+// gs_tiles.hip -- tile binning: every (tile, Gaussian) instance into its
+// tile's list, each list in (depth, Gaussian id) order.
+//
+// Reference: DGR/cuda_rasterizer/rasterizer_impl.cu:70-138 and :283-314
+// (duplicateWithKeys over an inclusive scan of tiles_touched, a global cub
+// radix sort of (tile << 32 | depth bits) keys on 32 + getHigherMsb(tiles)
+// bits, identifyTileRanges).  That sort is stable, so inside a tile the list
+// is ordered by depth bits with ties in Gaussian index order.
+//
+// MI355X design -- no global sort at all:
+//  1. plan   (tile_hist_kernel): TB_BLOCKS workgroups each histogram the
+//     instances of a contiguous slice of the Gaussians over the tiles in LDS
+//     and write one column of a [tile][block] count matrix;
+//     (tile_rowscan_kernel) turns every row into per-block offsets inside
+//     the tile and a tile total; (tile_offsets_kernel, one workgroup) scans
+//     the totals into ranges[tile], finds the longest tile and lists tiles
+//     too long for the LDS sort.  Its header {L, max length, #long tiles}
+//     is the one device->host read of the forward (the reference's
+//     num_rendered read, :287).
+//  2. bucket (tile_hist_kernel<WRITE>): the same walk, each instance taking
+//     a slot from an LDS cursor, writes a 64-bit (depth bits << 32 | id) key
+//     into its tile's segment -- the order inside a segment is arbitrary.
+//  3. sort   (tile_sort_kernel): one workgroup per tile sorts its segment by
+//     depth bits with an LDS radix sort (wave-owned quarters, ballot-matched
+//     stable scatter, skipped constant-digit passes) and orders equal depths
+//     by id -- exactly the reference's stable order -- then writes the ids.
+//     Tiles longer than the LDS capacity run the same sort in global memory.
+// Integer work, HBM- and latency-bound; 5 launches instead of the
+// reference's scan + 6-pass 64-bit radix sort + ranges.
+#include "gs_common.h"
+#include "gs_kernels.h"
+
+namespace gs {
+
+// Instances of one rect handled by one lane; larger rects are spread over the
+// wave (a full-screen Gaussian must not serialize its wave for 2,500 tiles).
+constexpr int LANE_TILES = 16;
+
+template <bool WRITE>
+__global__ __launch_bounds__(TB_THREADS) void tile_hist_kernel(TileArgs a, int t0, int nt) {
+  extern __shared__ uint32_t s_bin[];  // nt counters (hist) or cursors (bucket)
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+  for (int i = tid; i < nt; i += TB_THREADS)
+    s_bin[i] = WRITE ? a.ranges[t0 + i].x + a.thist[(size_t)(t0 + i) * TB_BLOCKS + b] : 0u;
+  __syncthreads();
+  const int per = (a.P + TB_BLOCKS - 1) / TB_BLOCKS;
+  const int g0 = b * per, g1 = min(a.P, g0 + per);
+  const int gx = a.grid_x;
+  for (int base = g0; base < g1; base += TB_THREADS) {
+    const int g = base + tid;
+    int x0 = 0, y0 = 0, w = 0, n = 0;
+    uint64_t key = 0;
+    if (g < g1) {
+      const ushort4 r = reinterpret_cast<const ushort4*>(a.rect)[g];
+      x0 = r.x;
+      y0 = r.y;
+      w = (int)r.z - (int)r.x;
+      n = w * ((int)r.w - (int)r.y);
+      if (WRITE && n > 0)
+        key = ((uint64_t)__float_as_uint(a.rec[(size_t)REC * g + R_DEPTH]) << 32) | (uint32_t)g;
+    }
+    auto emit = [&](int x, int y, uint64_t k) {
+      const uint32_t u = (uint32_t)(y * gx + x - t0);
+      if (u < (uint32_t)nt) {
+        if (WRITE) a.keys[atomicAdd(&s_bin[u], 1u)] = k;
+        else atomicAdd(&s_bin[u], 1u);
+      }
+    };
+    if (n > 0 && n <= LANE_TILES) {
+      const int h = n / w;
+      for (int y = y0; y < y0 + h; ++y)
+        for (int x = x0; x < x0 + w; ++x) emit(x, y, key);
+    }
+    uint64_t big = __ballot(n > LANE_TILES);
+    while (big) {
+      const int j = __builtin_ctzll(big);
+      big &= big - 1;
+      const int bx0 = __shfl(x0, j, 64), by0 = __shfl(y0, j, 64), bw = __shfl(w, j, 64);
+      const int bn = __shfl(n, j, 64);
+      const uint64_t bk = WRITE ? (uint64_t)__shfl((long long)key, j, 64) : 0ull;
+      for (int i = lane; i < bn; i += 64) emit(bx0 + i % bw, by0 + i / bw, bk);
+    }
+  }
+  if (!WRITE) {
+    __syncthreads();
+    for (int i = tid; i < nt; i += TB_THREADS) a.thist[(size_t)(t0 + i) * TB_BLOCKS + b] = s_bin[i];
+  }
+}
+
+// Row scan of the [tile][block] count matrix, one workgroup per tile:
+// per-block offset inside the tile, and the tile total.
+static_assert(TB_BLOCKS == 256, "tile_rowscan_kernel scans one count per thread");
+__global__ __launch_bounds__(TB_BLOCKS) void tile_rowscan_kernel(uint32_t* __restrict__ thist,
+                                                                 uint32_t* __restrict__ ttotal) {
+  __shared__ uint32_t s_w[TB_BLOCKS / 64];
+  const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  uint32_t* row = thist + (size_t)t * TB_BLOCKS;
+  const uint32_t v = row[tid];
+  uint32_t inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
+  }
+  if (lane == 63) s_w[wave] = inc;
+  __syncthreads();
+  uint32_t woff = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < TB_BLOCKS / 64; ++w) {
+    const uint32_t x = s_w[w];
+    if (w < wave) woff += x;
+    tot += x;
+  }
+  row[tid] = woff + inc - v;
+  if (tid == 0) ttotal[t] = tot;
+}
+
+// One workgroup: exclusive scan of the tile totals into ranges, and the header.
+constexpr int OFF_T = 1024;
+__global__ __launch_bounds__(OFF_T) void tile_offsets_kernel(const uint32_t* __restrict__ ttotal, int T,
+                                                             uint2* __restrict__ ranges,
+                                                             uint32_t* __restrict__ meta, int prefiltered) {
+  __shared__ unsigned long long s_sum[OFF_T / 64];
+  __shared__ uint32_t s_max;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) s_max = 0;
+  const int per = (T + OFF_T - 1) / OFF_T;
+  const int a0 = min(T, tid * per), a1 = min(T, a0 + per);
+  unsigned long long sum = 0;
+  uint32_t mx = 0;
+  for (int t = a0; t < a1; ++t) {
+    const uint32_t v = ttotal[t];
+    sum += v;
+    mx = max(mx, v);
+  }
+  // wave inclusive scan, then across the 16 waves
+  unsigned long long inc = sum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
+  }
+  if (lane == 63) s_sum[wave] = inc;
+  __syncthreads();
+  atomicMax(&s_max, mx);
+  unsigned long long woff = 0, total = 0;
+#pragma unroll
+  for (int w = 0; w < OFF_T / 64; ++w) {
+    const unsigned long long v = s_sum[w];
+    if (w < wave) woff += v;
+    total += v;
+  }
+  unsigned long long run = woff + inc - sum;
+  for (int t = a0; t < a1; ++t) {
+    const uint32_t v = ttotal[t];
+    // empty tiles keep (0, 0), as identifyTileRanges leaves them (rasterizer_impl.cu:116-138)
+    ranges[t] = v ? make_uint2((uint32_t)run, (uint32_t)(run + v)) : make_uint2(0u, 0u);
+    run += v;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const uint32_t ovf = total > 0xFFFFFFFFull ? 2u : 0u;  // ranges are 32-bit, as in the reference
+    meta[M_L] = (uint32_t)total;
+    meta[M_MAXN] = s_max;
+    meta[M_RSVD] = 0;
+    meta[M_STATUS] = prefiltered ? (meta[M_STATUS] | ovf) : ovf;
+  }
+}
+
+// One tile per workgroup: LSD radix sort of its (depth bits << 32 | id) keys
+// on the 32 depth bits, 8 bits a pass (passes whose digit is the same for
+// every key are skipped).  Wave w owns the contiguous quarter
+// [w*q, (w+1)*q) of the keys; per pass it counts digits per wave (ballot
+// match, one leader per digit and round), a 256-thread scan turns the counts
+// into per-(wave, digit) bases, and each wave scatters its keys in order --
+// stable, with no barrier inside the scatter.  LSD passes keep equal depths
+// in their incoming (arbitrary bucket) order, so a last step sorts any run of
+// equal depth by id: the result is the reference's (depth, index) order.
+// Keys live in LDS (two buffers) or, for tiles longer than the launch's LDS
+// capacity, in global memory (the keys segment and its twin in keys2).
+__device__ inline uint64_t match_digit8(uint32_t d, uint64_t valid) {
+  uint64_t peers = valid;
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    const bool set = (d >> b) & 1u;
+    const uint64_t m = __ballot(set);
+    peers &= set ? m : ~m;
+  }
+  return peers;
+}
+
+struct RadixSmem {
+  uint32_t wcnt[4][256];  // per-wave digit counts, then per-wave bases
+  uint32_t wsum[4];
+  int skip, unsorted;
+};
+
+template <class KP>
+__device__ __attribute__((always_inline)) KP tile_radix_sort(KP A, KP B, int n, RadixSmem& sm) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  const int q = (n + 3) >> 2;
+  const int w0 = min(n, wave * q), w1 = min(n, w0 + q);
+  KP src = A, dst = B;
+  for (int shift = 32; shift < 64; shift += 8) {
+#pragma unroll
+    for (int w = 0; w < 4; ++w) sm.wcnt[w][tid] = 0;
+    if (tid == 0) sm.skip = 0;
+    __syncthreads();
+    for (int i0 = w0; i0 < w1; i0 += 64) {
+      const int i = i0 + lane;
+      const bool valid = i < w1;
+      const uint32_t d = valid ? (uint32_t)(src[i] >> shift) & 255u : 0u;
+      const uint64_t peers = match_digit8(d, __ballot(valid));
+      if (valid && (peers & lt) == 0) sm.wcnt[wave][d] += (uint32_t)__popcll(peers);
+    }
+    __syncthreads();
+    const uint32_t c0 = sm.wcnt[0][tid], c1 = sm.wcnt[1][tid], c2 = sm.wcnt[2][tid], c3 = sm.wcnt[3][tid];
+    const uint32_t tot = c0 + c1 + c2 + c3;
+    if (tot == (uint32_t)n) sm.skip = 1;
+    // exclusive scan of the digit totals over the 256 threads
+    uint32_t inc = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += y;
+    }
+    if (lane == 63) sm.wsum[wave] = inc;
+    __syncthreads();
+    uint32_t ex = inc - tot;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) ex += w < wave ? sm.wsum[w] : 0u;
+    const bool skip = sm.skip != 0;
+    sm.wcnt[0][tid] = ex;
+    sm.wcnt[1][tid] = ex + c0;
+    sm.wcnt[2][tid] = ex + c0 + c1;
+    sm.wcnt[3][tid] = ex + c0 + c1 + c2;
+    __syncthreads();
+    if (skip) continue;  // uniform: one digit holds every key
+    for (int i0 = w0; i0 < w1; i0 += 64) {
+      const int i = i0 + lane;
+      const bool valid = i < w1;
+      const uint64_t k = valid ? src[i] : 0ull;
+      const uint32_t d = (uint32_t)(k >> shift) & 255u;
+      const uint64_t peers = match_digit8(d, __ballot(valid));
+      const uint64_t below = peers & lt;
+      const uint32_t base = sm.wcnt[wave][d];
+      if (valid) dst[base + (uint32_t)__popcll(below)] = k;
+      if (valid && below == 0) sm.wcnt[wave][d] = base + (uint32_t)__popcll(peers);
+    }
+    __syncthreads();
+    const KP t = src;
+    src = dst;
+    dst = t;
+  }
+  // equal depths: order by id (rare; runs are short)
+  if (tid == 0) sm.unsorted = 0;
+  __syncthreads();
+  for (int i = tid; i + 1 < n; i += TS_THREADS)
+    if ((src[i] >> 32) == (src[i + 1] >> 32) && src[i + 1] < src[i]) sm.unsorted = 1;
+  __syncthreads();
+  if (sm.unsorted) {
+    for (int i = tid; i < n; i += TS_THREADS) {
+      if (i > 0 && (src[i - 1] >> 32) == (src[i] >> 32)) continue;  // not a run start
+      int e = i + 1;
+      while (e < n && (src[e] >> 32) == (src[i] >> 32)) ++e;
+      for (int a = i + 1; a < e; ++a) {  // insertion sort of [i, e)
+        const uint64_t v = src[a];
+        int b = a - 1;
+        while (b >= i && src[b] > v) { src[b + 1] = src[b]; --b; }
+        src[b + 1] = v;
+      }
+    }
+    __syncthreads();
+  }
+  return src;
+}
+
+__global__ __launch_bounds__(TS_THREADS) void tile_sort_kernel(const uint2* __restrict__ ranges,
+                                                               uint64_t* __restrict__ keys,
+                                                               uint64_t* __restrict__ keys2,
+                                                               uint32_t* __restrict__ plist, int cap) {
+  extern __shared__ uint64_t s_key[];  // 2 x cap keys
+  __shared__ RadixSmem sm;
+  const uint2 r = ranges[blockIdx.x];
+  const int n = (int)(r.y - r.x);
+  if (n == 0) return;
+  if (n == 1) {
+    if (threadIdx.x == 0) plist[r.x] = (uint32_t)keys[r.x];
+    return;
+  }
+  if (n <= cap) {
+    for (int i = threadIdx.x; i < n; i += TS_THREADS) s_key[i] = keys[r.x + i];
+    __syncthreads();
+    const uint64_t* out = tile_radix_sort<uint64_t*>(s_key, s_key + cap, n, sm);
+    for (int i = threadIdx.x; i < n; i += TS_THREADS) plist[r.x + i] = (uint32_t)out[i];
+  } else {  // longer than the LDS capacity of this launch: sort in global memory
+    const uint64_t* out = tile_radix_sort<uint64_t*>(keys + r.x, keys2 + r.x, n, sm);
+    for (int i = threadIdx.x; i < n; i += TS_THREADS) plist[r.x + i] = (uint32_t)out[i];
+  }
+}
+
+// ------------------------------------------------------------------ launchers
+
+void launch_tile_plan(const TileArgs& a, int prefiltered, hipStream_t s) {
+  const int T = a.num_tiles;
+  for (int t0 = 0; t0 < T; t0 += TB_BINS) {
+    const int nt = min(TB_BINS, T - t0);
+    hipLaunchKernelGGL(tile_hist_kernel<false>, dim3(TB_BLOCKS), dim3(TB_THREADS), sizeof(uint32_t) * nt, s, a,
+                       t0, nt);
+  }
+  hipLaunchKernelGGL(tile_rowscan_kernel, dim3(T), dim3(TB_BLOCKS), 0, s, a.thist, a.ttotal);
+  hipLaunchKernelGGL(tile_offsets_kernel, dim3(1), dim3(OFF_T), 0, s, a.ttotal, T, a.ranges, a.meta,
+                     prefiltered);
+}
+
+void launch_tile_bucket(const TileArgs& a, hipStream_t s) {
+  const int T = a.num_tiles;
+  for (int t0 = 0; t0 < T; t0 += TB_BINS) {
+    const int nt = min(TB_BINS, T - t0);
+    hipLaunchKernelGGL(tile_hist_kernel<true>, dim3(TB_BLOCKS), dim3(TB_THREADS), sizeof(uint32_t) * nt, s, a,
+                       t0, nt);
+  }
+}
+
+void launch_tile_sort(const TileArgs& a, int64_t max_len, hipStream_t s) {
+  // LDS sized to the longest tile when the plan's header is known on the host
+  const int cap = (max_len >= 0 && max_len < TS_CAP) ? (int)max_len : TS_CAP;
+  hipLaunchKernelGGL(tile_sort_kernel, dim3(a.num_tiles), dim3(TS_THREADS), 2 * sizeof(uint64_t) * (cap > 0 ? cap : 1),
+                     s, a.ranges, a.keys, a.keys2, a.plist, cap > 0 ? cap : 1);
+}
+
+}  // namespace gs

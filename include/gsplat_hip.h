@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 2
+#define GS_ABI_VERSION 3
 
 /* compat modes: numerics of the as-shipped reference vs corrected ones */
 #define GS_COMPAT_REFERENCE 0
@@ -92,13 +92,16 @@ size_t gs_image_buffer_bytes(int32_t W, int32_t H);
 size_t gs_backward_scratch_bytes(int64_t P, int32_t F);
 
 /* Forward, phase 1 -- replaces CR/rasterizer_impl.cu:198-287 (preprocess,
- * inclusive scan, D2H of num_rendered).  Writes radii[P] and *num_rendered. */
+ * inclusive scan of tiles_touched, D2H of num_rendered).  Writes radii[P],
+ * *num_rendered and the binning plan (per-tile counts and ranges) into the
+ * image buffer, which must be the one later passed to gs_forward_render. */
 int gs_forward_plan(const gs_gaussians *g, const gs_camera *cam, int prefiltered,
-                    int debug, int compat, void *geom_buffer, int32_t *radii,
-                    int64_t *num_rendered, gs_stream_t stream);
+                    int debug, int compat, void *geom_buffer, void *image_buffer,
+                    int32_t *radii, int64_t *num_rendered, gs_stream_t stream);
 
 /* Forward, phase 2 -- replaces CR/rasterizer_impl.cu:289-345 (duplicateWithKeys,
- * radix sort, identifyTileRanges, render).  Outputs are planar CHW:
+ * radix sort, identifyTileRanges, render): instances are bucketed by tile and
+ * each tile's list sorted by (depth, index) -- the reference's order.  Outputs are planar CHW:
  * out_color 3xHxW, out_feature FxHxW (may be NULL if F==0), out_depth HxW,
  * out_alpha HxW.  Every output pixel is written.  In GS_COMPAT_REFERENCE mode
  * out_alpha receives zeros (the reference never writes it, Q1) and may be NULL;
