@@ -341,6 +341,7 @@ int gs_backward(const gs_gaussians* g, const gs_camera* cam, const int32_t* radi
   b.focal_y = (float)H / (2.0f * cam->tan_fovy);  // CR/rasterizer_impl.cu:398-399
   b.focal_x = (float)W / (2.0f * cam->tan_fovx);
   b.acc = acc;
+  b.rec = at<float>(geom, gl.rec);
   b.grad_mask = g->grad_mask;
   b.dmeans2D = dL_dmeans2D; b.dcolors = dL_dcolors; b.dsemantic = dL_dsemantic; b.dopacity = dL_dopacity;
   b.dmeans3D = dL_dmeans3D; b.dcov3D = dL_dcov3D; b.dsh = dL_dsh; b.dscales = dL_dscales;

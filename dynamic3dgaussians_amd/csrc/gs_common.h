@@ -28,7 +28,11 @@ enum RecField {
   R_RAD = 12,                 // screen radius (ceil(3 sqrt(lambda_max)))
 };
 
-// Gradient accumulation record per Gaussian (backward scratch): CS = 10 + F
+// Gradient accumulation record per Gaussian (backward scratch), sums over
+// the Gaussian's pixels with e = dL/dG * G:  A_MX = sum e dx, A_MY = sum e dy,
+// A_CA = sum e dx^2, A_CB = sum e dx dy, A_CC = sum e dy^2 (turned into
+// dL/dmean2D and dL/dconic by preprocess_bwd), A_OP = dL/dopacity,
+// A_R..A_B = dL/dcolour, A_DEPTH = dL/ddepth.
 enum AccField {
   A_MX = 0, A_MY = 1, A_CA = 2, A_CB = 3, A_CC = 4, A_OP = 5,
   A_R = 6, A_G = 7, A_B = 8, A_DEPTH = 9, A_FEAT = 10,

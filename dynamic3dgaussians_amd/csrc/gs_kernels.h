@@ -41,7 +41,8 @@ struct PreprocessBwdArgs {
   const float* proj;
   const float* campos;
   float scale_modifier, c_x, c_y, tan_fovx, tan_fovy, focal_x, focal_y;
-  const float* acc;  // P x 10 blend gradients (A_MX..A_DEPTH)
+  const float* rec;  // P x REC render records (conic)
+  const float* acc;  // P x 10 blend gradient sums (AccField)
   const float* grad_mask;  // P or null (Q12 label)
   float* dmeans2D;
   float* dcolors;

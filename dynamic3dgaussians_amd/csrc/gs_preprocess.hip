@@ -362,9 +362,18 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdArgs a
   const float* acc = a.acc + (size_t)A_FEAT * g;
   const bool vis = a.radii[g] > 0;
   // blend gradients -> output tensors (zero for culled Gaussians: never touched)
-  // the blend kernel accumulates dL/d(pixel offset); the ndc scale
-  // ddelx_dx = 0.5 W, ddely_dy = 0.5 H (CR/backward.cu:520-521) is applied once here
-  const float am0 = acc[A_MX] * (0.5f * (float)a.W), am1 = acc[A_MY] * (0.5f * (float)a.H);
+  // dL/dmean2D = sum over pixels of dL/dG * dG/d(offset) * ndc scale
+  // (CR/backward.cu:616-621): from the blend kernel's basis sums (AccField),
+  // the conic and ddelx_dx = 0.5 W, ddely_dy = 0.5 H (:520-521).
+  float am0 = 0.f, am1 = 0.f;
+  float4 con = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (vis) {
+    con = reinterpret_cast<const float4*>(a.rec + (size_t)REC * g)[0];  // x, y, a, b
+    const float cc = a.rec[(size_t)REC * g + R_CC];
+    const float sex = acc[A_MX], sey = acc[A_MY];
+    am0 = (-con.z * sex - con.w * sey) * (0.5f * (float)a.W);
+    am1 = (-cc * sey - con.w * sex) * (0.5f * (float)a.H);
+  }
   a.dmeans2D[3 * g] = am0; a.dmeans2D[3 * g + 1] = am1; a.dmeans2D[3 * g + 2] = 0.f;
   const float dcol[3] = {acc[A_R], acc[A_G], acc[A_B]};
   // Q12 label mask (DGR/__init__.py:159-173), applied at store time exactly as
@@ -382,7 +391,8 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdArgs a
     float c3v[6];
 #pragma unroll
     for (int i = 0; i < 6; ++i) c3v[i] = c3[i];
-    const float dcx = acc[A_CA], dcy = acc[A_CB], dcz = acc[A_CC];
+    // dL/dconic = -1/2 sum e (dx^2, dx dy, dy^2) (CR/backward.cu:622-624)
+    const float dcx = -0.5f * acc[A_CA], dcy = -0.5f * acc[A_CB], dcz = -0.5f * acc[A_CC];
     Ewa e;
     ewa_setup(mean, a.view, a.W, a.H, a.c_x, a.c_y, a.focal_x, a.focal_y, a.tan_fovx, a.tan_fovy, e);
     float xg, yg;

@@ -31,6 +31,7 @@ namespace gs {
 constexpr float ALPHA_MIN = 1.0f / 255.0f;
 constexpr int CHUNK = 64;
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float float4_t __attribute__((ext_vector_type(4)));
 
 __device__ inline bool wave_any(bool p) { return __ballot(p) != 0ull; }
 
@@ -99,6 +100,17 @@ __device__ inline RecRegs load_rec(const uint32_t* __restrict__ point_list, cons
   return r;
 }
 
+// Gaussian exponent at pixel offset (dx, dy) from the conic scaled once per
+// record: h = (-a/2, -b, -c/2).  power = -1/2 (a dx^2 + c dy^2) - b dx dy
+// (CR/forward.cu:353-355) in a fixed fma order shared by the forward and the
+// backward kernel, so both make bit-identical alpha decisions.
+__device__ inline float4 half_conic(const float4& q0, const float4& q1) {
+  return make_float4(-0.5f * q0.z, -q0.w, -0.5f * q1.x, 0.0f);
+}
+__device__ inline float gauss_power(float dx, float dy, const float4& h) {
+  return fmaf(h.x * dx, dx, fmaf(h.z * dy, dy, (h.y * dx) * dy));
+}
+
 __device__ inline bool strip_culled(const RecRegs& q, float sx0, float sx1, float sy0, float sy1) {
   return q.q0.x + q.q2.z < sx0 || q.q0.x - q.q2.z > sx1 || q.q0.y + q.q2.w < sy0 || q.q0.y - q.q2.w > sy1;
 }
@@ -115,6 +127,7 @@ __global__ __launch_bounds__(256) void render_fwd_kernel(
   constexpr bool MF = (F == 32 || F == 64);  // features on the matrix cores
   constexpr int FB = MF ? F / 32 : 1;        // 32-channel blocks
   constexpr int NSF = (!MF && F > 0) ? F : 1;
+  // per record: (x, y, -a/2, -b) (-c/2, opacity, r, g) (b, depth, -, -)
   __shared__ float4 s_rec[4][CHUNK][3];
   __shared__ uint32_t s_gid[4][CHUNK];
 
@@ -136,7 +149,9 @@ __global__ __launch_bounds__(256) void render_fwd_kernel(
 #pragma unroll
   for (int i = 0; i < 2 * FB; ++i) acc[i] = f32x16{0};
   uint32_t last = 0;
-  bool done = !inside;
+  // lane still blending (the reference's !done); an integer, not a bool, so
+  // that it lives in a VGPR instead of exec-mask bookkeeping across the loops
+  uint32_t live = inside ? 1u : 0u;
   // MFMA pairing: a blended Gaussian waits for a partner; a completed pair's
   // feature rows are loaded one pair ahead of its MFMAs (latency hiding).
   int pend = 0;
@@ -164,15 +179,18 @@ __global__ __launch_bounds__(256) void render_fwd_kernel(
   const uint32_t lastv = range.y > range.x ? range.y - 1 : range.x;
   RecRegs q;
   if (range.y > range.x) q = load_rec(point_list, rec, range.x + lane, lastv);
-  bool all_done = !wave_any(!done);
+  STAT_DECL(st_it);
   STAT(6, 1);
   STAT(7, range.y - range.x);
-  STAT_DECL(st_it);
-  for (uint32_t c0 = range.x; c0 < range.y && !all_done; c0 += CHUNK) {
+  if (!wave_any(live != 0u)) goto blend_done;
+  for (uint32_t c0 = range.x; c0 < range.y; c0 += CHUNK) {
     const bool keep = (c0 + lane < range.y) && !strip_culled(q, sx0, sx1, sy0, sy1);
-    s_rec[wave][lane][0] = q.q0;
-    s_rec[wave][lane][1] = q.q1;
-    s_rec[wave][lane][2] = q.q2;
+    {
+      const float4 h = half_conic(q.q0, q.q1);
+      s_rec[wave][lane][0] = make_float4(q.q0.x, q.q0.y, h.x, h.y);
+      s_rec[wave][lane][1] = make_float4(h.z, q.q1.y, q.q1.z, q.q1.w);
+      s_rec[wave][lane][2] = q.q2;
+    }
     s_gid[wave][lane] = q.gid;
     uint64_t mask = __ballot(keep);
     STAT(0, 1);
@@ -181,31 +199,34 @@ __global__ __launch_bounds__(256) void render_fwd_kernel(
     q = load_rec(point_list, rec, c0 + CHUNK + lane, lastv);  // prefetch (clamped)
     while (mask) {
       const int j = __builtin_ctzll(mask);
-      mask &= mask - 1;
+      mask &= ~(1ull << j);
       STAT(3, 1);
       STAT_INC(st_it);
       const float4 r0 = s_rec[wave][j][0];
       const float4 r1 = s_rec[wave][j][1];
       const float4 r2 = s_rec[wave][j][2];
       const float dx = r0.x - pfx, dy = r0.y - pfy;
-      const float power = -0.5f * (r0.z * dx * dx + r1.x * dy * dy) - r0.w * dx * dy;
+      const float power = gauss_power(dx, dy, make_float4(r0.z, r0.w, r1.x, 0.f));
       const float alpha = fminf(0.99f, r1.y * fast_exp(power));
       const float test_T = T * (1 - alpha);
-      bool blend = !done && !(power > 0.0f) && !(alpha < ALPHA_MIN);
-      if (blend && test_T < 0.0001f) { done = true; blend = false; }
+      // Branch-free blend (CR/forward.cu:350-380): non-blending lanes add
+      // zero-weighted terms, and T / last / live are selected, so the loop
+      // body has no exec-mask juggling.
+      const bool cand = live != 0u && !(power > 0.0f) && !(alpha < ALPHA_MIN);
+      const bool fin = cand && test_T < 0.0001f;  // saturated: not blended, lane done
+      const bool blend = cand && !fin;
+      live = fin ? 0u : live;
+      const float w = blend ? alpha * T : 0.0f;
+      C0 = fmaf(r1.z, w, C0);
+      C1 = fmaf(r1.w, w, C1);
+      C2 = fmaf(r2.x, w, C2);
+      Dp = fmaf(r2.y, w, Dp);
+      T = blend ? test_T : T;
+      last = blend ? c0 + j - range.x + 1 : last;
       STAT(4, wave_any(blend));
       STAT(5, __builtin_popcountll(__ballot(blend)));
-      if (wave_any(blend)) {
-        const float w = blend ? alpha * T : 0.0f;
-        if (blend) {
-          C0 += r1.z * w;
-          C1 += r1.w * w;
-          C2 += r2.x * w;
-          Dp += r2.y * w;
-          T = test_T;
-          last = c0 + j - range.x + 1;
-        }
-        if constexpr (F > 0) {
+      if (F > 0 && wave_any(blend)) {
+        {
           const uint32_t gid = __builtin_amdgcn_readfirstlane(s_gid[wave][j]);
           if constexpr (MF) {
             if (pend == 0) {
@@ -221,16 +242,17 @@ __global__ __launch_bounds__(256) void render_fwd_kernel(
               push_pair(b0, b1, an);
               pend = 0;
             }
-          } else if (blend) {
+          } else {
             const float* f = feats + (size_t)gid * F;
 #pragma unroll
-            for (int c = 0; c < NSF; ++c) SF[c] += f[c] * w;
+            for (int c = 0; c < NSF; ++c) SF[c] = fmaf(f[c], w, SF[c]);
           }
         }
       }
-      if (!wave_any(!done)) { all_done = true; break; }
+      if (!wave_any(live != 0u)) goto blend_done;
     }
   }
+blend_done:
   STAT_WAVE(16, 20, st_it);
   if constexpr (MF) {
     if (pend) {
@@ -309,8 +331,44 @@ __device__ inline void commit(const float (&v)[N], float* __restrict__ acc_g, fl
   for (int c = 0; c < n; ++c) t[c] = v[OFF + c];
   const float s = wave_reduce_transposed<n>(t, lane);
   const int comp = OFF + bitrev6(lane);
+#ifdef GS_EXP_NO_ACC_ATOMIC
+  if (comp < OFF + n && s == 12345.f) acc_g[comp] = s;
+#else
   if (comp < OFF + n) atomicAdd(comp < A_FEAT ? acc_g + comp : dsem_g + (comp - A_FEAT), s);
+#endif
   if constexpr (OFF + 64 < N) commit<N, OFF + 64>(v, acc_g, dsem_g, lane);
+}
+
+// dL/dsemantic of a batch of WB (<= 16) Gaussians: C[g][ch] = sum over the
+// wave's 64 pixels of w[g][pix] * dLf[pix][ch] on v_mfma_f32_16x16x4_f32
+// (A[g = l&15][k = l>>4] from the batch weights in LDS, B from registers,
+// C row (l>>4)*4 + r, column l&15), then one atomic per (Gaussian, channel).
+__device__ inline float4_t mfma16(float a, float b, float4_t c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+template <int F, int WB>
+__device__ inline void flush_feature_batch(const float (*w)[68], const uint32_t* bgid, const float (&Bs)[F / 16][16],
+                                           float* __restrict__ dsem, int lane, int rows) {
+  float a[16];
+#pragma unroll
+  for (int s = 0; s < 16; ++s) a[s] = w[lane & 15][4 * s + (lane >> 4)];
+#pragma unroll
+  for (int cb = 0; cb < F / 16; ++cb) {
+    float4_t c = float4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 16; ++s) c = mfma16(a[s], Bs[cb][s], c);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = (lane >> 4) * 4 + r;
+      if (row < rows) {
+#ifdef GS_EXP_NO_FEAT_ATOMIC
+        if (c[r] == 12345.f) dsem[(size_t)bgid[row] * F + cb * 16 + (lane & 15)] = c[r];
+#else
+        atomicAdd(dsem + (size_t)bgid[row] * F + cb * 16 + (lane & 15), c[r]);
+#endif
+      }
+    }
+  }
 }
 
 template <int F, int COMPAT>
@@ -324,12 +382,14 @@ __global__ __launch_bounds__(256) void render_bwd_kernel(
   constexpr bool MF = (F == 32 || F == 64);
   constexpr int FB = MF ? F / 32 : 1;
   constexpr int NV = MF ? A_FEAT : A_FEAT + F;  // components reduced on the VALU
-  constexpr int WB = 32;                        // Gaussians per MFMA batch
+  constexpr int WB = 16;                        // Gaussians per MFMA batch
+  constexpr int CB = MF ? F / 16 : 1;           // 16-channel blocks
   constexpr bool FIXED_FEAT = (COMPAT != COMPAT_REFERENCE) && F > 0;
   constexpr int NF_REG = (!MF && F > 0) ? F : 1;
-  __shared__ float4 s_rec[4][CHUNK][3];
+  __shared__ float4 s_rec[4][CHUNK][4];  // the record's 3 float4 + half conic
   __shared__ uint32_t s_gid[4][CHUNK];
-  __shared__ float s_w[MF ? 4 : 1][MF ? WB : 1][65];
+  // batch weights w[g][pixel] (row pad 4: the 16x16x4 A reads are conflict-free)
+  __shared__ float s_w[MF ? 4 : 1][MF ? WB : 1][68];
   __shared__ uint32_t s_bgid[MF ? 4 : 1][WB];
 
   const int tile = xcd_remap(blockIdx.x, num_tiles);
@@ -355,22 +415,23 @@ __global__ __launch_bounds__(256) void render_bwd_kernel(
   const float bg_dot = bg[0] * dLp[0] + bg[1] * dLp[1] + bg[2] * dLp[2];
 
   // Upstream feature gradients.  VALU path: one register per channel.
-  // MFMA path: the B operands of dL/df = W . dLf, lane l / step s holding
-  // dLf[pixel 2s + (l>>5)][channel fb*32 + (l&31)], transposed through LDS.
+  // MFMA path (v_mfma_f32_16x16x4_f32, K = pixels): the B operands of
+  // dL/df = W . dLf, lane l / step s / block cb holding
+  // dLf[pixel 4s + (l>>4)][channel 16cb + (l&15)], transposed through LDS.
   float dLf[NF_REG];
-  float Bs[MF ? FB : 1][MF ? 32 : 1];
+  float Bs[MF ? CB : 1][MF ? 16 : 1];
   float dLf_own[FIXED_FEAT && MF ? F : 1];  // fixed mode also needs f . dLf per pixel
   if constexpr (MF) {
 #pragma unroll
-    for (int fb = 0; fb < FB; ++fb) {
+    for (int cb = 0; cb < CB; ++cb) {
 #pragma unroll
-      for (int c = 0; c < 32; ++c) {
-        const float v = inside ? dL_dfeat[(size_t)(fb * 32 + c) * HW + pix] : 0.f;
+      for (int c = 0; c < 16; ++c) {
+        const float v = inside ? dL_dfeat[(size_t)(cb * 16 + c) * HW + pix] : 0.f;
         s_w[wave][c][lane] = v;
-        if constexpr (FIXED_FEAT) dLf_own[fb * 32 + c] = v;
+        if constexpr (FIXED_FEAT) dLf_own[cb * 16 + c] = v;
       }
 #pragma unroll
-      for (int s = 0; s < 32; ++s) Bs[fb][s] = s_w[wave][lane & 31][2 * s + (lane >> 5)];
+      for (int s = 0; s < 16; ++s) Bs[cb][s] = s_w[wave][lane & 15][4 * s + (lane >> 4)];
     }
   } else {
 #pragma unroll
@@ -404,6 +465,7 @@ __global__ __launch_bounds__(256) void render_bwd_kernel(
     s_rec[wave][lane][0] = q.q0;
     s_rec[wave][lane][1] = q.q1;
     s_rec[wave][lane][2] = q.q2;
+    s_rec[wave][lane][3] = half_conic(q.q0, q.q1);
     s_gid[wave][lane] = q.gid;
     uint64_t mask = __ballot(keep);
     STAT(8, 1);
@@ -421,8 +483,8 @@ __global__ __launch_bounds__(256) void render_bwd_kernel(
       const float4 r1 = s_rec[wave][j][1];
       const float4 r2 = s_rec[wave][j][2];
       const float dx = r0.x - pfx, dy = r0.y - pfy;
-      const float ca = r0.z, cb = r0.w, cc = r1.x, op = r1.y;
-      const float power = -0.5f * (ca * dx * dx + cc * dy * dy) - cb * dx * dy;
+      const float op = r1.y;
+      const float power = gauss_power(dx, dy, s_rec[wave][j][3]);
       const float G = fast_exp(power);
       const float alpha = fminf(0.99f, op * G);
       const bool valid = (k < last) && !(power > 0.0f) && !(alpha < ALPHA_MIN);
@@ -468,32 +530,24 @@ __global__ __launch_bounds__(256) void render_bwd_kernel(
 #pragma unroll
         for (int c = 0; c < NF_REG; ++c) if (A_FEAT + c < NV) v[A_FEAT + c] = dch * dLf[c];
       }
-      // dL/dG -> mean2D (scaled by 0.5W, 0.5H in preprocess_bwd) and conic
-      const float dL_dG = op * dL_dopa;
-      const float gdx = Gv * dx, gdy = Gv * dy;
-      v[A_MX] = dL_dG * fmaf(-gdx, ca, -gdy * cb);
-      v[A_MY] = dL_dG * fmaf(-gdy, cc, -gdx * cb);
-      const float hx = -0.5f * dL_dG * gdx, hy = -0.5f * dL_dG * gdy;
-      v[A_CA] = hx * dx;
-      v[A_CB] = hx * dy;
-      v[A_CC] = hy * dy;
+      // dL/dG -> mean2D and conic (CR/backward.cu:616-630).  Those are linear
+      // in e = dL/dG * G times dx, dy, dx^2, dx dy, dy^2 with per-Gaussian
+      // factors (conic, -1/2, ndc scale), so the wave sums only the five
+      // basis terms; preprocess_bwd applies the factors once per Gaussian.
+      const float e = (op * dL_dopa) * Gv;
+      const float ex = e * dx, ey = e * dy;
+      v[A_MX] = ex;
+      v[A_MY] = ey;
+      v[A_CA] = ex * dx;
+      v[A_CB] = ex * dy;
+      v[A_CC] = ey * dy;
       v[A_OP] = Gv * dL_dopa;
       commit<NV>(v, acc + (size_t)A_FEAT * gid, dsem + (size_t)F * gid, lane);
       if constexpr (MF) {
         s_w[wave][nb][lane] = dch;
         if (lane == 0) s_bgid[wave][nb] = gid;
         if (++nb == WB) {
-#pragma unroll
-          for (int fb = 0; fb < FB; ++fb) {
-            f32x16 c = f32x16{0};
-#pragma unroll
-            for (int s = 0; s < 32; ++s) c = mfma32(s_w[wave][lane & 31][2 * s + (lane >> 5)], Bs[fb][s], c);
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-              atomicAdd(dsem + (size_t)s_bgid[wave][row] * F + fb * 32 + (lane & 31), c[r]);
-            }
-          }
+          flush_feature_batch<F, WB>(s_w[wave], s_bgid[wave], Bs, dsem, lane, WB);
           nb = 0;
         }
       }
@@ -502,21 +556,9 @@ __global__ __launch_bounds__(256) void render_bwd_kernel(
   }
   STAT_WAVE(17, 25, st_it);
   if constexpr (MF) {
-    if (nb > 0) {
-      // rows >= nb hold stale weights; MFMA rows are independent, so they
-      // only produce results that are not committed
-#pragma unroll
-      for (int fb = 0; fb < FB; ++fb) {
-        f32x16 c = f32x16{0};
-#pragma unroll
-        for (int s = 0; s < 32; ++s) c = mfma32(s_w[wave][lane & 31][2 * s + (lane >> 5)], Bs[fb][s], c);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-          if (row < nb) atomicAdd(dsem + (size_t)s_bgid[wave][row] * F + fb * 32 + (lane & 31), c[r]);
-        }
-      }
-    }
+    // rows >= nb hold stale weights; MFMA rows are independent, so they only
+    // produce results that are not committed
+    if (nb > 0) flush_feature_batch<F, WB>(s_w[wave], s_bgid[wave], Bs, dsem, lane, nb);
   }
 }
 
