@@ -121,14 +121,17 @@ def make_settings(cams, dev, compat):
     return out
 
 
-def stage_bytes(L, Pv, P, npix, F, C=3):
-    """Algorithmic HBM bytes per launch; K=1 (precomputed colours)."""
+def stage_bytes(L, Pv, P, W, H, F, C=3, TB=256):
+    """Algorithmic HBM bytes per launch (with this build's
+    binning: tile plan, bucket, per-tile sort); K=1 (precomputed colours)."""
+    npix = W * H
+    T = ((W + 15) // 16) * ((H + 15) // 16)
     return {
-        "preprocess": P * (12 + 12 + 16 + 4 + 12) + P * (4 + 8 + 4 + 16 + 4 + 24 + 12 + 3),
-        "scan": 8 * P,
-        "duplicate": 20 * Pv + 12 * L,
-        "sort": 24 * L,  # lower bound: one full pass
-        "ranges": 8 * L + 8 * ((npix + 255) // 256),
+        "preprocess": P * (12 + 12 + 16 + 4 + 12) + P * (4 + 64 + 24 + 4 + 8),
+        "scan": 8 * P + 3 * 4 * TB * T + 12 * T,       # tile histograms, row scans, ranges
+        "duplicate": 12 * P + 4 * TB * T + 8 * L,      # bucket (depth, id) keys by tile
+        "sort": 8 * L + 4 * L,                          # per-tile sort: keys in, ids out
+        "ranges": 0,
         "render_fwd": L * (4 + 8 + 16 + 4 * C + 4 + 4 * F) + npix * 4 * (C + F + 2 + 1),
         "render_bwd": L * (4 + 8 + 16 + 4 * C + 4 + 4 * F) + npix * 4 * (C + F + 4 + 1)
         + Pv * 4 * (3 + 4 + 1 + C + F + 1),
@@ -255,11 +258,21 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    # one untimed step with every stage timed: the per-stage breakdown and the
+    # dominant kernel; the timed region then records events around that kernel
+    # only (each timed stage costs an event pair on the stream)
+    torch.cuda.synchronize()
+    _lib.timing_enable(True)
+    step()
+    all_stages = _lib.timing_read()
+    _lib.timing_enable(False)
+    stage_ms = {k: v[0] for k, v in all_stages.items()}
+    dom = max(stage_ms, key=stage_ms.get)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    _lib.timing_enable(True)
+    _lib.timing_enable(True, stages=[dom])
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -280,12 +293,10 @@ def main():
     value = mpix_total / (ms_per_step / 1e3)
 
     # roofline of the dominant stage (live HIP-event durations over the timed region)
-    per_cam_bytes = [stage_bytes(L, Pv, args.gaussians, W_ * H_, args.features) for L, Pv in inst]
-    stage_ms = {k: v[0] for k, v in stages.items()}
-    dom = max(stage_ms, key=stage_ms.get)
+    per_cam_bytes = [stage_bytes(L, Pv, args.gaussians, W_, H_, args.features) for L, Pv in inst]
     launches = stages[dom][1]
     alg_bytes_total = sum(b[dom] for b in per_cam_bytes) * args.steps
-    avg_ms = stage_ms[dom] / max(launches, 1)
+    avg_ms = stages[dom][0] / max(launches, 1)
     alg_per_launch = alg_bytes_total / max(launches, 1)
     achieved = alg_per_launch / (avg_ms / 1e3) / 1e9 if avg_ms > 0 else 0.0
     traffic = load_pmc_traffic(dom)
@@ -306,7 +317,7 @@ def main():
                    "height": H_, "feature_channels": args.features, "compat": args.compat,
                    "parallelism": f"camera-sharded dp{world}"},
         "roofline": roofline,
-        "stages_ms_per_step": {k: round(v / args.steps, 4) for k, v in stage_ms.items()},
+        "stages_ms_per_step": {k: round(v, 4) for k, v in stage_ms.items()},
         "instances_per_cam": int(np.mean([L for L, _ in inst])),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

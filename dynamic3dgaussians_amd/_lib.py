@@ -67,6 +67,7 @@ PROTOTYPES = {
     "gs_sort_pairs": (ctypes.c_int, [c_int64, c_void_p, c_void_p, ctypes.c_int, c_void_p, c_void_p]),
     "gs_test_wave_reduce": (ctypes.c_int, [ctypes.c_int, c_void_p, c_void_p, c_void_p]),
     "gs_timing_enable": (ctypes.c_int, [ctypes.c_int]),
+    "gs_timing_select": (ctypes.c_int, [ctypes.c_uint32]),
     "gs_timing_read": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_int64),
                                       ctypes.c_int]),
 }
@@ -75,8 +76,12 @@ STAGES = ["preprocess", "scan", "duplicate", "sort", "ranges", "render_fwd", "re
           "preprocess_bwd"]
 
 
-def timing_enable(on: bool = True):
-    load().gs_timing_enable(1 if on else 0)
+def timing_enable(on: bool = True, stages=None):
+    """Enable/disable live stage timing; `stages` (names) restricts it."""
+    L = load()
+    mask = 0xFFFFFFFF if stages is None else sum(1 << STAGES.index(s) for s in stages)
+    L.gs_timing_select(mask)
+    L.gs_timing_enable(1 if on else 0)
 
 
 def timing_read() -> dict:

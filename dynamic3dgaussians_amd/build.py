@@ -33,7 +33,9 @@ if VARIANT:
 VARIANT_FLAGS = {"": [], "stats": ["-DGS_STATS"],
                  # timing experiments only (results are wrong by construction)
                  "exp_nofeat": ["-DGS_EXP_NO_FEAT_ATOMIC"], "exp_noacc": ["-DGS_EXP_NO_ACC_ATOMIC"],
-                 "exp_noatomic": ["-DGS_EXP_NO_FEAT_ATOMIC", "-DGS_EXP_NO_ACC_ATOMIC"]}
+                 "exp_noatomic": ["-DGS_EXP_NO_FEAT_ATOMIC", "-DGS_EXP_NO_ACC_ATOMIC"],
+                 "exp_fwd_noload": ["-DGS_EXP_FWD_NO_FEAT_LOAD"], "exp_fwd_nomfma": ["-DGS_EXP_FWD_NO_MFMA"],
+                 "exp_bwd_nodlf": ["-DGS_EXP_BWD_NO_DLF"], "exp_bwd_nomfma": ["-DGS_EXP_BWD_NO_MFMA"]}
 ARCH = os.environ.get("GSPLAT_OFFLOAD_ARCH", "gfx950")
 
 # Per-file flags.  The preprocess kernels are compiled without FMA

@@ -89,6 +89,7 @@ struct TimedEvent {
 };
 std::mutex g_tmu;
 bool g_timing = false;
+uint32_t g_timing_mask = 0xFFFFFFFFu;  // stages timed while enabled
 std::vector<TimedEvent> g_events;
 std::vector<hipEvent_t> g_pool;
 
@@ -109,7 +110,7 @@ struct StageTimer {
   hipEvent_t a = nullptr, b = nullptr;
   StageTimer(hipStream_t s_, int kind_) : s(s_), kind(kind_) {
     std::lock_guard<std::mutex> lk(g_tmu);
-    if (!g_timing) return;
+    if (!g_timing || !((g_timing_mask >> kind) & 1u)) return;
     a = pool_get();
     b = pool_get();
     (void)hipEventRecord(a, s);
@@ -154,6 +155,12 @@ int gs_timing_enable(int enable) {
   for (auto& e : g_events) { g_pool.push_back(e.a); g_pool.push_back(e.b); }
   g_events.clear();
   g_timing = enable != 0;
+  return 0;
+}
+
+int gs_timing_select(uint32_t stage_mask) {
+  std::lock_guard<std::mutex> lk(g_tmu);
+  g_timing_mask = stage_mask;
   return 0;
 }
 

@@ -163,11 +163,13 @@ __global__ __launch_bounds__(256) void render_fwd_kernel(
   for (int fb = 0; fb < FB; ++fb) pa[fb] = 0.f;
   auto push_pair = [&](float b0, float b1, const float (&an)[FB]) {
     if (have_prev) {
+#ifndef GS_EXP_FWD_NO_MFMA
 #pragma unroll
       for (int fb = 0; fb < FB; ++fb) {
         acc[2 * fb] = mfma32(pa[fb], pb0, acc[2 * fb]);
         acc[2 * fb + 1] = mfma32(pa[fb], pb1, acc[2 * fb + 1]);
       }
+#endif
     }
 #pragma unroll
     for (int fb = 0; fb < FB; ++fb) pa[fb] = an[fb];
@@ -238,7 +240,11 @@ __global__ __launch_bounds__(256) void render_fwd_kernel(
               float b0, b1, an[FB];
               swap32(pend_w, w, b0, b1);
 #pragma unroll
+#ifdef GS_EXP_FWD_NO_FEAT_LOAD
+              for (int fb = 0; fb < FB; ++fb) an[fb] = (float)(ga & 7);
+#else
               for (int fb = 0; fb < FB; ++fb) an[fb] = feats[(size_t)ga * F + fb * 32 + (lane & 31)];
+#endif
               push_pair(b0, b1, an);
               pend = 0;
             }
@@ -426,7 +432,11 @@ __global__ __launch_bounds__(256) void render_bwd_kernel(
     for (int cb = 0; cb < CB; ++cb) {
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
+#ifdef GS_EXP_BWD_NO_DLF
+        const float v = (float)c;
+#else
         const float v = inside ? dL_dfeat[(size_t)(cb * 16 + c) * HW + pix] : 0.f;
+#endif
         s_w[wave][c][lane] = v;
         if constexpr (FIXED_FEAT) dLf_own[cb * 16 + c] = v;
       }
@@ -547,7 +557,9 @@ __global__ __launch_bounds__(256) void render_bwd_kernel(
         s_w[wave][nb][lane] = dch;
         if (lane == 0) s_bgid[wave][nb] = gid;
         if (++nb == WB) {
+#ifndef GS_EXP_BWD_NO_MFMA
           flush_feature_batch<F, WB>(s_w[wave], s_bgid[wave], Bs, dsem, lane, WB);
+#endif
           nb = 0;
         }
       }

@@ -149,6 +149,10 @@ int gs_mark_visible(int64_t P, const float *means3D, const float *viewmatrix,
 #define GS_STAGE_PREPROCESS_BWD 7
 #define GS_NUM_STAGES 8
 int gs_timing_enable(int enable);
+/* Restrict timing to the stages whose bit (1 << GS_STAGE_x) is set (default:
+ * all).  Each timed stage adds an event pair -- a few microseconds of stream
+ * time -- so a benchmark times only the kernel it reports on. */
+int gs_timing_select(uint32_t stage_mask);
 int gs_timing_read(double *ms, int64_t *count, int n_stages);
 
 /* ---- inspection entry points (tests and benchmarks; no reference analogue) */

@@ -21,7 +21,7 @@ from dynamic3dgaussians_amd.camera import camera_rig  # noqa: E402
 from dynamic3dgaussians_amd.scene import make_gaussians  # noqa: E402
 
 
-def run(P, F, W, H, cams, reps, compat, scale_mult=1.0):
+def run(P, F, W, H, cams, reps, compat, scale_mult=1.0, timing=True):
     dev = "cuda"
     g = make_gaussians(P, F=F, seed=0, scale_mult=scale_mult, device=dev)
     rig = camera_rig(27, W, H)[:cams]
@@ -56,7 +56,7 @@ def run(P, F, W, H, cams, reps, compat, scale_mult=1.0):
 
     once()
     torch.cuda.synchronize()
-    _lib.timing_enable(True)
+    _lib.timing_enable(timing)
     s0 = torch.cuda.Event(enable_timing=True)
     s1 = torch.cuda.Event(enable_timing=True)
     s0.record()
@@ -82,11 +82,12 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--compat", default="reference")
     ap.add_argument("--scale-mult", type=float, default=1.0)
+    ap.add_argument("--no-timing", action="store_true", help="no stage events (total time only)")
     a = ap.parse_args()
     _lib.load()
     for F in a.features:
         print(json.dumps(run(a.gaussians, F, a.width, a.height, a.cams, a.reps, a.compat,
-                             a.scale_mult)), flush=True)
+                             a.scale_mult, timing=not a.no_timing)), flush=True)
 
 
 if __name__ == "__main__":
