@@ -124,12 +124,14 @@ __global__ __launch_bounds__(256) void render_fwd_kernel(
     const float* __restrict__ feats, const float* __restrict__ bg, float* __restrict__ out_color,
     float* __restrict__ out_feature, float* __restrict__ out_depth, float* __restrict__ out_alpha,
     uint32_t* __restrict__ n_contrib) {
-  constexpr bool MF = (F == 32 || F == 64);  // features on the matrix cores
+  // Features: 8 / 16 channels on the VALU (v_pk_fma_f32 with the Gaussian's
+  // row in SGPRs, requested at the top of the iteration); 32 / 64 channels on
+  // the matrix cores (measured faster at 32: 223 vs 227 us on the bench scene).
+  constexpr bool MF = (F == 32 || F == 64);
   constexpr int FB = MF ? F / 32 : 1;        // 32-channel blocks
   constexpr int NSF = (!MF && F > 0) ? F : 1;
   // per record: (x, y, -a/2, -b) (-c/2, opacity, r, g) (b, depth, -, -)
   __shared__ float4 s_rec[4][CHUNK][3];
-  __shared__ uint32_t s_gid[4][CHUNK];
 
   const int tile = xcd_remap(blockIdx.x, num_tiles);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -193,7 +195,7 @@ __global__ __launch_bounds__(256) void render_fwd_kernel(
       s_rec[wave][lane][1] = make_float4(h.z, q.q1.y, q.q1.z, q.q1.w);
       s_rec[wave][lane][2] = q.q2;
     }
-    s_gid[wave][lane] = q.gid;
+    const uint32_t chunk_gid = q.gid;  // lane j: id of the chunk's j-th record
     uint64_t mask = __ballot(keep);
     STAT(0, 1);
     STAT(1, range.y - c0 < CHUNK ? range.y - c0 : CHUNK);
@@ -202,6 +204,14 @@ __global__ __launch_bounds__(256) void render_fwd_kernel(
     while (mask) {
       const int j = __builtin_ctzll(mask);
       mask &= ~(1ull << j);
+      // the survivor's feature row, requested before its alpha is computed so
+      // the scalar loads overlap that work
+      float fcur[NSF];
+      if constexpr (!MF && F > 0) {
+        const uint32_t g = __builtin_amdgcn_readlane(chunk_gid, j);
+#pragma unroll
+        for (int c = 0; c < NSF; ++c) fcur[c] = feats[(size_t)g * F + c];
+      }
       STAT(3, 1);
       STAT_INC(st_it);
       const float4 r0 = s_rec[wave][j][0];
@@ -227,9 +237,14 @@ __global__ __launch_bounds__(256) void render_fwd_kernel(
       last = blend ? c0 + j - range.x + 1 : last;
       STAT(4, wave_any(blend));
       STAT(5, __builtin_popcountll(__ballot(blend)));
+      if constexpr (!MF && F > 0) {
+        // keep the row loads above the blend decision (issued early, used late)
+#pragma unroll
+        for (int c = 0; c < NSF; ++c) asm volatile("" ::"s"(fcur[c]));
+      }
       if (F > 0 && wave_any(blend)) {
         {
-          const uint32_t gid = __builtin_amdgcn_readfirstlane(s_gid[wave][j]);
+          const uint32_t gid = __builtin_amdgcn_readlane(chunk_gid, j);
           if constexpr (MF) {
             if (pend == 0) {
               pend = 1;
@@ -249,9 +264,9 @@ __global__ __launch_bounds__(256) void render_fwd_kernel(
               pend = 0;
             }
           } else {
-            const float* f = feats + (size_t)gid * F;
+            (void)gid;
 #pragma unroll
-            for (int c = 0; c < NSF; ++c) SF[c] = fmaf(f[c], w, SF[c]);
+            for (int c = 0; c < NSF; ++c) SF[c] = fmaf(fcur[c], w, SF[c]);
           }
         }
       }
@@ -385,7 +400,11 @@ __global__ __launch_bounds__(256) void render_bwd_kernel(
     const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dpix,
     const float* __restrict__ dL_dfeat, const float* __restrict__ dL_ddepth,
     const float* __restrict__ dL_dalpha, float* __restrict__ acc, float* __restrict__ dsem) {
+#ifdef GS_EXP_BWD_VALU_FEAT
+  constexpr bool MF = false;
+#else
   constexpr bool MF = (F == 32 || F == 64);
+#endif
   constexpr int FB = MF ? F / 32 : 1;
   constexpr int NV = MF ? A_FEAT : A_FEAT + F;  // components reduced on the VALU
   constexpr int WB = 16;                        // Gaussians per MFMA batch
@@ -393,7 +412,6 @@ __global__ __launch_bounds__(256) void render_bwd_kernel(
   constexpr bool FIXED_FEAT = (COMPAT != COMPAT_REFERENCE) && F > 0;
   constexpr int NF_REG = (!MF && F > 0) ? F : 1;
   __shared__ float4 s_rec[4][CHUNK][4];  // the record's 3 float4 + half conic
-  __shared__ uint32_t s_gid[4][CHUNK];
   // batch weights w[g][pixel] (row pad 4: the 16x16x4 A reads are conflict-free)
   __shared__ float s_w[MF ? 4 : 1][MF ? WB : 1][68];
   __shared__ uint32_t s_bgid[MF ? 4 : 1][WB];
@@ -476,7 +494,7 @@ __global__ __launch_bounds__(256) void render_bwd_kernel(
     s_rec[wave][lane][1] = q.q1;
     s_rec[wave][lane][2] = q.q2;
     s_rec[wave][lane][3] = half_conic(q.q0, q.q1);
-    s_gid[wave][lane] = q.gid;
+    const uint32_t chunk_gid = q.gid;  // lane j: id of the chunk's j-th record
     uint64_t mask = __ballot(keep);
     STAT(8, 1);
     STAT(9, hi - c0);
@@ -503,7 +521,7 @@ __global__ __launch_bounds__(256) void render_bwd_kernel(
       STAT(12, wave_any(valid));
       STAT(13, __builtin_popcountll(__ballot(valid)));
       if (!wave_any(valid)) continue;
-      const uint32_t gid = __builtin_amdgcn_readfirstlane(s_gid[wave][j]);
+      const uint32_t gid = __builtin_amdgcn_readlane(chunk_gid, j);
       // Invalid lanes keep dch = dL_dopa = Gv = 0, which zeroes every
       // contribution below without per-component selects.
       float dch = 0.f, dL_dopa = 0.f, Gv = 0.f;
@@ -579,8 +597,13 @@ __global__ __launch_bounds__(256) void render_bwd_kernel(
 template <int F>
 static void fwd_f(const RenderArgs& a, hipStream_t s) {
   dim3 grid(a.num_tiles), block(256);
+#ifdef GS_EXP_FWD_LDS_PAD
+  const size_t pad = GS_EXP_FWD_LDS_PAD;  // occupancy experiment: unused dynamic LDS
+#else
+  const size_t pad = 0;
+#endif
   if (a.compat == COMPAT_REFERENCE)
-    hipLaunchKernelGGL((render_fwd_kernel<F, COMPAT_REFERENCE>), grid, block, 0, s, a.W, a.H, a.grid_x,
+    hipLaunchKernelGGL((render_fwd_kernel<F, COMPAT_REFERENCE>), grid, block, pad, s, a.W, a.H, a.grid_x,
                        a.num_tiles, a.ranges, a.point_list, a.rec, a.feats, a.bg, a.out_color,
                        a.out_feature, a.out_depth, a.out_alpha, a.n_contrib);
   else
