@@ -26,6 +26,7 @@ enum RecField {
   R_DEPTH = 9,                // view-space z
   R_EX = 10, R_EY = 11,       // half extents of the alpha >= 1/255 region
   R_RAD = 12,                 // screen radius (ceil(3 sqrt(lambda_max)))
+  R_TQ = 13,                  // cull threshold on a dx^2 + 2b dx dy + c dy^2
 };
 
 // Gradient accumulation record per Gaussian (backward scratch), sums over

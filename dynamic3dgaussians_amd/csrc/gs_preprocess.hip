@@ -108,21 +108,26 @@ __device__ inline void ewa_cov2d(const Ewa& e, const float c3[6], float out[3]) 
 // skipped by the reference too, so a wave whose 16x4 pixels all lie outside
 // skips the Gaussian as a whole.  Conservative: tau is inflated by the
 // rounding error the fp32 power evaluation can make on this conic.
-__device__ inline void alpha_extent(float ca, float cb, float cc, float op, float& ex, float& ey) {
+// Also returns `tq`, the same inflated threshold on the quadratic form
+// q(d) = a dx^2 + 2 b dx dy + c dy^2 (alpha >= 1/255 needs q <= tq), used by
+// the blend kernels' exact ellipse-vs-strip test; +inf = never cull,
+// -inf = never blends.
+__device__ inline void alpha_extent(float ca, float cb, float cc, float op, float& ex, float& ey, float& tq) {
   const float thr = 1.0f / 255.0f;
-  if (!(op >= thr)) { ex = -INFINITY; ey = -INFINITY; return; }  // never blends
+  if (!(op >= thr)) { ex = -INFINITY; ey = -INFINITY; tq = -INFINITY; return; }  // never blends
   const double a = ca, b = cb, c = cc;
   const double det = a * c - b * b;
   const double tr = a + c;
-  if (!(a > 0.0 && c > 0.0 && det > 0.0)) { ex = INFINITY; ey = INFINITY; return; }
+  if (!(a > 0.0 && c > 0.0 && det > 0.0)) { ex = INFINITY; ey = INFINITY; tq = INFINITY; return; }
   const double disc = sqrt(fmax(tr * tr - 4.0 * det, 0.0));
   const double lmin = 0.5 * (tr - disc), lmax = 0.5 * (tr + disc);
   const double cond = lmin > 0.0 ? lmax / lmin : 1e30;
-  if (!(cond < 5.0e5)) { ex = INFINITY; ey = INFINITY; return; }
+  if (!(cond < 5.0e5)) { ex = INFINITY; ey = INFINITY; tq = INFINITY; return; }
   const double tau = 2.0 * log((double)op / (double)thr);
   const double taup = tau * (1.02 + 32.0 * 6.0e-8 * cond) + 1e-3;
   ex = (float)(sqrt(taup * c / det) + 0.01);
   ey = (float)(sqrt(taup * a / det) + 0.01);
+  tq = (float)(taup * 1.0001 + 1e-4);
 }
 
 // computeColorFromSH forward (forward.cu:20-71), one colour channel at a time.
@@ -223,13 +228,13 @@ __global__ __launch_bounds__(256) void preprocess_fwd_kernel(PreprocessArgs a) {
     a.clamped[g] = cl;
   }
   const float op = a.opacities[g];
-  float ex, ey;
-  alpha_extent(ca, cb, cc, op, ex, ey);
+  float ex, ey, tq;
+  alpha_extent(ca, cb, cc, op, ex, ey, tq);
   float4* rec = reinterpret_cast<float4*>(a.rec + (size_t)REC * g);
   rec[0] = make_float4(px, py, ca, cb);
   rec[1] = make_float4(cc, op, rgb[0], rgb[1]);
   rec[2] = make_float4(rgb[2], pv.z, ex, ey);
-  rec[3] = make_float4((float)rad, 0.f, 0.f, 0.f);
+  rec[3] = make_float4((float)rad, tq, 0.f, 0.f);
   a.radii[g] = (int)rad;
   a.tiles[g] = (uint32_t)((rmax.y - rmin.y) * (rmax.x - rmin.x));
   reinterpret_cast<ushort4*>(a.rect)[g] =

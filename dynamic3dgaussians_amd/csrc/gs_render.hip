@@ -80,13 +80,13 @@ __device__ inline void swap32(float a, float b, float& lo, float& hi) {
   hi = bits_f(r[1]);
 }
 
-// Gather the record of list entry i (fields 0..11).  The index is clamped to
-// the last entry of the (non-empty) range, so the loads are unconditional:
+// Gather the record of list entry i (all 16 fields).  The index is clamped
+// to the last entry of the (non-empty) range, so the loads are unconditional:
 // lanes past the end re-read a valid record and are masked out by the caller.
 // (A conditional update of a register struct made the compiler keep it in
 // scratch memory.)
 struct RecRegs {
-  float4 q0, q1, q2;
+  float4 q0, q1, q2, q3;
   uint32_t gid;
 };
 __device__ inline RecRegs load_rec(const uint32_t* __restrict__ point_list, const float* __restrict__ rec,
@@ -97,6 +97,7 @@ __device__ inline RecRegs load_rec(const uint32_t* __restrict__ point_list, cons
   r.q0 = p[0];  // x, y, conic a, conic b
   r.q1 = p[1];  // conic c, opacity, r, g
   r.q2 = p[2];  // b, depth, ext x, ext y
+  r.q3 = p[3];  // radius, cull threshold tq, -, -
   return r;
 }
 
@@ -111,8 +112,24 @@ __device__ inline float gauss_power(float dx, float dy, const float4& h) {
   return fmaf(h.x * dx, dx, fmaf(h.z * dy, dy, (h.y * dx) * dy));
 }
 
+// Can the Gaussian reach alpha >= 1/255 at any pixel centre of the strip
+// [sx0, sx1] x [sy0, sy1]?  The minimum of the quadratic form over the strip
+// rectangle (0 when the mean is inside, else the least of the four clamped
+// edge minima) against the record's inflated threshold tq (preprocess:
+// alpha_extent).  Exact up to that margin, so it culls the Gaussians whose
+// bounding box touches the strip but whose ellipse does not; a culled
+// Gaussian is one every pixel of the strip would skip in the reference loop.
 __device__ inline bool strip_culled(const RecRegs& q, float sx0, float sx1, float sy0, float sy1) {
-  return q.q0.x + q.q2.z < sx0 || q.q0.x - q.q2.z > sx1 || q.q0.y + q.q2.w < sy0 || q.q0.y - q.q2.w > sy1;
+  const float a = q.q0.z, b = q.q0.w, c = q.q1.x, tq = q.q3.y;
+  const float xlo = q.q0.x - sx1, xhi = q.q0.x - sx0;  // offsets mean - pixel
+  const float ylo = q.q0.y - sy1, yhi = q.q0.y - sy0;
+  if (xlo <= 0.f && xhi >= 0.f && ylo <= 0.f && yhi >= 0.f) return !(tq >= 0.f);
+  auto qf = [&](float x, float y) { return fmaf(a * x, x, fmaf(c * y, y, 2.f * b * x * y)); };
+  const float ra = fast_rcp(a), rc = fast_rcp(c);
+  const float ty0 = fminf(fmaxf(-b * xlo * rc, ylo), yhi), ty1 = fminf(fmaxf(-b * xhi * rc, ylo), yhi);
+  const float tx0 = fminf(fmaxf(-b * ylo * ra, xlo), xhi), tx1 = fminf(fmaxf(-b * yhi * ra, xlo), xhi);
+  const float m = fminf(fminf(qf(xlo, ty0), qf(xhi, ty1)), fminf(qf(tx0, ylo), qf(tx1, yhi)));
+  return m > tq;  // NaN keeps the Gaussian
 }
 
 // ------------------------------------------------------------------ forward
