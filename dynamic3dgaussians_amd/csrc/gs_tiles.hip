@@ -168,8 +168,9 @@ __global__ __launch_bounds__(OFF_T) void tile_offsets_kernel(const uint32_t* __r
 }
 
 // One tile per workgroup: LSD radix sort of its (depth bits << 32 | id) keys
-// on the 32 depth bits, 8 bits a pass (passes whose digit is the same for
-// every key are skipped).  Wave w owns the contiguous quarter
+// on the depth bits relative to the tile's minimum, 8 bits a pass, only as
+// many passes as the tile's depth-bit span needs (and passes whose digit is
+// the same for every key are skipped).  Wave w owns the contiguous quarter
 // [w*q, (w+1)*q) of the keys; per pass it counts digits per wave (ballot
 // match, one leader per digit and round), a 256-thread scan turns the counts
 // into per-(wave, digit) bases, and each wave scatters its keys in order --
@@ -179,20 +180,24 @@ __global__ __launch_bounds__(OFF_T) void tile_offsets_kernel(const uint32_t* __r
 // Keys live in LDS (two buffers) or, for tiles longer than the launch's LDS
 // capacity, in global memory (the keys segment and its twin in keys2).
 __device__ inline uint64_t match_digit8(uint32_t d, uint64_t valid) {
-  uint64_t peers = valid;
+  // peers &= (bit set ? ballot : ~ballot), per 32-bit half: with s = 0 / -1
+  // the sign-extended bit, keep = ~(ballot ^ s) -> peers & ~(ballot ^ s)
+  uint32_t lo = (uint32_t)valid, hi = (uint32_t)(valid >> 32);
 #pragma unroll
   for (int b = 0; b < 8; ++b) {
-    const bool set = (d >> b) & 1u;
-    const uint64_t m = __ballot(set);
-    peers &= set ? m : ~m;
+    const uint64_t m = __ballot((d >> b) & 1u);
+    const uint32_t sx = ~(uint32_t)__builtin_amdgcn_sbfe(d, b, 1);  // bit set -> 0, clear -> ~0
+    lo &= ~((uint32_t)m ^ ~sx);
+    hi &= ~((uint32_t)(m >> 32) ^ ~sx);
   }
-  return peers;
+  return ((uint64_t)hi << 32) | lo;
 }
 
 struct RadixSmem {
   uint32_t wcnt[4][256];  // per-wave digit counts, then per-wave bases
   uint32_t wsum[4];
   int skip, unsorted;
+  uint32_t dmin, dmax;  // depth-bit range of the tile
 };
 
 template <class KP>
@@ -202,7 +207,22 @@ __device__ __attribute__((always_inline)) KP tile_radix_sort(KP A, KP B, int n, 
   const int q = (n + 3) >> 2;
   const int w0 = min(n, wave * q), w1 = min(n, w0 + q);
   KP src = A, dst = B;
-  for (int shift = 32; shift < 64; shift += 8) {
+  // Sort on depth bits relative to the tile's minimum: positive float bits
+  // order like the floats, and only the bits that vary need passes.
+  if (tid == 0) { sm.dmin = 0xFFFFFFFFu; sm.dmax = 0u; }
+  uint32_t lmin = 0xFFFFFFFFu, lmax = 0u;
+  for (int i = tid; i < n; i += TS_THREADS) {
+    const uint32_t h = (uint32_t)(src[i] >> 32);
+    lmin = min(lmin, h);
+    lmax = max(lmax, h);
+  }
+  __syncthreads();
+  atomicMin(&sm.dmin, lmin);
+  atomicMax(&sm.dmax, lmax);
+  __syncthreads();
+  const uint32_t dmin = sm.dmin, span = sm.dmax - dmin;
+  const int nbits = span ? 32 - __builtin_clz(span) : 0;
+  for (int shift = 0; shift < nbits; shift += 8) {
 #pragma unroll
     for (int w = 0; w < 4; ++w) sm.wcnt[w][tid] = 0;
     if (tid == 0) sm.skip = 0;
@@ -210,9 +230,8 @@ __device__ __attribute__((always_inline)) KP tile_radix_sort(KP A, KP B, int n, 
     for (int i0 = w0; i0 < w1; i0 += 64) {
       const int i = i0 + lane;
       const bool valid = i < w1;
-      const uint32_t d = valid ? (uint32_t)(src[i] >> shift) & 255u : 0u;
-      const uint64_t peers = match_digit8(d, __ballot(valid));
-      if (valid && (peers & lt) == 0) sm.wcnt[wave][d] += (uint32_t)__popcll(peers);
+      // counts need no order: one LDS atomic per key
+      if (valid) atomicAdd(&sm.wcnt[wave][(((uint32_t)(src[i] >> 32) - dmin) >> shift) & 255u], 1u);
     }
     __syncthreads();
     const uint32_t c0 = sm.wcnt[0][tid], c1 = sm.wcnt[1][tid], c2 = sm.wcnt[2][tid], c3 = sm.wcnt[3][tid];
@@ -241,7 +260,7 @@ __device__ __attribute__((always_inline)) KP tile_radix_sort(KP A, KP B, int n, 
       const int i = i0 + lane;
       const bool valid = i < w1;
       const uint64_t k = valid ? src[i] : 0ull;
-      const uint32_t d = (uint32_t)(k >> shift) & 255u;
+      const uint32_t d = (((uint32_t)(k >> 32) - dmin) >> shift) & 255u;
       const uint64_t peers = match_digit8(d, __ballot(valid));
       const uint64_t below = peers & lt;
       const uint32_t base = sm.wcnt[wave][d];
