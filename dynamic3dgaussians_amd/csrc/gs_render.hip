@@ -120,6 +120,9 @@ __device__ inline float gauss_power(float dx, float dy, const float4& h) {
 // bounding box touches the strip but whose ellipse does not; a culled
 // Gaussian is one every pixel of the strip would skip in the reference loop.
 __device__ inline bool strip_culled(const RecRegs& q, float sx0, float sx1, float sy0, float sy1) {
+#ifdef GS_EXP_BOX_CULL
+  return q.q0.x + q.q2.z < sx0 || q.q0.x - q.q2.z > sx1 || q.q0.y + q.q2.w < sy0 || q.q0.y - q.q2.w > sy1;
+#endif
   const float a = q.q0.z, b = q.q0.w, c = q.q1.x, tq = q.q3.y;
   const float xlo = q.q0.x - sx1, xhi = q.q0.x - sx0;  // offsets mean - pixel
   const float ylo = q.q0.y - sy1, yhi = q.q0.y - sy0;
