@@ -68,12 +68,20 @@ def setup_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # Rehearsal knobs for a one-GPU box (never used by the driver's runs):
+    # GS_BENCH_BACKEND=gloo with GS_BENCH_SHARE_GPU=1 puts every rank on
+    # cuda:0 and exchanges the gradient bucket over gloo.
+    backend = os.environ.get("GS_BENCH_BACKEND", "nccl")
+    dev_index = 0 if os.environ.get("GS_BENCH_SHARE_GPU") == "1" else local
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(dev_index)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
-    return world, rank, torch.device("cuda", local if world > 1 else 0)
+    return world, rank, torch.device("cuda", dev_index if world > 1 else 0)
 
 
 def make_params(args, dev):
