@@ -257,6 +257,7 @@ __global__ __launch_bounds__(256) void render_fwd_kernel(
       last = blend ? c0 + j - range.x + 1 : last;
       STAT(4, wave_any(blend));
       STAT(5, __builtin_popcountll(__ballot(blend)));
+      STAT(18, wave_any(blend) && ((__ballot(blend) & 0xFFFFFFFFull) == 0 || (__ballot(blend) >> 32) == 0));
       if constexpr (!MF && F > 0) {
         // keep the row loads above the blend decision (issued early, used late)
 #pragma unroll
@@ -466,20 +467,27 @@ __global__ __launch_bounds__(256) void render_bwd_kernel(
   float Bs[MF ? CB : 1][MF ? 16 : 1];
   float dLf_own[FIXED_FEAT && MF ? F : 1];  // fixed mode also needs f . dLf per pixel
   if constexpr (MF) {
+    // B operands straight from the CHW image: lane l, step s reads channel
+    // 16cb + (l&15) at strip pixel 4s + (l>>4) (4 lanes share a 16-B run of
+    // one row); the loads are first needed at the first batch flush.
 #pragma unroll
-    for (int cb = 0; cb < CB; ++cb) {
+    for (int s = 0; s < 16; ++s) {
+      const int p = 4 * s + (lane >> 4);
+      const int qx = tx * TILE + (p & 15), qy = ty * TILE + wave * WAVE_ROWS + (p >> 4);
+      const bool qin = qx < W && qy < H;
+      const size_t qpix = qin ? (size_t)qy * W + qx : 0;
 #pragma unroll
-      for (int c = 0; c < 16; ++c) {
+      for (int cb = 0; cb < CB; ++cb) {
 #ifdef GS_EXP_BWD_NO_DLF
-        const float v = (float)c;
+        Bs[cb][s] = (float)cb;
 #else
-        const float v = inside ? dL_dfeat[(size_t)(cb * 16 + c) * HW + pix] : 0.f;
+        Bs[cb][s] = qin ? dL_dfeat[(size_t)(cb * 16 + (lane & 15)) * HW + qpix] : 0.f;
 #endif
-        s_w[wave][c][lane] = v;
-        if constexpr (FIXED_FEAT) dLf_own[cb * 16 + c] = v;
       }
+    }
+    if constexpr (FIXED_FEAT) {
 #pragma unroll
-      for (int s = 0; s < 16; ++s) Bs[cb][s] = s_w[wave][lane & 15][4 * s + (lane >> 4)];
+      for (int c = 0; c < F; ++c) dLf_own[c] = inside ? dL_dfeat[(size_t)c * HW + pix] : 0.f;
     }
   } else {
 #pragma unroll

@@ -26,7 +26,7 @@ from tools.stage_bench import run  # noqa: E402
 
 NAMES = {0: "fwd_chunks", 1: "fwd_records", 2: "fwd_survivors", 3: "fwd_iters",
          4: "fwd_iters_active", 5: "fwd_active_lanes", 6: "fwd_waves", 7: "fwd_list_total",
-         8: "bwd_chunks", 9: "bwd_records", 10: "bwd_survivors", 11: "bwd_iters",
+         18: "fwd_iters_one_half_active", 8: "bwd_chunks", 9: "bwd_records", 10: "bwd_survivors", 11: "bwd_iters",
          12: "bwd_iters_active", 13: "bwd_active_lanes", 14: "bwd_waves", 15: "bwd_walk_total"}
 MAXES = {16: "fwd_wave_iters_max", 17: "bwd_wave_iters_max"}
 HISTS = {20: "fwd_wave_iters_hist", 25: "bwd_wave_iters_hist"}  # <256,<512,<1024,<2048,more
