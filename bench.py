@@ -222,7 +222,7 @@ def main():
         {"params": [params["logit_opacities"]], "lr": 0.05},
         {"params": [params["log_scales"]], "lr": 1e-3},
     ] + ([{"params": [params["semantic_feature"]], "lr": 1e-3}] if args.features else []),
-        lr=0.0, eps=1e-15)
+        lr=0.0, eps=1e-15, fused=os.environ.get("GS_BENCH_FUSED_ADAM", "0") == "1")
     bucket = GradBucket(list(params.values()))
     g = torch.Generator(device=dev).manual_seed(1 + rank)
     H_, W_ = args.height, args.width

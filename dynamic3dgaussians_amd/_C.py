@@ -199,7 +199,10 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, semantic_fe
     inp = _Inputs(means3D, colors, semantic_feature, None, scales, rotations, scale_modifier,
                   cov3D_precomp, sh, degree)
     dev, P = inp.device, inp.P
-    H, W = dL_dout_color.size(1), dL_dout_color.size(2)  # rasterize_points.cu:160-161
+    # rasterize_points.cu:160-161 takes H, W from dL_dout_color; an absent
+    # (None / empty) upstream gradient counts as zeros, sized from the alpha image
+    img_ref = dL_dout_color if _present(dL_dout_color) else alphas
+    H, W = img_ref.size(-2), img_ref.size(-1)
     f32 = dict(dtype=torch.float32, device=dev)
     if P == 0:
         z = lambda *s: torch.zeros(*s, **f32)  # noqa: E731
@@ -213,18 +216,15 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, semantic_fe
         if gm.numel() != P:
             raise RuntimeError(f"grad_mask must have {P} elements, got {gm.numel()}")
         g.grad_mask = gm.data_ptr()
-    dLc = _dev(dL_dout_color, dev, "dL_dout_color")
-    dLd = _dev(dL_dout_depth, dev, "dL_dout_depth")
-    dLa = _dev(dL_dout_alpha, dev, "dL_dout_alpha")
+    dLc = _dev(dL_dout_color, dev, "dL_dout_color") if _present(dL_dout_color) else None
+    dLd = _dev(dL_dout_depth, dev, "dL_dout_depth") if _present(dL_dout_depth) else None
+    dLa = _dev(dL_dout_alpha, dev, "dL_dout_alpha") if _present(dL_dout_alpha) else None
     alphas_c = _dev(alphas, dev, "alpha")
     dLf = None
-    if inp.F:
-        if _present(dL_dout_feature):
-            dLf = _dev(dL_dout_feature, dev, "dL_dout_feature").reshape(-1, H, W)
-            if dLf.size(0) < inp.F:
-                dLf = torch.cat([dLf, torch.zeros(inp.F - dLf.size(0), H, W, **f32)]).contiguous()
-        else:
-            dLf = torch.zeros(inp.F, H, W, **f32)
+    if inp.F and _present(dL_dout_feature):
+        dLf = _dev(dL_dout_feature, dev, "dL_dout_feature").reshape(-1, H, W)
+        if dLf.size(0) < inp.F:
+            dLf = torch.cat([dLf, torch.zeros(inp.F - dLf.size(0), H, W, **f32)]).contiguous()
     radii_c = radii.to(device=dev, dtype=torch.int32).contiguous()
     out = dict(
         dmeans2D=torch.empty(P, 3, **f32), dcolors=torch.empty(P, 3, **f32),
@@ -237,7 +237,7 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, semantic_fe
     p = lambda t: t.data_ptr() if (t is not None and t.numel()) else None  # noqa: E731
     check(L_.gs_backward(ctypes.byref(g), ctypes.byref(cam), radii_c.data_ptr(), int(bool(debug)), cm,
                          geomBuffer.data_ptr(), p(binningBuffer), imageBuffer.data_ptr(), int(R),
-                         alphas_c.data_ptr(), dLc.data_ptr(), p(dLf), dLd.data_ptr(), dLa.data_ptr(),
+                         alphas_c.data_ptr(), p(dLc), p(dLf), p(dLd), p(dLa),
                          scratch.data_ptr(), out["dmeans2D"].data_ptr(), out["dcolors"].data_ptr(),
                          p(out["dsem"]), out["dopacity"].data_ptr(), out["dmeans3D"].data_ptr(),
                          out["dcov3D"].data_ptr(), p(out["dsh"]), out["dscales"].data_ptr(),

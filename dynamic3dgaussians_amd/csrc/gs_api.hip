@@ -307,8 +307,7 @@ int gs_backward(const gs_gaussians* g, const gs_camera* cam, const int32_t* radi
   const int P = g->P;
   if (P == 0) return 0;
   if (!geom || !image || !scratch || !radii || (L > 0 && !binning)) return fail(-1, "state buffers are required");
-  if (!alphas || !dL_dout_color || !dL_dout_depth || !dL_dout_alpha || (g->F > 0 && !dL_dout_feature))
-    return fail(-1, "upstream gradients are required");
+  if (!alphas) return fail(-1, "the forward's alpha image is required");
   if (!dL_dmeans2D || !dL_dcolors || !dL_dopacity || !dL_dmeans3D || !dL_dcov3D || !dL_dscales ||
       !dL_drotations || (g->F > 0 && !dL_dsemantic) || (g->M > 0 && !dL_dsh))
     return fail(-1, "gradient outputs are required");

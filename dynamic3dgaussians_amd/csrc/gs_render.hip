@@ -452,11 +452,12 @@ __global__ __launch_bounds__(256) void render_bwd_kernel(
   float T = T_final;
   const uint32_t last = inside ? n_contrib[pix] : 0u;
   float dLp[3];
-  dLp[0] = inside ? dL_dpix[pix] : 0.f;
-  dLp[1] = inside ? dL_dpix[HW + pix] : 0.f;
-  dLp[2] = inside ? dL_dpix[2 * HW + pix] : 0.f;
-  const float dLd = inside ? dL_ddepth[pix] : 0.f;
-  const float dLa = inside ? dL_dalpha[pix] : 0.f;
+  // absent upstream gradients (NULL) are zeros
+  dLp[0] = inside && dL_dpix ? dL_dpix[pix] : 0.f;
+  dLp[1] = inside && dL_dpix ? dL_dpix[HW + pix] : 0.f;
+  dLp[2] = inside && dL_dpix ? dL_dpix[2 * HW + pix] : 0.f;
+  const float dLd = inside && dL_ddepth ? dL_ddepth[pix] : 0.f;
+  const float dLa = inside && dL_dalpha ? dL_dalpha[pix] : 0.f;
   const float bg_dot = bg[0] * dLp[0] + bg[1] * dLp[1] + bg[2] * dLp[2];
 
   // Upstream feature gradients.  VALU path: one register per channel.
@@ -481,17 +482,17 @@ __global__ __launch_bounds__(256) void render_bwd_kernel(
 #ifdef GS_EXP_BWD_NO_DLF
         Bs[cb][s] = (float)cb;
 #else
-        Bs[cb][s] = qin ? dL_dfeat[(size_t)(cb * 16 + (lane & 15)) * HW + qpix] : 0.f;
+        Bs[cb][s] = qin && dL_dfeat ? dL_dfeat[(size_t)(cb * 16 + (lane & 15)) * HW + qpix] : 0.f;
 #endif
       }
     }
     if constexpr (FIXED_FEAT) {
 #pragma unroll
-      for (int c = 0; c < F; ++c) dLf_own[c] = inside ? dL_dfeat[(size_t)c * HW + pix] : 0.f;
+      for (int c = 0; c < F; ++c) dLf_own[c] = inside && dL_dfeat ? dL_dfeat[(size_t)c * HW + pix] : 0.f;
     }
   } else {
 #pragma unroll
-    for (int c = 0; c < NF_REG; ++c) dLf[c] = (F > 0 && inside) ? dL_dfeat[c * HW + pix] : 0.f;
+    for (int c = 0; c < NF_REG; ++c) dLf[c] = (F > 0 && inside && dL_dfeat) ? dL_dfeat[c * HW + pix] : 0.f;
   }
 
   // The reference carries per-channel "accum_rec" recurrences

@@ -99,6 +99,9 @@ class _RasterizeGaussians(torch.autograd.Function):
 
         ctx.raster_settings = raster_settings
         ctx.num_rendered = num_rendered
+        # outputs without a gradient arrive as None (no zero images are
+        # materialized); the binding treats them as zeros
+        ctx.set_materialize_grads(False)
         ctx.compat = compat
         ctx.c_xy = (c_x, c_y)
         ctx.sem_shape = None if semantic_feature is None else tuple(semantic_feature.shape)

@@ -115,6 +115,8 @@ int gs_forward_render(const gs_gaussians *g, const gs_camera *cam, int debug,
 /* Backward -- replaces RasterizeGaussiansBackwardCUDA / Rasterizer::backward
  * (DGR/rasterize_points.cu:128-225, CR/rasterizer_impl.cu:350-467).
  * Every element of every gradient output is written (no pre-zeroing needed).
+ * Upstream gradients (dL_dout_*) may be NULL: an output that received no
+ * gradient counts as zeros (autograd's unmaterialized grads).
  * dL_dmeans2D P x 3, dL_dcolors P x 3, dL_dsemantic P x F, dL_dopacity P,
  * dL_dmeans3D P x 3, dL_dcov3D P x 6, dL_dsh P x M x 3, dL_dscales P x 3,
  * dL_drotations P x 4. */

@@ -280,3 +280,26 @@ def test_reference_mode_alpha_is_zero():
     assert H.gpu_forward(inp, "reference")[4].abs().sum().item() == 0
     a = H.gpu_forward(inp, "fixed")[4]
     assert a.max().item() > 0.5
+
+
+def test_absent_upstream_gradients_are_zeros():
+    """Unused outputs give None grads (no materialized zeros); the binding
+    treats them as zero images -- same result as passing zeros."""
+    inp = H.scene(F=8)
+    g = H.gpu_forward(inp)
+    z = H.upstream_grads(inp["image_height"], inp["image_width"], 8)
+    dc, df, dd, da = z
+    zeros = [dc, torch.zeros_like(df), dd, torch.zeros_like(da)]
+    full = H.gpu_backward(inp, g, zeros)
+    num_rendered, color, feat, depth, alpha, radii, geom, binning, img = g
+    d = lambda k: H._to(inp[k], H.DEV)  # noqa: E731
+    part = _C.rasterize_gaussians_backward(
+        d("bg"), d("means3D"), radii, d("colors"), d("semantic_feature"), d("scales"),
+        d("rotations"), 1.0, d("cov3D_precomp"), d("viewmatrix"), d("projmatrix"),
+        *H.bwd_cam4(inp, True), dc.to(H.DEV), None, dd.to(H.DEV), None, d("sh"), inp["degree"],
+        d("campos"), geom, num_rendered, binning, img, alpha, False)
+    for a, b in zip(full, part):
+        b = b.cpu().numpy()
+        assert a.shape == b.shape
+        if a.size:
+            assert H.rel_l2(b, a) <= 1e-5 or np.abs(a).max() == 0
