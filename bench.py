@@ -159,6 +159,30 @@ def load_pmc_traffic(stage):
         return None
 
 
+# stage -> (kernel key in profiles/pmc_valu.json, matrix-core cycles per MFMA)
+VALU_KERNEL = {"render_bwd": ("render_bwd", 32), "render_fwd": ("render_fwd", 64),
+               "sort": ("tile_sort", 0), "duplicate": ("tile_hist_kernel<true>", 0),
+               "preprocess": ("preprocess_fwd", 0), "preprocess_bwd": ("preprocess_bwd", 0)}
+SIMDS, CLOCK_GHZ, VALU_ISSUE_CYC = 1024, 2.4, 4  # MI355X: 256 CUs x 4 SIMDs; wave64 VALU = 4 cycles
+
+
+def valu_view(stage, avg_ms):
+    """Issue-rate view of a kernel (the blend kernels are VALU/MFMA-issue
+    bound): committed per-launch instruction counts
+    (profiles/pmc_valu.json) over the live launch time."""
+    try:
+        d = json.load(open(os.path.join(REPO, "profiles", "pmc_valu.json")))["kernels"]
+        key, mfma_cyc = VALU_KERNEL[stage]
+        k = d[key]
+    except Exception:
+        return None
+    cyc = k["SQ_INSTS_VALU"] * VALU_ISSUE_CYC + k.get("SQ_INSTS_MFMA", 0) * mfma_cyc
+    avail = SIMDS * CLOCK_GHZ * 1e9 * avg_ms * 1e-3
+    return {"valu_insts_per_launch": k["SQ_INSTS_VALU"], "mfma_insts_per_launch": k.get("SQ_INSTS_MFMA", 0),
+            "issue_cycles_per_launch": int(cyc), "issue_frac": round(cyc / avail, 4),
+            "peak": f"{SIMDS} SIMDs x {CLOCK_GHZ} GHz, {VALU_ISSUE_CYC} cycles per wave64 VALU instruction"}
+
+
 def cpu_baseline(args, params, label, cam, settings, dev):
     """The CPU oracle (plain C restatement, 1 thread) on one camera of the same
     scene: forward + backward.  Also returns the PSNR of the HIP render of the
@@ -314,7 +338,8 @@ def main():
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic, "kernel": dom, "avg_launch_ms": round(avg_ms, 4),
-                "alg_bytes_per_launch": int(alg_per_launch)}
+                "alg_bytes_per_launch": int(alg_per_launch),
+                "issue": valu_view(dom, avg_ms)}
 
     result = {
         "metric": METRIC, "value": round(value, 3), "unit": "Mpix/s", "n_gpus": world,
