@@ -20,7 +20,7 @@ ABI_VERSION = 3  # include/gsplat_hip.h GS_ABI_VERSION
 c_int32, c_int64, c_float, c_size_t = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_size_t
 
 GS_COMPAT = {"reference": 0, "fixed": 1}
-SUPPORTED_F = (0, 8, 16, 32, 64)
+SUPPORTED_F = (0, 4, 8, 16, 32, 64)
 
 
 class GsGaussians(ctypes.Structure):

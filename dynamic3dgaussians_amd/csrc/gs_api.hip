@@ -58,7 +58,7 @@ T* at(void* base, size_t off) { return reinterpret_cast<T*>(static_cast<char*>(b
 template <class T>
 const T* at(const void* base, size_t off) { return reinterpret_cast<const T*>(static_cast<const char*>(base) + off); }
 
-bool feature_supported(int F) { return F == 0 || F == 8 || F == 16 || F == 32 || F == 64; }
+bool feature_supported(int F) { return F == 0 || F == 4 || F == 8 || F == 16 || F == 32 || F == 64; }
 
 int check_gaussians(const gs_gaussians* g, const gs_camera* c, bool forward) {
   if (!g || !c) return fail(-1, "null argument block");
@@ -66,7 +66,7 @@ int check_gaussians(const gs_gaussians* g, const gs_camera* c, bool forward) {
   if (c->image_width <= 0 || c->image_height <= 0)
     return fail(-1, "image size must be positive (got %dx%d)", c->image_width, c->image_height);
   if (!feature_supported(g->F))
-    return fail(-1, "semantic feature width %d not instantiated (0, 8, 16, 32, 64)", g->F);
+    return fail(-1, "semantic feature width %d not instantiated (0, 4, 8, 16, 32, 64)", g->F);
   if (g->P > 0) {
     if (!g->means3D || (forward && !g->opacities)) return fail(-1, "means3D and opacities are required");
     if (!c->viewmatrix || !c->projmatrix || !c->campos || !c->background)

@@ -658,6 +658,7 @@ bool launch_render_fwd(const RenderArgs& a, hipStream_t s) {
   if (a.num_tiles <= 0) return true;
   switch (a.F) {
     case 0: fwd_f<0>(a, s); return true;
+    case 4: fwd_f<4>(a, s); return true;
     case 8: fwd_f<8>(a, s); return true;
     case 16: fwd_f<16>(a, s); return true;
     case 32: fwd_f<32>(a, s); return true;
@@ -670,6 +671,7 @@ bool launch_render_bwd(const RenderBwdArgs& a, hipStream_t s) {
   if (a.num_tiles <= 0) return true;
   switch (a.F) {
     case 0: bwd_f<0>(a, s); return true;
+    case 4: bwd_f<4>(a, s); return true;
     case 8: bwd_f<8>(a, s); return true;
     case 16: bwd_f<16>(a, s); return true;
     case 32: bwd_f<32>(a, s); return true;

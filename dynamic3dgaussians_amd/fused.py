@@ -1,0 +1,69 @@
+"""Fused colour + segmentation rendering.
+
+The reference training step rasterizes every camera twice: once for colour
+(`train.py:145`, `dyn_train.py:244`) and once more with
+`colors_precomp = params['seg_colors']` for the segmentation image
+(`train.py:246-249`).  Both passes share the geometry, so here the seg
+colours ride along as 3 extra feature channels of the colour pass -- one
+projection, one binning, one blend -- and come back as the seg image.
+
+In the reference numerics (compat="reference") the feature channels receive
+the background exactly like colour (`CR/forward.cu:398-404`, Q4: bg[ch] for
+ch < 3), and the blend adds w * feature with the same fp32 fma as colour, so
+the fused seg image is bit-identical to the reference's second render
+(`tests/test_gpu_parity.py::test_fused_colour_seg_matches_two_passes`).
+
+Gradients.  dL/dseg_colors is the same per-Gaussian sum of w * dL/dseg as
+the second pass's dL/dcolors_precomp.  Geometry: in reference numerics the
+feature term of dL/dalpha is dead (Q5, `CR/backward.cu:596-612`), so the fused
+pass's geometry and means2D gradients are exactly the colour render's -- what
+the reference wants for densification ("Gradient only accum from colour
+render", `train.py:245`) -- while two passes would add the seg image's
+geometry term (the reference's seg loss is disabled, `train.py:250`, so its
+training sees no difference).  In compat="fixed" features feed dL/dalpha, so
+the fused pass gives the full two-pass gradient, with means2D carrying the sum
+of both renders' screen-space gradients; the background is added to seg as
+(1 - alpha) * bg there, since fixed-mode features get no background.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+
+from ._C import get_default_compat as _default_compat
+from .rasterizer import GaussianRasterizer
+
+
+def render_colour_and_seg(raster_settings, means3D: torch.Tensor, means2D: torch.Tensor,
+                          opacities: torch.Tensor, seg_colors: torch.Tensor,
+                          colors_precomp: Optional[torch.Tensor] = None,
+                          shs: Optional[torch.Tensor] = None, scales=None, rotations=None,
+                          cov3D_precomp=None, semantic_feature: Optional[torch.Tensor] = None,
+                          label=None) -> Tuple[torch.Tensor, ...]:
+    """One rasterization for the colour image AND the seg image.
+
+    Returns (colour[3,H,W], radii[P], depth[1,H,W], seg[3,H,W]) -- plus the
+    caller's own semantic feature map [F,H,W] as a fifth element when
+    `semantic_feature` is given (the seg channels are appended after it).
+    """
+    if seg_colors.dim() != 2 or seg_colors.size(1) != 3:
+        raise ValueError("seg_colors must be [P, 3]")
+    F_user = 0 if semantic_feature is None else semantic_feature.reshape(means3D.size(0), -1).size(1)
+    if F_user:
+        # the seg channels go first so that they get the background (ch < 3)
+        feats = torch.cat([seg_colors, semantic_feature.reshape(means3D.size(0), -1)], dim=1)
+    else:
+        feats = seg_colors
+    ras = GaussianRasterizer(raster_settings)
+    lab = label if label is not None else torch.ones(means3D.size(0), device=means3D.device)
+    color, radii, feature_map, depth, alpha = ras(
+        means3D=means3D, means2D=means2D, opacities=opacities, shs=shs, colors_precomp=colors_precomp,
+        semantic_feature=feats, scales=scales, rotations=rotations, cov3D_precomp=cov3D_precomp, label=lab)
+    seg = feature_map[:3]
+    compat = getattr(raster_settings, "compat", None) or _default_compat()
+    if compat != "reference":
+        seg = seg + (1.0 - alpha) * raster_settings.bg.reshape(3, 1, 1)
+    if F_user:
+        return color, radii, depth, seg, feature_map[3:]
+    return color, radii, depth, seg

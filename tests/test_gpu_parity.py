@@ -113,7 +113,7 @@ def test_preprocess_and_binning_bitexact(kw):
 @pytest.mark.parametrize("kw", [
     dict(), dict(F=32), dict(F=8, use_sh=True, sh_degree=3), dict(F=16, use_cov=True),
     dict(F=64, W=80, H=48), dict(F=32, bg=(0.2, 0.5, 0.9)), dict(W=100, H=75, P=4000),
-    dict(F=32, cx=30.0, cy=60.0)])
+    dict(F=32, cx=30.0, cy=60.0), dict(F=3, bg=(0.2, 0.5, 0.9))])
 def test_forward_parity(compat, kw):
     _cmp_forward(H.scene(**kw), compat, kw.get("F", 0))
 
@@ -137,7 +137,7 @@ GRAD_NAMES = ["dmeans2D", "dcolors", "dsemantic", "dopacity", "dmeans3D", "dcov3
 @pytest.mark.parametrize("kw", [
     dict(), dict(F=32), dict(F=8, use_sh=True, sh_degree=3), dict(F=16, use_cov=True),
     dict(F=32, bg=(0.3, 0.1, 0.7)), dict(W=100, H=75, P=4000, use_sh=True, sh_degree=1),
-    dict(F=32, cx=30.0, cy=60.0)])
+    dict(F=32, cx=30.0, cy=60.0), dict(F=3, bg=(0.3, 0.1, 0.7))])
 def test_backward_parity(compat, kw):
     inp = H.scene(**kw)
     F = kw.get("F", 0)
