@@ -39,7 +39,15 @@ class GsCamera(ctypes.Structure):
                 ("image_width", c_int32), ("image_height", c_int32)]
 
 
+class GsNeighborGraph(ctypes.Structure):
+    """include/gs_neighbor.h gs_neighbor_graph."""
+    _fields_ = [("N", c_int64), ("K", c_int32), ("_pad", c_int32), ("nbr", c_void_p),
+                ("weight", c_void_p), ("dist", c_void_p), ("prev_offset", c_void_p),
+                ("prev_inv_rot", c_void_p), ("rev_ptr", c_void_p), ("rev_pos", c_void_p)]
+
+
 P_G = ctypes.POINTER(GsGaussians)
+P_NG = ctypes.POINTER(GsNeighborGraph)
 P_C = ctypes.POINTER(GsCamera)
 
 # name -> (restype, argtypes); must match include/gsplat_hip.h
@@ -67,6 +75,14 @@ PROTOTYPES = {
     "gs_sort_pairs": (ctypes.c_int, [c_int64, c_void_p, c_void_p, ctypes.c_int, c_void_p, c_void_p]),
     "gs_test_wave_reduce": (ctypes.c_int, [ctypes.c_int, c_void_p, c_void_p, c_void_p]),
     "gs_timing_enable": (ctypes.c_int, [ctypes.c_int]),
+    # include/gs_neighbor.h
+    "gs_neighbor_workspace_bytes": (c_size_t, [c_int64, c_int32, ctypes.c_int]),
+    "gs_neighbor_loss_forward": (ctypes.c_int, [P_NG, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "gs_neighbor_loss_backward": (ctypes.c_int, [P_NG, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                                 c_void_p, c_void_p]),
+    "gs_neighbor_reverse_workspace_bytes": (c_size_t, [c_int64, c_int32]),
+    "gs_neighbor_reverse": (ctypes.c_int, [c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
+                                           c_void_p, c_void_p]),
     "gs_timing_select": (ctypes.c_int, [ctypes.c_uint32]),
     "gs_timing_read": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_int64),
                                       ctypes.c_int]),

@@ -48,6 +48,7 @@ SOURCES = {
     "gs_binning.hip": [],
     "gs_tiles.hip": [],
     "gs_render.hip": [],
+    "gs_neighbor.hip": [],
     "gs_api.hip": [],
 }
 COMMON = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall",

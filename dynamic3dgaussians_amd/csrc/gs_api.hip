@@ -13,6 +13,7 @@
 #include <string>
 #include <vector>
 
+#include "../../include/gs_neighbor.h"
 #include "../../include/gsplat_hip.h"
 #include "gs_common.h"
 #include "gs_kernels.h"
@@ -421,6 +422,105 @@ int gs_sort_pairs(int64_t n, uint64_t* keys, uint32_t* vals, int end_bit, void* 
     (void)hipMemcpyAsync(vals, v1, 4 * n, hipMemcpyDeviceToDevice, s);
   }
   return check("sort", 0, s);
+}
+
+// ---- neighbour losses (include/gs_neighbor.h) ----
+
+static int check_graph(const gs_neighbor_graph* g, bool backward, NeighborArgs* a) {
+  if (!g) return fail(-1, "null neighbour graph");
+  if (g->N < 0 || g->K < 0) return fail(-1, "N and K must be >= 0 (got N=%lld K=%d)", (long long)g->N, g->K);
+  if ((double)g->N * g->K >= 2147483647.0) return fail(-1, "N*K must fit in int32 (got N=%lld K=%d)", (long long)g->N, g->K);
+  if (g->N > 0 && (!g->prev_inv_rot || (g->K > 0 && (!g->nbr || !g->weight || !g->dist || !g->prev_offset))))
+    return fail(-1, "neighbour graph arrays are required");
+  if (backward && g->N > 0 && (!g->rev_ptr || (g->K > 0 && !g->rev_pos)))
+    return fail(-1, "the backward needs the reverse CSR (gs_neighbor_reverse)");
+  *a = NeighborArgs{g->N, g->K, nullptr, nullptr, g->nbr, g->weight, g->dist, g->prev_offset, g->prev_inv_rot,
+                    g->rev_ptr, g->rev_pos};
+  return 0;
+}
+
+size_t gs_neighbor_workspace_bytes(int64_t N, int32_t K, int backward) {
+  return NeighborLayout(N < 0 ? 0 : N, K < 0 ? 0 : K, backward != 0).total;
+}
+
+int gs_neighbor_loss_forward(const gs_neighbor_graph* g, const float* fg_pts, const float* fg_rot, float* losses,
+                             void* workspace, gs_stream_t stream) {
+  NeighborArgs a;
+  if (int e = check_graph(g, false, &a)) return e;
+  if (!losses || !workspace) return fail(-1, "losses and workspace are required");
+  if (a.N > 0 && (!fg_pts || !fg_rot)) return fail(-1, "fg_pts and fg_rot are required");
+  a.fg_pts = fg_pts;
+  a.fg_rot = fg_rot;
+  hipStream_t s = (hipStream_t)stream;
+  launch_neighbor_forward(a, losses, workspace, s);
+  return check("neighbour loss forward", 0, s);
+}
+
+int gs_neighbor_loss_backward(const gs_neighbor_graph* g, const float* fg_pts, const float* fg_rot,
+                              const float* dL_dlosses, float* d_fg_pts, float* d_fg_rot, void* workspace,
+                              gs_stream_t stream) {
+  NeighborArgs a;
+  if (int e = check_graph(g, true, &a)) return e;
+  if (a.N == 0) return 0;
+  if (!fg_pts || !fg_rot || !dL_dlosses || !d_fg_pts || !d_fg_rot || !workspace)
+    return fail(-1, "neighbour loss backward: null argument");
+  a.fg_pts = fg_pts;
+  a.fg_rot = fg_rot;
+  hipStream_t s = (hipStream_t)stream;
+  launch_neighbor_backward(a, dL_dlosses, d_fg_pts, d_fg_rot, workspace, s);
+  return check("neighbour loss backward", 0, s);
+}
+
+namespace {
+struct RevLayout {
+  size_t keys, vals, status, sort, total;
+  explicit RevLayout(int64_t NK) {
+    size_t o = 0;
+    keys = o; o = align_up(o + 8 * (size_t)NK, 256);
+    vals = o; o = align_up(o + 4 * (size_t)NK, 256);
+    status = o; o = align_up(o + 4, 256);
+    sort = o; o = align_up(o + SortLayout(NK).total, 256);
+    total = o;
+  }
+};
+}  // namespace
+
+size_t gs_neighbor_reverse_workspace_bytes(int64_t N, int32_t K) {
+  return RevLayout((N < 0 ? 0 : N) * (K < 0 ? 0 : K)).total;
+}
+
+int gs_neighbor_reverse(int64_t N, int32_t K, const int64_t* nbr, int32_t* rev_ptr, int32_t* rev_pair,
+                        int32_t* rev_pos, void* workspace, gs_stream_t stream) {
+  if (N < 0 || K < 0) return fail(-1, "N and K must be >= 0");
+  if ((double)N * K >= 2147483647.0) return fail(-1, "N*K must fit in int32");
+  const int64_t NK = N * K;
+  if (!rev_ptr || !workspace || (NK > 0 && (!nbr || !rev_pos))) return fail(-1, "neighbour reverse: null argument");
+  hipStream_t s = (hipStream_t)stream;
+  const RevLayout L(NK);
+  uint64_t* keys = at<uint64_t>(workspace, L.keys);
+  uint32_t* vals = at<uint32_t>(workspace, L.vals);
+  int* status = at<int>(workspace, L.status);
+  (void)hipMemsetAsync(status, 0, 4, s);
+  launch_neighbor_rev_keys(NK, N, nbr, keys, vals, status, s);
+  if (NK > 1) {
+    const SortLayout sl(NK);
+    void* sc = at<char>(workspace, L.sort);
+    uint64_t* k1 = at<uint64_t>(sc, sl.keys1);
+    uint32_t* v1 = at<uint32_t>(sc, sl.vals1);
+    int end_bit = 1;  // keys <= N (N marks invalid ids)
+    while (end_bit < 63 && ((uint64_t)N >> end_bit)) ++end_bit;
+    if (launch_radix_sort(NK, keys, vals, k1, v1, at<uint32_t>(sc, sl.hist), at<uint32_t>(sc, sl.rowtot),
+                          end_bit, s)) {
+      keys = k1;
+      vals = v1;
+    }
+  }
+  launch_neighbor_rev_ptr(NK, N, keys, vals, rev_ptr, rev_pair, rev_pos, s);
+  int host_status = 0;
+  (void)hipMemcpyAsync(&host_status, status, 4, hipMemcpyDeviceToHost, s);
+  if (int e = check("neighbour reverse", 1, s)) return e;
+  if (host_status) return fail(-1, "neighbor_indices out of range [0, %lld)", (long long)N);
+  return 0;
 }
 
 int gs_test_wave_reduce(int n_comp, const float* in, float* out, gs_stream_t stream) {

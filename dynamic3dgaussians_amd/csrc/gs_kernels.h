@@ -121,4 +121,30 @@ bool launch_render_bwd(const RenderBwdArgs& a, hipStream_t s);
 
 void launch_test_wave_reduce(int n, const float* in, float* out, hipStream_t s);
 
+// Neighbour losses (gs_neighbor.hip, include/gs_neighbor.h).
+struct NeighborArgs {
+  int64_t N;
+  int K;
+  const float* fg_pts;        // N x 3
+  const float* fg_rot;        // N x 4
+  const int64_t* nbr;         // N x K
+  const float* weight;        // N x K
+  const float* dist;          // N x K
+  const float* prev_offset;   // N x K x 3
+  const float* prev_inv_rot;  // N x 4
+  const int32_t* rev_ptr;     // N + 1
+  const int32_t* rev_pos;     // N x K: slot of pair i*K+k in the reverse order
+};
+struct NeighborLayout {
+  size_t qv, Rm, partial, revbuf, selfbuf, total;
+  NeighborLayout(int64_t N, int K, bool backward);
+};
+void launch_neighbor_forward(const NeighborArgs& a, float* losses, void* ws, hipStream_t s);
+void launch_neighbor_backward(const NeighborArgs& a, const float* dL, float* d_pts, float* d_rot, void* ws,
+                              hipStream_t s);
+void launch_neighbor_rev_keys(int64_t NK, int64_t N, const int64_t* nbr, uint64_t* keys, uint32_t* vals,
+                              int* status, hipStream_t s);
+void launch_neighbor_rev_ptr(int64_t NK, int64_t N, const uint64_t* keys, const uint32_t* vals, int32_t* rev_ptr,
+                             int32_t* rev_pair, int32_t* rev_pos, hipStream_t s);
+
 }  // namespace gs

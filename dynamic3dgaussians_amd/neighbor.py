@@ -1,0 +1,142 @@
+"""Local-rigidity / rotation / isometry neighbour losses on the HIP kernels of
+csrc/gs_neighbor.hip (C ABI include/gs_neighbor.h).
+
+Drop-in for the loss block of the reference's per-step loss
+(train.py:253-273; cvpr_dyn.py:302-322):
+
+    rel_rot = quat_mult(fg_rot, variables["prev_inv_rot_fg"])
+    rot = build_rotation(rel_rot)
+    neighbor_pts = fg_pts[variables["neighbor_indices"]]
+    curr_offset = neighbor_pts - fg_pts[:, None]
+    curr_offset_in_prev_coord = (rot.transpose(2, 1)[:, None] @ curr_offset[:, :, :, None]).squeeze(-1)
+    losses['rigid'] = weighted_l2_loss_v2(curr_offset_in_prev_coord, variables["prev_offset"], w)
+    losses['rot'] = weighted_l2_loss_v2(rel_rot[nbr], rel_rot[:, None], w)
+    losses['iso'] = weighted_l2_loss_v1(sqrt(|curr_offset|^2 + 1e-20), variables["neighbor_dist"], w)
+
+becomes
+
+    losses['rigid'], losses['rot'], losses['iso'] = neighbor_losses(fg_pts, fg_rot, variables)
+
+`variables` is the reference's dict (same keys, same tensors).  The reverse
+adjacency the backward needs is built on the GPU the first time a neighbour
+graph is seen and cached in `variables` (the graph is fixed after the first
+timestep, train.py:316-326).  Gradients flow to fg_pts and fg_rot (and from
+there through the caller's own indexing / normalize, as in the reference).
+There is no CPU path: CPU tensors raise.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+_REV_KEY = "_neighbor_reverse_csr"
+
+
+def _ptr(t):
+    return t.data_ptr() if t is not None and t.numel() else None
+
+
+def _stream(dev):
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+def _need(t: torch.Tensor, name: str, dtype, shape) -> torch.Tensor:
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a tensor")
+    if not t.is_cuda:
+        raise _lib.GsplatError(f"the HIP neighbour losses need device tensors ({name} is on the CPU)")
+    if t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype} (got {t.dtype})")
+    if tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name} must have shape {tuple(shape)} (got {tuple(t.shape)})")
+    return t.contiguous()
+
+
+def reverse_csr(neighbor_indices: torch.Tensor):
+    """(rev_ptr [N+1], rev_pair [N*K], rev_pos [N*K]) int32: for each
+    Gaussian, the pairs (i*K + k) that name it as a neighbour, in ascending
+    pair order, and the inverse permutation (pair -> slot)."""
+    nbr = neighbor_indices
+    if not nbr.is_cuda:
+        raise _lib.GsplatError("neighbor_indices must be a device tensor")
+    nbr = nbr.to(torch.int64).contiguous()
+    N, K = nbr.shape
+    L = _lib.load()
+    dev = nbr.device
+    rev_ptr = torch.empty(N + 1, dtype=torch.int32, device=dev)
+    rev_pair = torch.empty(N * K, dtype=torch.int32, device=dev)
+    rev_pos = torch.empty(N * K, dtype=torch.int32, device=dev)
+    ws = torch.empty(L.gs_neighbor_reverse_workspace_bytes(N, K), dtype=torch.uint8, device=dev)
+    _lib.check(L.gs_neighbor_reverse(N, K, _ptr(nbr), rev_ptr.data_ptr(), _ptr(rev_pair), _ptr(rev_pos),
+                                     ws.data_ptr(), _stream(dev)), "neighbor reverse")
+    return rev_ptr, rev_pair, rev_pos
+
+
+class _Graph:
+    """Device arrays of one neighbour graph + the previous timestep's state."""
+
+    def __init__(self, variables: dict, N: int, dev):
+        nbr = variables["neighbor_indices"]
+        if nbr.dim() != 2 or nbr.size(0) != N:
+            raise ValueError(f"neighbor_indices must be [N={N}, K] (got {tuple(nbr.shape)})")
+        K = nbr.size(1)
+        self.N, self.K = N, K
+        self.nbr = _need(nbr, "neighbor_indices", torch.int64, (N, K))
+        self.weight = _need(variables["neighbor_weight"], "neighbor_weight", torch.float32, (N, K))
+        self.dist = _need(variables["neighbor_dist"], "neighbor_dist", torch.float32, (N, K))
+        self.prev_offset = _need(variables["prev_offset"], "prev_offset", torch.float32, (N, K, 3))
+        self.prev_inv_rot = _need(variables["prev_inv_rot_fg"], "prev_inv_rot_fg", torch.float32, (N, 4))
+        key = (self.nbr.data_ptr(), N, K, self.nbr._version)
+        cached = variables.get(_REV_KEY)
+        if cached is None or cached[0] != key:
+            rev_ptr, _, rev_pos = reverse_csr(self.nbr)
+            cached = (key, rev_ptr, rev_pos)
+            variables[_REV_KEY] = cached
+        self.rev_ptr, self.rev_pos = cached[1], cached[2]
+
+    def struct(self) -> _lib.GsNeighborGraph:
+        return _lib.GsNeighborGraph(N=self.N, K=self.K, _pad=0, nbr=_ptr(self.nbr), weight=_ptr(self.weight),
+                                    dist=_ptr(self.dist), prev_offset=_ptr(self.prev_offset),
+                                    prev_inv_rot=_ptr(self.prev_inv_rot), rev_ptr=_ptr(self.rev_ptr),
+                                    rev_pos=_ptr(self.rev_pos))
+
+
+class _NeighborLosses(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, fg_pts, fg_rot, graph: _Graph):
+        L = _lib.load()
+        dev = fg_pts.device
+        pts = _need(fg_pts.detach(), "fg_pts", torch.float32, (graph.N, 3))
+        rot = _need(fg_rot.detach(), "fg_rot", torch.float32, (graph.N, 4))
+        out = torch.empty(3, dtype=torch.float32, device=dev)
+        ws = torch.empty(L.gs_neighbor_workspace_bytes(graph.N, graph.K, 0), dtype=torch.uint8, device=dev)
+        g = graph.struct()
+        _lib.check(L.gs_neighbor_loss_forward(g, _ptr(pts), _ptr(rot), out.data_ptr(), ws.data_ptr(),
+                                              _stream(dev)), "neighbor loss forward")
+        ctx.graph = graph
+        ctx.save_for_backward(pts, rot)
+        return out[0], out[1], out[2]
+
+    @staticmethod
+    def backward(ctx, g_rigid, g_rot, g_iso):
+        pts, rot = ctx.saved_tensors
+        graph = ctx.graph
+        dev = pts.device
+        L = _lib.load()
+        z = torch.zeros((), device=dev)
+        dL = torch.stack([g if g is not None else z for g in (g_rigid, g_rot, g_iso)]).float().contiguous()
+        d_pts = torch.empty_like(pts)
+        d_rot = torch.empty_like(rot)
+        ws = torch.empty(L.gs_neighbor_workspace_bytes(graph.N, graph.K, 1), dtype=torch.uint8, device=dev)
+        _lib.check(L.gs_neighbor_loss_backward(graph.struct(), _ptr(pts), _ptr(rot), dL.data_ptr(),
+                                               _ptr(d_pts), _ptr(d_rot), ws.data_ptr(), _stream(dev)),
+                   "neighbor loss backward")
+        return d_pts, d_rot, None
+
+
+def neighbor_losses(fg_pts: torch.Tensor, fg_rot: torch.Tensor, variables: dict):
+    """(rigid, rot, iso) scalar losses of train.py:259-273, differentiable in
+    fg_pts [N, 3] and fg_rot [N, 4]."""
+    graph = _Graph(variables, fg_pts.size(0), fg_pts.device)
+    return _NeighborLosses.apply(fg_pts, fg_rot, graph)

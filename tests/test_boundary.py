@@ -22,9 +22,12 @@ GOLD = os.path.join(REPO, "tests", "golden", "boundary_conventions.json")
 
 
 def _declared_symbols():
-    txt = open(os.path.join(REPO, "include", "gsplat_hip.h")).read()
-    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    return sorted(set(re.findall(r"\b(gs_[a-z_0-9]+)\s*\(", txt)))
+    names = set()
+    for h in ("gsplat_hip.h", "gs_neighbor.h"):
+        txt = open(os.path.join(REPO, "include", h)).read()
+        txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+        names |= set(re.findall(r"\b(gs_[a-z_0-9]+)\s*\(", txt))
+    return sorted(names)
 
 
 def test_library_exports_every_declared_symbol():
