@@ -40,6 +40,7 @@ sys.path.insert(0, REPO)
 from dynamic3dgaussians_amd import _lib  # noqa: E402
 from dynamic3dgaussians_amd.camera import camera_rig  # noqa: E402
 from dynamic3dgaussians_amd.distributed import GradBucket  # noqa: E402
+from dynamic3dgaussians_amd.optim import FusedAdam  # noqa: E402
 from dynamic3dgaussians_amd.rasterizer import (GaussianRasterizationSettings,  # noqa: E402
                                                GaussianRasterizer)
 from dynamic3dgaussians_amd.scene import make_gaussians  # noqa: E402
@@ -239,14 +240,22 @@ def main():
     # the CPU-baseline / PSNR leg renders the initial scene (independent of the
     # optimizer steps taken by warmup and timing)
     params0 = {k: v.detach().clone() for k, v in params.items()}
-    opt = torch.optim.Adam([
-        {"params": [params["means3D"]], "lr": 1.6e-4},
-        {"params": [params["rgb_colors"]], "lr": 2.5e-3},
-        {"params": [params["unnorm_rotations"]], "lr": 1e-3},
-        {"params": [params["logit_opacities"]], "lr": 0.05},
-        {"params": [params["log_scales"]], "lr": 1e-3},
-    ] + ([{"params": [params["semantic_feature"]], "lr": 1e-3}] if args.features else []),
-        lr=0.0, eps=1e-15, fused=os.environ.get("GS_BENCH_FUSED_ADAM", "0") == "1")
+    # The reference's Adam (train.py:119-135).  Default: FusedAdam, one HIP
+    # launch, bit-identical to torch.optim.Adam (tests/test_optim.py);
+    # GS_BENCH_OPTIM=torch / torch_fused selects torch's own kernels.
+    groups = [
+        {"params": [params["means3D"]], "lr": 1.6e-4, "name": "means3D"},
+        {"params": [params["rgb_colors"]], "lr": 2.5e-3, "name": "rgb_colors"},
+        {"params": [params["unnorm_rotations"]], "lr": 1e-3, "name": "unnorm_rotations"},
+        {"params": [params["logit_opacities"]], "lr": 0.05, "name": "logit_opacities"},
+        {"params": [params["log_scales"]], "lr": 1e-3, "name": "log_scales"},
+    ] + ([{"params": [params["semantic_feature"]], "lr": 1e-3, "name": "semantic_feature"}]
+         if args.features else [])
+    optim_kind = os.environ.get("GS_BENCH_OPTIM", "fused_hip")
+    if optim_kind == "fused_hip":
+        opt = FusedAdam(groups, lr=0.0, eps=1e-15)
+    else:
+        opt = torch.optim.Adam(groups, lr=0.0, eps=1e-15, fused=optim_kind == "torch_fused")
     bucket = GradBucket(list(params.values()))
     g = torch.Generator(device=dev).manual_seed(1 + rank)
     H_, W_ = args.height, args.width
@@ -349,6 +358,7 @@ def main():
         "config": {"workload": f"{args.gaussians // 1000}k Gaussians x {args.cams} cams/rank x "
                                f"{W_}x{H_}, F={args.features} semantic channels, colors_precomp; "
                                "fwd+bwd per camera + grad all-reduce + Adam",
+                   "optimizer": optim_kind,
                    "gaussians": args.gaussians, "cams_per_rank": args.cams, "width": W_,
                    "height": H_, "feature_channels": args.features, "compat": args.compat,
                    "parallelism": f"camera-sharded dp{world}"},

@@ -46,6 +46,24 @@ class GsNeighborGraph(ctypes.Structure):
                 ("prev_inv_rot", c_void_p), ("rev_ptr", c_void_p), ("rev_pos", c_void_p)]
 
 
+class GsAdamTensor(ctypes.Structure):
+    """include/gs_optim.h gs_adam_tensor."""
+    _fields_ = [("param", c_void_p), ("grad", c_void_p), ("exp_avg", c_void_p), ("exp_avg_sq", c_void_p),
+                ("numel", c_int64), ("step_size", c_float), ("bc2_sqrt", c_float)]
+
+
+class GsAdamArgs(ctypes.Structure):
+    """include/gs_optim.h gs_adam_args (GS_ADAM_MAX_TENSORS = 16)."""
+    _fields_ = [("n_tensors", c_int32), ("_pad", c_int32), ("beta1", ctypes.c_double),
+                ("beta2", ctypes.c_double), ("eps", ctypes.c_double), ("t", GsAdamTensor * 16)]
+
+
+class GsDensifyStats(ctypes.Structure):
+    """include/gs_optim.h gs_densify_stats."""
+    _fields_ = [("P", c_int64), ("radii", c_void_p), ("means2D_grad", c_void_p), ("max_radius", c_void_p),
+                ("grad_accum", c_void_p), ("denom", c_void_p)]
+
+
 P_G = ctypes.POINTER(GsGaussians)
 P_NG = ctypes.POINTER(GsNeighborGraph)
 P_C = ctypes.POINTER(GsCamera)
@@ -75,6 +93,8 @@ PROTOTYPES = {
     "gs_sort_pairs": (ctypes.c_int, [c_int64, c_void_p, c_void_p, ctypes.c_int, c_void_p, c_void_p]),
     "gs_test_wave_reduce": (ctypes.c_int, [ctypes.c_int, c_void_p, c_void_p, c_void_p]),
     "gs_timing_enable": (ctypes.c_int, [ctypes.c_int]),
+    # include/gs_optim.h
+    "gs_adam_step": (ctypes.c_int, [ctypes.POINTER(GsAdamArgs), ctypes.POINTER(GsDensifyStats), c_void_p]),
     # include/gs_neighbor.h
     "gs_neighbor_workspace_bytes": (c_size_t, [c_int64, c_int32, ctypes.c_int]),
     "gs_neighbor_loss_forward": (ctypes.c_int, [P_NG, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),

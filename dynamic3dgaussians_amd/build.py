@@ -49,6 +49,7 @@ SOURCES = {
     "gs_tiles.hip": [],
     "gs_render.hip": [],
     "gs_neighbor.hip": [],
+    "gs_optim.hip": ["-ffp-contract=off"],
     "gs_api.hip": [],
 }
 COMMON = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall",

@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "../../include/gs_neighbor.h"
+#include "../../include/gs_optim.h"
 #include "../../include/gsplat_hip.h"
 #include "gs_common.h"
 #include "gs_kernels.h"
@@ -422,6 +423,29 @@ int gs_sort_pairs(int64_t n, uint64_t* keys, uint32_t* vals, int end_bit, void* 
     (void)hipMemcpyAsync(vals, v1, 4 * n, hipMemcpyDeviceToDevice, s);
   }
   return check("sort", 0, s);
+}
+
+// ---- fused Adam + densification statistics (include/gs_optim.h) ----
+
+int gs_adam_step(const gs_adam_args* a, const gs_densify_stats* st, gs_stream_t stream) {
+  if (!a) return fail(-1, "null Adam arguments");
+  if (a->n_tensors < 0 || a->n_tensors > GS_ADAM_MAX_TENSORS)
+    return fail(-1, "n_tensors must be in [0, %d] (got %d)", GS_ADAM_MAX_TENSORS, a->n_tensors);
+  for (int t = 0; t < a->n_tensors; ++t) {
+    const gs_adam_tensor& x = a->t[t];
+    if (x.numel < 0) return fail(-1, "tensor %d: numel < 0", t);
+    if (x.numel > 0 && (!x.param || !x.grad || !x.exp_avg || !x.exp_avg_sq))
+      return fail(-1, "tensor %d: param, grad, exp_avg and exp_avg_sq are required", t);
+    if (!(x.bc2_sqrt > 0.f)) return fail(-1, "tensor %d: bc2_sqrt must be > 0 (step >= 1)", t);
+  }
+  if (st && st->P > 0) {
+    if (!st->radii) return fail(-1, "densify stats: radii are required");
+    if (st->grad_accum && (!st->denom || !st->means2D_grad))
+      return fail(-1, "densify stats: grad_accum needs denom and means2D_grad");
+  }
+  hipStream_t s = (hipStream_t)stream;
+  if (!launch_adam_step(*a, st, s)) return fail(-1, "Adam step: too many blocks");
+  return check("adam step", 0, s);
 }
 
 // ---- neighbour losses (include/gs_neighbor.h) ----

@@ -2,6 +2,8 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+
+#include "../../include/gs_optim.h"
 #include <stdint.h>
 
 namespace gs {
@@ -120,6 +122,9 @@ bool launch_render_fwd(const RenderArgs& a, hipStream_t s);
 bool launch_render_bwd(const RenderBwdArgs& a, hipStream_t s);
 
 void launch_test_wave_reduce(int n, const float* in, float* out, hipStream_t s);
+
+// Fused Adam + densification statistics (gs_optim.hip, include/gs_optim.h).
+bool launch_adam_step(const gs_adam_args& a, const gs_densify_stats* st, hipStream_t s);
 
 // Neighbour losses (gs_neighbor.hip, include/gs_neighbor.h).
 struct NeighborArgs {
