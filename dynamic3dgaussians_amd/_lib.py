@@ -93,6 +93,9 @@ PROTOTYPES = {
     "gs_sort_pairs": (ctypes.c_int, [c_int64, c_void_p, c_void_p, ctypes.c_int, c_void_p, c_void_p]),
     "gs_test_wave_reduce": (ctypes.c_int, [ctypes.c_int, c_void_p, c_void_p, c_void_p]),
     "gs_timing_enable": (ctypes.c_int, [ctypes.c_int]),
+    # include/gs_knn.h
+    "gs_knn_workspace_bytes": (c_size_t, [c_int64]),
+    "gs_knn": (ctypes.c_int, [c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     # include/gs_optim.h
     "gs_adam_step": (ctypes.c_int, [ctypes.POINTER(GsAdamArgs), ctypes.POINTER(GsDensifyStats), c_void_p]),
     # include/gs_neighbor.h

@@ -50,6 +50,7 @@ SOURCES = {
     "gs_render.hip": [],
     "gs_neighbor.hip": [],
     "gs_optim.hip": ["-ffp-contract=off"],
+    "gs_knn.hip": ["-ffp-contract=off"],
     "gs_api.hip": [],
 }
 COMMON = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall",

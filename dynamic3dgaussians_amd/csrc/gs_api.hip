@@ -13,6 +13,7 @@
 #include <string>
 #include <vector>
 
+#include "../../include/gs_knn.h"
 #include "../../include/gs_neighbor.h"
 #include "../../include/gs_optim.h"
 #include "../../include/gsplat_hip.h"
@@ -423,6 +424,22 @@ int gs_sort_pairs(int64_t n, uint64_t* keys, uint32_t* vals, int end_bit, void* 
     (void)hipMemcpyAsync(vals, v1, 4 * n, hipMemcpyDeviceToDevice, s);
   }
   return check("sort", 0, s);
+}
+
+// ---- exact k-nearest neighbours (include/gs_knn.h) ----
+
+size_t gs_knn_workspace_bytes(int64_t N) { return KnnLayout(N < 0 ? 0 : N).total; }
+
+int gs_knn(int64_t N, int32_t K, const float* points, double* sq_dist, int64_t* index, void* workspace,
+           gs_stream_t stream) {
+  if (N < 0) return fail(-1, "N must be >= 0");
+  if (K < 1 || K > GS_KNN_MAX_K) return fail(-1, "K must be in [1, %d] (got %d)", GS_KNN_MAX_K, K);
+  if (N >= (int64_t)1 << 31) return fail(-1, "N must fit in int32");
+  if (N == 0) return 0;
+  if (!points || !sq_dist || !index || !workspace) return fail(-1, "knn: null argument");
+  hipStream_t s = (hipStream_t)stream;
+  if (!launch_knn(N, K, points, sq_dist, index, workspace, s)) return fail(-1, "knn: unsupported K %d", K);
+  return check("knn", 0, s);
 }
 
 // ---- fused Adam + densification statistics (include/gs_optim.h) ----

@@ -126,6 +126,13 @@ void launch_test_wave_reduce(int n, const float* in, float* out, hipStream_t s);
 // Fused Adam + densification statistics (gs_optim.hip, include/gs_optim.h).
 bool launch_adam_step(const gs_adam_args& a, const gs_densify_stats* st, hipStream_t s);
 
+// Exact k-nearest neighbours (gs_knn.hip, include/gs_knn.h).
+struct KnnLayout {
+  size_t bbox, keys, vals, sort, spts, boxes, total;
+  explicit KnnLayout(int64_t N);
+};
+bool launch_knn(int64_t N, int K, const float* pts, double* out_d, int64_t* out_i, void* ws, hipStream_t s);
+
 // Neighbour losses (gs_neighbor.hip, include/gs_neighbor.h).
 struct NeighborArgs {
   int64_t N;

@@ -1,0 +1,273 @@
+// gs_knn.hip -- exact k-nearest neighbours of a point cloud (SURVEY.md 8(f)
+// rank 4): the reference's o3d_knn (Open3D KDTreeFlann, helpers.py:135-146:
+// k + 1 hits, the point itself dropped) used for the initial scales
+// (train.py:95) and the neighbour graph (train.py:316-326), and the vendored
+// simple-knn distCUDA2 (submodules_fsgs/simple-knn/simple_knn.cu:192-228,
+// scene/gaussian_model.py:162) -- both exact 3-/k-NN searches.
+//
+// MI355X form, no tree: Morton-sort the points (library radix sort), cut the
+// sorted order into boxes of 256 points with their bounds, then one workgroup
+// per box of queries visits every box whose bounds can still beat ANY of its
+// queries' current k-th distance, spiralling out from its own box (a tight
+// bound early), loading each visited box once into LDS for all 256 queries.
+// Distances are computed in double from the fp32 coordinates, unfused
+// (-ffp-contract=off), like Open3D's L2 adaptor on the float64 copy the
+// reference hands it; the k best are kept sorted by (distance, index) in
+// registers, so ties resolve to the lower index.
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+
+#include "gs_common.h"
+#include "gs_kernels.h"
+
+namespace gs {
+
+namespace {
+
+constexpr int KB = 256;  // box size = workgroup size
+
+__device__ inline uint32_t spread10(uint32_t x) {
+  x = (x | (x << 16)) & 0x030000FF;
+  x = (x | (x << 8)) & 0x0300F00F;
+  x = (x | (x << 4)) & 0x030C30C3;
+  x = (x | (x << 2)) & 0x09249249;
+  return x;
+}
+
+// bounding box: per-block min/max -> atomics on an ordered-int encoding
+__device__ inline uint32_t ord(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ inline float unord(uint32_t u) { return __uint_as_float((u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u); }
+
+__global__ void __launch_bounds__(256) knn_bbox_kernel(int64_t N, const float* __restrict__ pts,
+                                                       uint32_t* __restrict__ bb) {
+  float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < N; i += (int64_t)gridDim.x * 256)
+    for (int c = 0; c < 3; ++c) {
+      const float v = pts[3 * i + c];
+      mn[c] = fminf(mn[c], v);
+      mx[c] = fmaxf(mx[c], v);
+    }
+  for (int o = 32; o > 0; o >>= 1)
+    for (int c = 0; c < 3; ++c) {
+      mn[c] = fminf(mn[c], __shfl_xor(mn[c], o, 64));
+      mx[c] = fmaxf(mx[c], __shfl_xor(mx[c], o, 64));
+    }
+  // block reduce, then one atomic per block and component
+  __shared__ float s[6][4];
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0)
+    for (int c = 0; c < 3; ++c) {
+      s[c][wave] = mn[c];
+      s[3 + c][wave] = mx[c];
+    }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    const int c = threadIdx.x;
+    atomicMin(&bb[c], ord(fminf(fminf(s[c][0], s[c][1]), fminf(s[c][2], s[c][3]))));
+    atomicMax(&bb[3 + c], ord(fmaxf(fmaxf(s[3 + c][0], s[3 + c][1]), fmaxf(s[3 + c][2], s[3 + c][3]))));
+  }
+}
+
+__global__ void __launch_bounds__(256) knn_morton_kernel(int64_t N, const float* __restrict__ pts,
+                                                         const uint32_t* __restrict__ bb,
+                                                         uint64_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= N) return;
+  uint32_t code = 0;
+  for (int c = 0; c < 3; ++c) {
+    const float lo = unord(bb[c]), hi = unord(bb[3 + c]);
+    const float ext = hi - lo;
+    float q = ext > 0.f ? (pts[3 * i + c] - lo) / ext * 1023.f : 0.f;
+    q = fminf(fmaxf(q, 0.f), 1023.f);
+    code |= spread10((uint32_t)q) << c;
+  }
+  keys[i] = code;
+  vals[i] = (uint32_t)i;
+}
+
+// sorted points (x, y, z, original index as bits) and per-box bounds
+__global__ void __launch_bounds__(KB) knn_boxes_kernel(int64_t N, const float* __restrict__ pts,
+                                                       const uint32_t* __restrict__ order,
+                                                       float4* __restrict__ spts, float4* __restrict__ boxes) {
+  const int64_t i = (int64_t)blockIdx.x * KB + threadIdx.x;
+  float3 p = make_float3(FLT_MAX, FLT_MAX, FLT_MAX), q = make_float3(-FLT_MAX, -FLT_MAX, -FLT_MAX);
+  if (i < N) {
+    const uint32_t o = order[i];
+    const float x = pts[3 * (int64_t)o], y = pts[3 * (int64_t)o + 1], z = pts[3 * (int64_t)o + 2];
+    spts[i] = make_float4(x, y, z, __uint_as_float(o));
+    p = make_float3(x, y, z);
+    q = p;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    p.x = fminf(p.x, __shfl_xor(p.x, o, 64)); p.y = fminf(p.y, __shfl_xor(p.y, o, 64));
+    p.z = fminf(p.z, __shfl_xor(p.z, o, 64));
+    q.x = fmaxf(q.x, __shfl_xor(q.x, o, 64)); q.y = fmaxf(q.y, __shfl_xor(q.y, o, 64));
+    q.z = fmaxf(q.z, __shfl_xor(q.z, o, 64));
+  }
+  __shared__ float3 s[2][KB / 64];
+  if ((threadIdx.x & 63) == 0) {
+    s[0][threadIdx.x >> 6] = p;
+    s[1][threadIdx.x >> 6] = q;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < KB / 64; ++w) {
+      p.x = fminf(p.x, s[0][w].x); p.y = fminf(p.y, s[0][w].y); p.z = fminf(p.z, s[0][w].z);
+      q.x = fmaxf(q.x, s[1][w].x); q.y = fmaxf(q.y, s[1][w].y); q.z = fmaxf(q.z, s[1][w].z);
+    }
+    boxes[2 * blockIdx.x] = make_float4(p.x, p.y, p.z, 0.f);
+    boxes[2 * blockIdx.x + 1] = make_float4(q.x, q.y, q.z, 0.f);
+  }
+}
+
+// squared distance from p to the box (0 inside), in double; a lower bound of
+// every point distance in it
+__device__ inline double box_dist(float4 lo, float4 hi, double px, double py, double pz) {
+  const double dx = px < lo.x ? (double)lo.x - px : (px > hi.x ? px - (double)hi.x : 0.0);
+  const double dy = py < lo.y ? (double)lo.y - py : (py > hi.y ? py - (double)hi.y : 0.0);
+  const double dz = pz < lo.z ? (double)lo.z - pz : (pz > hi.z ? pz - (double)hi.z : 0.0);
+  return dx * dx + dy * dy + dz * dz;
+}
+
+template <int KM>
+__global__ void __launch_bounds__(KB) knn_query_kernel(int64_t N, int K, int nbox, const float4* __restrict__ spts,
+                                                       const float4* __restrict__ boxes,
+                                                       double* __restrict__ out_d, int64_t* __restrict__ out_i) {
+  __shared__ float4 s_p[KB];
+  const int own = blockIdx.x;
+  const int64_t qi = (int64_t)own * KB + threadIdx.x;
+  const bool active = qi < N;
+  double px = 0.0, py = 0.0, pz = 0.0;
+  uint32_t self = 0xFFFFFFFFu;
+  if (active) {
+    const float4 p = spts[qi];
+    px = p.x;
+    py = p.y;
+    pz = p.z;
+    self = __float_as_uint(p.w);
+  }
+  double bd[KM];
+  uint32_t bi[KM];
+#pragma unroll
+  for (int j = 0; j < KM; ++j) {
+    bd[j] = __builtin_inf();
+    bi[j] = 0xFFFFFFFFu;
+  }
+  // k-th best so far (slot K-1; slots >= K stay +inf and are never read out)
+  auto kth = [&]() {
+    double v = bd[0];
+#pragma unroll
+    for (int j = 0; j < KM; ++j)
+      if (j == K - 1) v = bd[j];
+    return v;
+  };
+  for (int step = 0; step < 2 * nbox; ++step) {
+    // spiral: own, own+1, own-1, own+2, ...
+    const int off = (step + 1) >> 1;
+    const int b = (step & 1) ? own + off : own - off;
+    if (b < 0 || b >= nbox) {
+      if (own - off < 0 && own + off >= nbox) break;
+      continue;
+    }
+    const float4 lo = boxes[2 * b], hi = boxes[2 * b + 1];
+    const bool need = active && box_dist(lo, hi, px, py, pz) <= kth();
+    if (!__syncthreads_or(need)) continue;
+    const int64_t j0 = (int64_t)b * KB;
+    const int n = (int)((N - j0) < KB ? (N - j0) : KB);
+    if ((int)threadIdx.x < n) s_p[threadIdx.x] = spts[j0 + threadIdx.x];
+    __syncthreads();
+    if (need) {
+      for (int j = 0; j < n; ++j) {
+        const float4 c = s_p[j];
+        const uint32_t ci = __float_as_uint(c.w);
+        const double dx = (double)c.x - px, dy = (double)c.y - py, dz = (double)c.z - pz;
+        double d = dx * dx + dy * dy + dz * dz;
+        const double kd = kth();
+        if (ci == self || d > kd) continue;
+        // insert (d, ci) into the sorted list by (distance, index)
+        uint32_t id = ci;
+#pragma unroll
+        for (int s = 0; s < KM; ++s) {
+          const bool better = d < bd[s] || (d == bd[s] && id < bi[s]);
+          const double td = bd[s];
+          const uint32_t ti = bi[s];
+          bd[s] = better ? d : td;
+          bi[s] = better ? id : ti;
+          d = better ? td : d;
+          id = better ? ti : id;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (!active) return;
+#pragma unroll
+  for (int j = 0; j < KM; ++j) {
+    if (j < K) {
+      out_d[(int64_t)self * K + j] = bd[j];
+      out_i[(int64_t)self * K + j] = bi[j] == 0xFFFFFFFFu ? -1 : (int64_t)bi[j];
+    }
+  }
+}
+
+inline unsigned blocks_for(int64_t n, int t) { return (unsigned)((n + t - 1) / t); }
+
+}  // namespace
+
+KnnLayout::KnnLayout(int64_t N) {
+  size_t o = 0;
+  bbox = o; o = align_up(o + 32, 256);
+  keys = o; o = align_up(o + 8 * (size_t)N, 256);
+  vals = o; o = align_up(o + 4 * (size_t)N, 256);
+  sort = o; o = align_up(o + SortLayout(N).total, 256);
+  spts = o; o = align_up(o + 16 * (size_t)N, 256);
+  boxes = o; o = align_up(o + 32 * (size_t)((N + KB - 1) / KB + 1), 256);
+  total = o;
+}
+
+bool launch_knn(int64_t N, int K, const float* pts, double* out_d, int64_t* out_i, void* ws, hipStream_t s) {
+  if (N <= 0 || K <= 0) return true;
+  const KnnLayout L(N);
+  char* w = static_cast<char*>(ws);
+  uint32_t* bb = reinterpret_cast<uint32_t*>(w + L.bbox);
+  uint64_t* keys = reinterpret_cast<uint64_t*>(w + L.keys);
+  uint32_t* vals = reinterpret_cast<uint32_t*>(w + L.vals);
+  float4* spts = reinterpret_cast<float4*>(w + L.spts);
+  float4* boxes = reinterpret_cast<float4*>(w + L.boxes);
+  // ordered-int min slots start at all-ones, max slots at zero
+  (void)hipMemsetAsync(bb, 0xFF, 12, s);
+  (void)hipMemsetAsync(bb + 3, 0, 12, s);
+  const unsigned nb = blocks_for(N, 256) < 256 ? blocks_for(N, 256) : 256;
+  hipLaunchKernelGGL(knn_bbox_kernel, dim3(nb), dim3(256), 0, s, N, pts, bb);
+  hipLaunchKernelGGL(knn_morton_kernel, dim3(blocks_for(N, 256)), dim3(256), 0, s, N, pts, bb, keys, vals);
+  if (N > 1) {
+    const SortLayout sl(N);
+    char* sc = w + L.sort;
+    uint64_t* k1 = reinterpret_cast<uint64_t*>(sc + sl.keys1);
+    uint32_t* v1 = reinterpret_cast<uint32_t*>(sc + sl.vals1);
+    if (launch_radix_sort(N, keys, vals, k1, v1, reinterpret_cast<uint32_t*>(sc + sl.hist),
+                          reinterpret_cast<uint32_t*>(sc + sl.rowtot), 30, s))
+      vals = v1;
+  }
+  const int nbox = (int)((N + KB - 1) / KB);
+  hipLaunchKernelGGL(knn_boxes_kernel, dim3(nbox), dim3(KB), 0, s, N, pts, vals, spts, boxes);
+  if (K <= 4)
+    hipLaunchKernelGGL(knn_query_kernel<4>, dim3(nbox), dim3(KB), 0, s, N, K, nbox, spts, boxes, out_d, out_i);
+  else if (K <= 8)
+    hipLaunchKernelGGL(knn_query_kernel<8>, dim3(nbox), dim3(KB), 0, s, N, K, nbox, spts, boxes, out_d, out_i);
+  else if (K <= 16)
+    hipLaunchKernelGGL(knn_query_kernel<16>, dim3(nbox), dim3(KB), 0, s, N, K, nbox, spts, boxes, out_d, out_i);
+  else if (K <= 20)  // the reference's neighbour graph (num_knn = 20)
+    hipLaunchKernelGGL(knn_query_kernel<20>, dim3(nbox), dim3(KB), 0, s, N, K, nbox, spts, boxes, out_d, out_i);
+  else if (K <= 32)
+    hipLaunchKernelGGL(knn_query_kernel<32>, dim3(nbox), dim3(KB), 0, s, N, K, nbox, spts, boxes, out_d, out_i);
+  else
+    return false;
+  return true;
+}
+
+}  // namespace gs

@@ -23,7 +23,7 @@ GOLD = os.path.join(REPO, "tests", "golden", "boundary_conventions.json")
 
 def _declared_symbols():
     names = set()
-    for h in ("gsplat_hip.h", "gs_neighbor.h", "gs_optim.h"):
+    for h in ("gsplat_hip.h", "gs_neighbor.h", "gs_optim.h", "gs_knn.h"):
         txt = open(os.path.join(REPO, "include", h)).read()
         txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
         names |= set(re.findall(r"\b(gs_[a-z_0-9]+)\s*\(", txt))
