@@ -38,7 +38,8 @@ VARIANT_FLAGS = {"": [], "stats": ["-DGS_STATS"],
                  "exp_bwd_nodlf": ["-DGS_EXP_BWD_NO_DLF"], "exp_bwd_nomfma": ["-DGS_EXP_BWD_NO_MFMA"],
                  "exp_occ5": ["-DGS_EXP_FWD_LDS_PAD=18000"], "exp_occ3": ["-DGS_EXP_FWD_LDS_PAD=40000"],
                  "exp_fwd_valu": ["-DGS_EXP_FWD_VALU_FEAT"], "exp_bwd_valu": ["-DGS_EXP_BWD_VALU_FEAT"],
-                 "exp_boxcull": ["-DGS_EXP_BOX_CULL"]}
+                 "exp_boxcull": ["-DGS_EXP_BOX_CULL"],
+                 "exp_fwd_wpe5": ["-DGS_FWD_WPE=5"], "exp_fwd_wpe6": ["-DGS_FWD_WPE=6"]}
 ARCH = os.environ.get("GSPLAT_OFFLOAD_ARCH", "gfx950")
 
 # Per-file flags.  The preprocess kernels are compiled without FMA

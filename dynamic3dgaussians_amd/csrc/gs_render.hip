@@ -137,8 +137,13 @@ __device__ inline bool strip_culled(const RecRegs& q, float sx0, float sx1, floa
 
 // ------------------------------------------------------------------ forward
 
+#ifdef GS_FWD_WPE  // occupancy experiment: request GS_FWD_WPE waves per SIMD
+#define GS_FWD_ATTR __attribute__((amdgpu_waves_per_eu(GS_FWD_WPE, 8)))
+#else
+#define GS_FWD_ATTR
+#endif
 template <int F, int COMPAT>
-__global__ __launch_bounds__(256) void render_fwd_kernel(
+__global__ __launch_bounds__(256) GS_FWD_ATTR void render_fwd_kernel(
     int W, int H, int grid_x, int num_tiles, const uint2* __restrict__ ranges,
     const uint32_t* __restrict__ point_list, const float* __restrict__ rec,
     const float* __restrict__ feats, const float* __restrict__ bg, float* __restrict__ out_color,
