@@ -24,7 +24,7 @@ enum RecField {
   R_OP = 5,                   // opacity
   R_R = 6, R_G = 7, R_B = 8,  // colour (SH-evaluated or precomputed)
   R_DEPTH = 9,                // view-space z
-  R_EX = 10, R_EY = 11,       // half extents of the alpha >= 1/255 region
+  R_EX = 10, R_EY = 11,       // half extents of the alpha >= 1/255 region (box-cull experiment only; 0)
   R_RAD = 12,                 // screen radius (ceil(3 sqrt(lambda_max)))
   R_TQ = 13,                  // cull threshold on a dx^2 + 2b dx dy + c dy^2
 };

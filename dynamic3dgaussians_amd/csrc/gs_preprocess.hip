@@ -123,10 +123,15 @@ __device__ inline void alpha_extent(float ca, float cb, float cc, float op, floa
   const double lmin = 0.5 * (tr - disc), lmax = 0.5 * (tr + disc);
   const double cond = lmin > 0.0 ? lmax / lmin : 1e30;
   if (!(cond < 5.0e5)) { ex = INFINITY; ey = INFINITY; tq = INFINITY; return; }
-  const double tau = 2.0 * log((double)op / (double)thr);
+  // fp32 log: its rounding is far inside the 2 % + 1e-3 inflation below
+  const double tau = 2.0 * (double)logf(op * 255.0f);
   const double taup = tau * (1.02 + 32.0 * 6.0e-8 * cond) + 1e-3;
+#ifdef GS_EXP_BOX_CULL  // the extents are only read by the box-cull experiment
   ex = (float)(sqrt(taup * c / det) + 0.01);
   ey = (float)(sqrt(taup * a / det) + 0.01);
+#else
+  ex = ey = 0.0f;
+#endif
   tq = (float)(taup * 1.0001 + 1e-4);
 }
 
