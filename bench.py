@@ -274,7 +274,9 @@ def main():
                 rv["opacities"], rv["scales"], rv["rotations"], 1.0, torch.Tensor([]),
                 s.viewmatrix, s.projmatrix, s.c_x, s.c_y, s.tanfovx, s.tanfovy, H_, W_,
                 torch.Tensor([]), 0, s.campos, False, False, compat=args.compat)
-            inst.append((out[0], int((out[5] > 0).sum().item())))
+            # list instances actually binned (the byte model's L) and the
+            # reference's num_rendered
+            inst.append((_C.binned_instances(out[8], H_, W_), int((out[5] > 0).sum().item()), out[0]))
     del out
 
     def step():
@@ -337,7 +339,7 @@ def main():
     value = mpix_total / (ms_per_step / 1e3)
 
     # roofline of the dominant stage (live HIP-event durations over the timed region)
-    per_cam_bytes = [stage_bytes(L, Pv, args.gaussians, W_, H_, args.features) for L, Pv in inst]
+    per_cam_bytes = [stage_bytes(L, Pv, args.gaussians, W_, H_, args.features) for L, Pv, _ in inst]
     launches = stages[dom][1]
     alg_bytes_total = sum(b[dom] for b in per_cam_bytes) * args.steps
     avg_ms = stages[dom][0] / max(launches, 1)
@@ -364,7 +366,8 @@ def main():
                    "parallelism": f"camera-sharded dp{world}"},
         "roofline": roofline,
         "stages_ms_per_step": {k: round(v, 4) for k, v in stage_ms.items()},
-        "instances_per_cam": int(np.mean([L for L, _ in inst])),
+        "instances_per_cam": int(np.mean([L for L, _, _ in inst])),
+        "num_rendered_per_cam": int(np.mean([R for _, _, R in inst])),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cb, psnr = cpu_baseline(args, params0, label, my_cams[0], settings[0], dev)

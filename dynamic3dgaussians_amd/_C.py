@@ -160,14 +160,18 @@ def rasterize_gaussians(background, means3D, colors, semantic_feature, opacity, 
     img = torch.empty(L_.gs_image_buffer_bytes(W, H), **u8)
     stream = _stream(dev)
     L = ctypes.c_int64(0)
+    NI = ctypes.c_int64(0)
     check(L_.gs_forward_plan(ctypes.byref(g), ctypes.byref(cam), int(bool(prefiltered)),
                              int(bool(debug)), cm, geom.data_ptr(), img.data_ptr(), radii.data_ptr(),
-                             ctypes.byref(L),
+                             ctypes.byref(L), ctypes.byref(NI),
                              stream), "rasterize_gaussians (preprocess)")
+    # num_rendered is the reference's count (returned, like the reference);
+    # the binned tile lists hold num_instances <= num_rendered entries
     num_rendered = int(L.value)
-    binning = torch.empty(L_.gs_binning_buffer_bytes(num_rendered), **u8)
+    num_instances = int(NI.value)
+    binning = torch.empty(L_.gs_binning_buffer_bytes(num_instances), **u8)
     check(L_.gs_forward_render(ctypes.byref(g), ctypes.byref(cam), int(bool(debug)), cm,
-                               geom.data_ptr(), binning.data_ptr(), img.data_ptr(), num_rendered,
+                               geom.data_ptr(), binning.data_ptr(), img.data_ptr(), num_instances,
                                radii.data_ptr(), out_color.data_ptr(),
                                out_feature.data_ptr() if inp.F else None, out_depth.data_ptr(),
                                out_alpha.data_ptr(), stream), "rasterize_gaussians (render)")
@@ -246,6 +250,20 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, semantic_fe
     dsem = out["dsem"][:, :inp.F_user] if inp.F_user != inp.F else out["dsem"]
     return (out["dmeans2D"], out["dcolors"], dsem, out["dopacity"], out["dmeans3D"],
             out["dcov3D"], out["dsh"], out["dscales"], out["drot"])
+
+
+def binned_instances(imageBuffer, image_height, image_width) -> int:
+    """Length of the tile lists a forward binned (num_instances <= the
+    returned num_rendered): read from the image buffer's tile ranges.  An
+    introspection helper (byte models, tests); synchronises the stream."""
+    L_ = _lib.load()
+    W, H = int(image_width), int(image_height)
+    tiles = ((W + 15) // 16) * ((H + 15) // 16)
+    rg = torch.empty(max(tiles, 1), 2, dtype=torch.int32, device=imageBuffer.device)
+    check(L_.gs_debug_export(0, W, H, None, None, imageBuffer.data_ptr(), 0, None, None, None, None, None,
+                             None, rg.data_ptr(), None, _stream(imageBuffer.device)), "binned_instances")
+    r = rg[:tiles].cpu().numpy().view("uint32")
+    return int(r[:, 1].max()) if tiles else 0
 
 
 def mark_visible(means3D, viewmatrix, projmatrix):

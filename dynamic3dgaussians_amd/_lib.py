@@ -16,7 +16,7 @@ _lock = threading.Lock()
 _lib = None
 
 c_void_p = ctypes.c_void_p
-ABI_VERSION = 3  # include/gsplat_hip.h GS_ABI_VERSION
+ABI_VERSION = 4  # include/gsplat_hip.h GS_ABI_VERSION
 c_int32, c_int64, c_float, c_size_t = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_size_t
 
 GS_COMPAT = {"reference": 0, "fixed": 1}
@@ -77,7 +77,8 @@ PROTOTYPES = {
     "gs_image_buffer_bytes": (c_size_t, [c_int32, c_int32]),
     "gs_backward_scratch_bytes": (c_size_t, [c_int64, c_int32]),
     "gs_forward_plan": (ctypes.c_int, [P_G, P_C, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void_p,
-                                       c_void_p, c_void_p, ctypes.POINTER(c_int64), c_void_p]),
+                                       c_void_p, c_void_p, ctypes.POINTER(c_int64), ctypes.POINTER(c_int64),
+                                       c_void_p]),
     "gs_forward_render": (ctypes.c_int, [P_G, P_C, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p,
                                          c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
                                          c_void_p, c_void_p]),

@@ -142,9 +142,11 @@ TileArgs tile_args(int P, int W, int H, void* geom, void* image) {
   t.grid_x = (W + TILE - 1) / TILE; t.grid_y = (H + TILE - 1) / TILE;
   t.num_tiles = (int)il.tiles;
   t.rect = at<uint16_t>(geom, gl.rect);
+  t.tiles = at<uint32_t>(geom, gl.tiles);
   t.rec = at<float>(geom, gl.rec);
   t.thist = at<uint32_t>(image, il.thist);
   t.ttotal = at<uint32_t>(image, il.ttotal);
+  t.bsum = at<uint32_t>(image, il.bsum);
   t.meta = at<uint32_t>(image, il.meta);
   t.ranges = at<uint2>(image, il.ranges);
   return t;
@@ -194,10 +196,12 @@ size_t gs_backward_scratch_bytes(int64_t P, int32_t F) {
 }
 
 int gs_forward_plan(const gs_gaussians* g, const gs_camera* cam, int prefiltered, int debug, int compat,
-                    void* geom, void* image, int32_t* radii, int64_t* num_rendered, gs_stream_t stream) {
+                    void* geom, void* image, int32_t* radii, int64_t* num_rendered, int64_t* num_instances,
+                    gs_stream_t stream) {
   if (int e = check_gaussians(g, cam, true)) return e;
   if (!num_rendered) return fail(-1, "num_rendered is null");
   *num_rendered = 0;
+  if (num_instances) *num_instances = 0;
   g_plan = PlanInfo{};
   const int P = g->P;
   if (P == 0) return 0;
@@ -235,8 +239,9 @@ int gs_forward_plan(const gs_gaussians* g, const gs_camera* cam, int prefiltered
     launch_tile_plan(ta, prefiltered, s);
   }
   if (int e = check("tile plan", debug, s)) return e;
-  // The one host read of the forward (CR/rasterizer_impl.cu:287): the total
-  // instance count sizes the binning buffer; the rest of the header rides along.
+  // The one host read of the forward (CR/rasterizer_impl.cu:287): the list
+  // instance count sizes the binning buffer; the reference's count and the
+  // rest of the header ride along.
   uint32_t host[4] = {0, 0, 0, 0};
   hipError_t he = hipMemcpyAsync(host, ta.meta, sizeof(host), hipMemcpyDeviceToHost, s);
   if (he == hipSuccess) he = hipStreamSynchronize(s);
@@ -244,7 +249,8 @@ int gs_forward_plan(const gs_gaussians* g, const gs_camera* cam, int prefiltered
   if (prefiltered && (host[M_STATUS] & 1u))
     return fail(-2, "Point is filtered although prefiltered is set. This shouldn't happen!");
   if (host[M_STATUS] & 2u) return fail(-1, "more than 2^32 tile instances");
-  *num_rendered = host[M_L];
+  *num_rendered = host[M_LREF];
+  if (num_instances) *num_instances = host[M_L];
   g_plan.image = image;
   g_plan.L = host[M_L];
   g_plan.max_len = host[M_MAXN];
@@ -309,7 +315,11 @@ int gs_backward(const gs_gaussians* g, const gs_camera* cam, const int32_t* radi
   if (int e = check_gaussians(g, cam, false)) return e;
   const int P = g->P;
   if (P == 0) return 0;
-  if (!geom || !image || !scratch || !radii || (L > 0 && !binning)) return fail(-1, "state buffers are required");
+  // L (num_rendered) is not needed: the tile lists sit at the start of the
+  // binning buffer and the ranges say how long they are (an empty binning
+  // buffer means every list is empty)
+  (void)L;
+  if (!geom || !image || !scratch || !radii) return fail(-1, "state buffers are required");
   if (!alphas) return fail(-1, "the forward's alpha image is required");
   if (!dL_dmeans2D || !dL_dcolors || !dL_dopacity || !dL_dmeans3D || !dL_dcov3D || !dL_dscales ||
       !dL_drotations || (g->F > 0 && !dL_dsemantic) || (g->M > 0 && !dL_dsh))
@@ -326,7 +336,7 @@ int gs_backward(const gs_gaussians* g, const gs_camera* cam, const int32_t* radi
   RenderBwdArgs ra{};
   ra.W = W; ra.H = H; ra.grid_x = gx; ra.num_tiles = gx * gy; ra.F = g->F; ra.compat = compat;
   ra.ranges = at<uint2>(image, il.ranges);
-  ra.point_list = L > 0 ? at<uint32_t>(binning, bl.plist) : nullptr;
+  ra.point_list = binning ? at<uint32_t>(binning, bl.plist) : nullptr;
   ra.rec = at<float>(geom, gl.rec);
   ra.feats = g->semantic_feature;
   ra.bg = cam->background;

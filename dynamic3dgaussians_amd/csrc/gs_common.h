@@ -84,12 +84,12 @@ struct GeomLayout {
 // Binning buffer (per tile/Gaussian instance): the (depth bits, id) keys in
 // tile-bucket order and the per-tile sorted id list the blend kernels read.
 struct BinLayout {
-  size_t keys, keys2, plist, total;
+  size_t plist, keys, keys2, total;
   __host__ __device__ BinLayout(int64_t L) {
     size_t o = 0;
+    plist = o; o = align_up(o + sizeof(uint32_t) * L, 256);  // first: located without L
     keys = o;  o = align_up(o + sizeof(uint64_t) * L, 256);
     keys2 = o; o = align_up(o + sizeof(uint64_t) * L, 256);  // radix twin of long tiles
-    plist = o; o = align_up(o + sizeof(uint32_t) * L, 256);
     total = o;
   }
 };
@@ -111,9 +111,11 @@ struct SortLayout {
 // Image buffer (per pixel / per tile), also the binning plan: per-block tile
 // histograms (turned into per-block offsets), tile totals and a 4-word
 // header {L, max tile length, -, status}.
-enum ImgMeta { M_L = 0, M_MAXN = 1, M_RSVD = 2, M_STATUS = 3 };
+// header: M_L = list instances (after the exact tile test), M_LREF = the
+// reference's num_rendered (bounding-rect instances), longest tile, status
+enum ImgMeta { M_L = 0, M_MAXN = 1, M_LREF = 2, M_STATUS = 3 };
 struct ImgLayout {
-  size_t ranges, n_contrib, thist, ttotal, meta, total;
+  size_t ranges, n_contrib, thist, ttotal, bsum, meta, total;
   int64_t tiles;
   __host__ __device__ ImgLayout(int W, int H) {
     tiles = (int64_t)((W + TILE - 1) / TILE) * ((H + TILE - 1) / TILE);
@@ -123,12 +125,34 @@ struct ImgLayout {
     n_contrib = o; o = align_up(o + sizeof(uint32_t) * (int64_t)W * H, 256);
     thist = o;     o = align_up(o + sizeof(uint32_t) * TB_BLOCKS * t, 256);
     ttotal = o;    o = align_up(o + sizeof(uint32_t) * t, 256);
+    bsum = o;      o = align_up(o + sizeof(uint32_t) * TB_BLOCKS, 256);  // per-block rect instances
     meta = o;      o = align_up(o + sizeof(uint32_t) * 4, 256);
     total = o;
   }
 };
 
 // ---------------------------------------------------------------- device math
+
+// Can a Gaussian (mean (mx, my), conic (a, b, c), threshold tq on the
+// quadratic form, see preprocess alpha_extent) reach alpha >= 1/255 at any
+// pixel centre of the rectangle [sx0, sx1] x [sy0, sy1]?  The minimum of the
+// form over the rectangle (0 when the mean is inside, else the least of the
+// four clamped edge minima) against tq, which carries a margin over fp32
+// rounding: exact in effect -- a culled Gaussian is one every pixel of the
+// rectangle would skip in the reference's loop.  Shared by the binning (tile
+// rectangles) and the blend kernels (strips), so their decisions agree.
+__device__ inline bool rect_culled(float mx, float my, float a, float b, float c, float tq, float sx0,
+                                   float sx1, float sy0, float sy1) {
+  const float xlo = mx - sx1, xhi = mx - sx0;  // offsets mean - pixel
+  const float ylo = my - sy1, yhi = my - sy0;
+  if (xlo <= 0.f && xhi >= 0.f && ylo <= 0.f && yhi >= 0.f) return !(tq >= 0.f);
+  auto qf = [&](float x, float y) { return fmaf(a * x, x, fmaf(c * y, y, 2.f * b * x * y)); };
+  const float ra = __builtin_amdgcn_rcpf(a), rc = __builtin_amdgcn_rcpf(c);
+  const float ty0 = fminf(fmaxf(-b * xlo * rc, ylo), yhi), ty1 = fminf(fmaxf(-b * xhi * rc, ylo), yhi);
+  const float tx0 = fminf(fmaxf(-b * ylo * ra, xlo), xhi), tx1 = fminf(fmaxf(-b * yhi * ra, xlo), xhi);
+  const float m = fminf(fminf(qf(xlo, ty0), qf(xhi, ty1)), fminf(qf(tx0, ylo), qf(tx1, yhi)));
+  return m > tq;  // NaN keeps the Gaussian
+}
 
 // XCD-aware block -> work-item remap (bijective for any n).  Consecutive
 // work items land on the same XCD (shared L2) instead of being dealt

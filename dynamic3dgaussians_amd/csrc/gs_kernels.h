@@ -26,7 +26,7 @@ struct PreprocessArgs {
   float* cov3D;
   uint8_t* clamped;
   uint32_t* tiles;
-  uint16_t* rect;  // P x 4: tile rect [x0, x1) x [y0, y1) (empty when culled)
+  uint16_t* rect;  // P x 4: binning tile rect [x0, x1) x [y0, y1) (empty when culled)
   int* status;
 };
 
@@ -101,10 +101,12 @@ int launch_radix_sort(int64_t n, uint64_t* keys0, uint32_t* vals0, uint64_t* key
 // Tile binning (gs_tiles.hip).
 struct TileArgs {
   int P, W, H, grid_x, grid_y, num_tiles;
-  const uint16_t* rect;  // P x 4
+  const uint16_t* rect;  // P x 4 (binning rect)
+  const uint32_t* tiles; // P: the reference's tiles_touched
   const float* rec;      // P x REC (depth)
   uint32_t* thist;       // TB_BLOCKS x num_tiles
   uint32_t* ttotal;      // num_tiles
+  uint32_t* bsum;        // TB_BLOCKS: bounding-rect instances per block (the reference's count)
   uint32_t* meta;        // 4
   uint2* ranges;         // num_tiles
   uint64_t* keys;        // L

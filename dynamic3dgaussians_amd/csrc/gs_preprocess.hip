@@ -126,12 +126,8 @@ __device__ inline void alpha_extent(float ca, float cb, float cc, float op, floa
   // fp32 log: its rounding is far inside the 2 % + 1e-3 inflation below
   const double tau = 2.0 * (double)logf(op * 255.0f);
   const double taup = tau * (1.02 + 32.0 * 6.0e-8 * cond) + 1e-3;
-#ifdef GS_EXP_BOX_CULL  // the extents are only read by the box-cull experiment
   ex = (float)(sqrt(taup * c / det) + 0.01);
   ey = (float)(sqrt(taup * a / det) + 0.01);
-#else
-  ex = ey = 0.0f;
-#endif
   tq = (float)(taup * 1.0001 + 1e-4);
 }
 
@@ -241,9 +237,19 @@ __global__ __launch_bounds__(256) void preprocess_fwd_kernel(PreprocessArgs a) {
   rec[2] = make_float4(rgb[2], pv.z, ex, ey);
   rec[3] = make_float4((float)rad, tq, 0.f, 0.f);
   a.radii[g] = (int)rad;
-  a.tiles[g] = (uint32_t)((rmax.y - rmin.y) * (rmax.x - rmin.x));
+  a.tiles[g] = (uint32_t)((rmax.y - rmin.y) * (rmax.x - rmin.x));  // the reference's tiles_touched
+  // The binning rect: the reference's rect cut down to the tiles whose pixel
+  // centres the alpha >= 1/255 ellipse's bounding box (half extents ex, ey,
+  // margins included) reaches -- the other instances blend at no pixel.
+  // +inf extents keep the reference rect; -inf (never blends) empties it.
+  const float fx0 = fminf(fmaxf(ceilf((px - ex - (TILE - 1)) / TILE), (float)rmin.x), (float)rmax.x);
+  const float fx1 = fminf(fmaxf(floorf((px + ex) / TILE) + 1.f, (float)rmin.x), (float)rmax.x);
+  const float fy0 = fminf(fmaxf(ceilf((py - ey - (TILE - 1)) / TILE), (float)rmin.y), (float)rmax.y);
+  const float fy1 = fminf(fmaxf(floorf((py + ey) / TILE) + 1.f, (float)rmin.y), (float)rmax.y);
+  const int bx0 = (int)fx0, by0 = (int)fy0;
+  const int bx1 = max((int)fx1, bx0), by1 = max((int)fy1, by0);
   reinterpret_cast<ushort4*>(a.rect)[g] =
-      make_ushort4((uint16_t)rmin.x, (uint16_t)rmin.y, (uint16_t)rmax.x, (uint16_t)rmax.y);
+      make_ushort4((uint16_t)bx0, (uint16_t)by0, (uint16_t)bx1, (uint16_t)by1);
 }
 
 void launch_preprocess_fwd(const PreprocessArgs& a, hipStream_t s) {

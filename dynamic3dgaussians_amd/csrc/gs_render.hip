@@ -113,26 +113,14 @@ __device__ inline float gauss_power(float dx, float dy, const float4& h) {
 }
 
 // Can the Gaussian reach alpha >= 1/255 at any pixel centre of the strip
-// [sx0, sx1] x [sy0, sy1]?  The minimum of the quadratic form over the strip
-// rectangle (0 when the mean is inside, else the least of the four clamped
-// edge minima) against the record's inflated threshold tq (preprocess:
-// alpha_extent).  Exact up to that margin, so it culls the Gaussians whose
-// bounding box touches the strip but whose ellipse does not; a culled
-// Gaussian is one every pixel of the strip would skip in the reference loop.
+// [sx0, sx1] x [sy0, sy1]?  rect_culled (gs_common.h) on the record's mean,
+// conic and threshold tq: exact up to tq's margin, so it culls the Gaussians
+// whose bounding box touches the strip but whose ellipse does not.
 __device__ inline bool strip_culled(const RecRegs& q, float sx0, float sx1, float sy0, float sy1) {
 #ifdef GS_EXP_BOX_CULL
   return q.q0.x + q.q2.z < sx0 || q.q0.x - q.q2.z > sx1 || q.q0.y + q.q2.w < sy0 || q.q0.y - q.q2.w > sy1;
 #endif
-  const float a = q.q0.z, b = q.q0.w, c = q.q1.x, tq = q.q3.y;
-  const float xlo = q.q0.x - sx1, xhi = q.q0.x - sx0;  // offsets mean - pixel
-  const float ylo = q.q0.y - sy1, yhi = q.q0.y - sy0;
-  if (xlo <= 0.f && xhi >= 0.f && ylo <= 0.f && yhi >= 0.f) return !(tq >= 0.f);
-  auto qf = [&](float x, float y) { return fmaf(a * x, x, fmaf(c * y, y, 2.f * b * x * y)); };
-  const float ra = fast_rcp(a), rc = fast_rcp(c);
-  const float ty0 = fminf(fmaxf(-b * xlo * rc, ylo), yhi), ty1 = fminf(fmaxf(-b * xhi * rc, ylo), yhi);
-  const float tx0 = fminf(fmaxf(-b * ylo * ra, xlo), xhi), tx1 = fminf(fmaxf(-b * yhi * ra, xlo), xhi);
-  const float m = fminf(fminf(qf(xlo, ty0), qf(xhi, ty1)), fminf(qf(tx0, ylo), qf(tx1, yhi)));
-  return m > tq;  // NaN keeps the Gaussian
+  return rect_culled(q.q0.x, q.q0.y, q.q0.z, q.q0.w, q.q1.x, q.q3.y, sx0, sx1, sy0, sy1);
 }
 
 // ------------------------------------------------------------------ forward

@@ -36,9 +36,15 @@ namespace gs {
 // wave (a full-screen Gaussian must not serialize its wave for 2,500 tiles).
 constexpr int LANE_TILES = 16;
 
+// A Gaussian's instances are the tiles of its binning rect (preprocess: the
+// reference's getRect cut to the bounding box of the alpha >= 1/255
+// ellipse, so the dropped instances are ones no pixel of their tile blends).
+// The reference's tiles_touched (its num_rendered) is summed per block
+// alongside.
 template <bool WRITE>
 __global__ __launch_bounds__(TB_THREADS) void tile_hist_kernel(TileArgs a, int t0, int nt) {
   extern __shared__ uint32_t s_bin[];  // nt counters (hist) or cursors (bucket)
+  __shared__ uint32_t s_rect[TB_THREADS / 64];
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   for (int i = tid; i < nt; i += TB_THREADS)
     s_bin[i] = WRITE ? a.ranges[t0 + i].x + a.thist[(size_t)(t0 + i) * TB_BLOCKS + b] : 0u;
@@ -46,6 +52,7 @@ __global__ __launch_bounds__(TB_THREADS) void tile_hist_kernel(TileArgs a, int t
   const int per = (a.P + TB_BLOCKS - 1) / TB_BLOCKS;
   const int g0 = b * per, g1 = min(a.P, g0 + per);
   const int gx = a.grid_x;
+  uint32_t rect_n = 0;
   for (int base = g0; base < g1; base += TB_THREADS) {
     const int g = base + tid;
     int x0 = 0, y0 = 0, w = 0, n = 0;
@@ -58,6 +65,7 @@ __global__ __launch_bounds__(TB_THREADS) void tile_hist_kernel(TileArgs a, int t
       n = w * ((int)r.w - (int)r.y);
       if (WRITE && n > 0)
         key = ((uint64_t)__float_as_uint(a.rec[(size_t)REC * g + R_DEPTH]) << 32) | (uint32_t)g;
+      if (!WRITE) rect_n += a.tiles[g];
     }
     auto emit = [&](int x, int y, uint64_t k) {
       const uint32_t u = (uint32_t)(y * gx + x - t0);
@@ -82,8 +90,18 @@ __global__ __launch_bounds__(TB_THREADS) void tile_hist_kernel(TileArgs a, int t
     }
   }
   if (!WRITE) {
+    // the reference's num_rendered: bounding-rect instances of this block
+    // (counted once, in the first tile pass)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) rect_n += __shfl_xor(rect_n, o, 64);
+    if (lane == 0) s_rect[tid >> 6] = rect_n;
     __syncthreads();
     for (int i = tid; i < nt; i += TB_THREADS) a.thist[(size_t)(t0 + i) * TB_BLOCKS + b] = s_bin[i];
+    if (tid == 0 && t0 == 0) {
+      uint32_t sum = 0;
+      for (int w2 = 0; w2 < TB_THREADS / 64; ++w2) sum += s_rect[w2];
+      a.bsum[b] = sum;
+    }
   }
 }
 
@@ -118,6 +136,7 @@ __global__ __launch_bounds__(TB_BLOCKS) void tile_rowscan_kernel(uint32_t* __res
 // One workgroup: exclusive scan of the tile totals into ranges, and the header.
 constexpr int OFF_T = 1024;
 __global__ __launch_bounds__(OFF_T) void tile_offsets_kernel(const uint32_t* __restrict__ ttotal, int T,
+                                                             const uint32_t* __restrict__ bsum,
                                                              uint2* __restrict__ ranges,
                                                              uint32_t* __restrict__ meta, int prefiltered) {
   __shared__ unsigned long long s_sum[OFF_T / 64];
@@ -159,10 +178,13 @@ __global__ __launch_bounds__(OFF_T) void tile_offsets_kernel(const uint32_t* __r
   }
   __syncthreads();
   if (tid == 0) {
-    const uint32_t ovf = total > 0xFFFFFFFFull ? 2u : 0u;  // ranges are 32-bit, as in the reference
+    unsigned long long lref = 0;
+    for (int bb = 0; bb < TB_BLOCKS; ++bb) lref += bsum[bb];
+    // ranges are 32-bit, as in the reference
+    const uint32_t ovf = (total > 0xFFFFFFFFull || lref > 0xFFFFFFFFull) ? 2u : 0u;
     meta[M_L] = (uint32_t)total;
     meta[M_MAXN] = s_max;
-    meta[M_RSVD] = 0;
+    meta[M_LREF] = (uint32_t)lref;
     meta[M_STATUS] = prefiltered ? (meta[M_STATUS] | ovf) : ovf;
   }
 }
@@ -329,7 +351,7 @@ void launch_tile_plan(const TileArgs& a, int prefiltered, hipStream_t s) {
                        t0, nt);
   }
   hipLaunchKernelGGL(tile_rowscan_kernel, dim3(T), dim3(TB_BLOCKS), 0, s, a.thist, a.ttotal);
-  hipLaunchKernelGGL(tile_offsets_kernel, dim3(1), dim3(OFF_T), 0, s, a.ttotal, T, a.ranges, a.meta,
+  hipLaunchKernelGGL(tile_offsets_kernel, dim3(1), dim3(OFF_T), 0, s, a.ttotal, T, a.bsum, a.ranges, a.meta,
                      prefiltered);
 }
 

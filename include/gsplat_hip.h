@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 3
+#define GS_ABI_VERSION 4
 
 /* compat modes: numerics of the as-shipped reference vs corrected ones */
 #define GS_COMPAT_REFERENCE 0
@@ -87,17 +87,24 @@ const char *gs_last_error(void);
  * ::fromChunk + required<>, CR/rasterizer_impl.cu:155-194,
  * CR/rasterizer_impl.h:67-73). */
 size_t gs_geom_buffer_bytes(int64_t P);
-size_t gs_binning_buffer_bytes(int64_t num_rendered);
+size_t gs_binning_buffer_bytes(int64_t num_instances);
 size_t gs_image_buffer_bytes(int32_t W, int32_t H);
 size_t gs_backward_scratch_bytes(int64_t P, int32_t F);
 
 /* Forward, phase 1 -- replaces CR/rasterizer_impl.cu:198-287 (preprocess,
- * inclusive scan of tiles_touched, D2H of num_rendered).  Writes radii[P],
- * *num_rendered and the binning plan (per-tile counts and ranges) into the
- * image buffer, which must be the one later passed to gs_forward_render. */
+ * inclusive scan of tiles_touched, D2H of num_rendered).  Writes radii[P]
+ * and the binning plan (per-tile counts and ranges) into the image buffer,
+ * which must be the one later passed to gs_forward_render.
+ * *num_rendered = the reference's count (sum of the Gaussians' bounding-rect
+ * tiles, tiles_touched); *num_instances (may be NULL) = the tile-list length
+ * actually binned: the bounding-rect tiles that the Gaussian's alpha >= 1/255
+ * ellipse reaches (an exact test -- a dropped instance is one the reference's
+ * blend loop skips at every pixel of the tile).  Size the binning buffer and
+ * call gs_forward_render / gs_debug_export with num_instances. */
 int gs_forward_plan(const gs_gaussians *g, const gs_camera *cam, int prefiltered,
                     int debug, int compat, void *geom_buffer, void *image_buffer,
-                    int32_t *radii, int64_t *num_rendered, gs_stream_t stream);
+                    int32_t *radii, int64_t *num_rendered, int64_t *num_instances,
+                    gs_stream_t stream);
 
 /* Forward, phase 2 -- replaces CR/rasterizer_impl.cu:289-345 (duplicateWithKeys,
  * radix sort, identifyTileRanges, render): instances are bucketed by tile and
@@ -108,7 +115,7 @@ int gs_forward_plan(const gs_gaussians *g, const gs_camera *cam, int prefiltered
  * in GS_COMPAT_FIXED mode it receives 1 - T_final. */
 int gs_forward_render(const gs_gaussians *g, const gs_camera *cam, int debug,
                       int compat, void *geom_buffer, void *binning_buffer,
-                      void *image_buffer, int64_t num_rendered, const int32_t *radii,
+                      void *image_buffer, int64_t num_instances, const int32_t *radii,
                       float *out_color, float *out_feature, float *out_depth,
                       float *out_alpha, gs_stream_t stream);
 
@@ -123,7 +130,7 @@ int gs_forward_render(const gs_gaussians *g, const gs_camera *cam, int debug,
 int gs_backward(const gs_gaussians *g, const gs_camera *cam, const int32_t *radii,
                 int debug, int compat, const void *geom_buffer,
                 const void *binning_buffer, const void *image_buffer,
-                int64_t num_rendered, const float *alphas,
+                int64_t num_rendered, const float *alphas,  /* num_rendered: either count; unused */
                 const float *dL_dout_color, const float *dL_dout_feature,
                 const float *dL_dout_depth, const float *dL_dout_alpha,
                 void *scratch, float *dL_dmeans2D, float *dL_dcolors,
@@ -166,7 +173,7 @@ int gs_timing_read(double *ms, int64_t *count, int n_stages);
  * Any output pointer may be NULL. */
 int gs_debug_export(int64_t P, int32_t W, int32_t H, const void *geom_buffer,
                     const void *binning_buffer, const void *image_buffer,
-                    int64_t num_rendered, float *means2D, float *depths,
+                    int64_t num_instances, float *means2D, float *depths,
                     float *conic_opacity, float *rgb, uint32_t *tiles_touched,
                     uint32_t *point_list, uint32_t *ranges, uint32_t *n_contrib,
                     gs_stream_t stream);

@@ -130,28 +130,81 @@ def oracle_backward(inp, ofwd, grads, compat="reference", swap=None):
 
 
 def export_state(P, W, H, fwd):
-    """Per-stage GPU state via gs_debug_export (for stage-level parity)."""
+    """Per-stage GPU state via gs_debug_export (for stage-level parity).  The
+    tile lists hold num_instances (<= num_rendered) entries: read the ranges
+    first, then the lists."""
     L_ = _lib.load()
     num_rendered, color, feat, depth, alpha, radii, geom, binning, img = fwd
     tiles = ((W + 15) // 16) * ((H + 15) // 16)
     f = lambda *s: torch.empty(*s, dtype=torch.float32, device=DEV)  # noqa: E731
     u = lambda *s: torch.empty(*s, dtype=torch.int32, device=DEV)  # noqa: E731
-    st = dict(means2D=f(P, 2), depths=f(P), conic_opacity=f(P, 4), rgb=f(P, 3), tiles=u(P),
-              point_list=u(max(num_rendered, 1)), ranges=u(tiles, 2), n_contrib=u(H * W))
     s = torch.cuda.current_stream().cuda_stream
+    rg = u(tiles, 2)
+    _lib.check(L_.gs_debug_export(P, W, H, geom.data_ptr(), None, img.data_ptr(), 0, None, None, None, None,
+                                  None, None, rg.data_ptr(), None, s), "debug export")
+    torch.cuda.synchronize()
+    n_inst = int(rg.view(torch.int64).cpu().numpy().view(np.uint32).reshape(-1, 2)[:, 1].max()) if tiles else 0
+    st = dict(means2D=f(P, 2), depths=f(P), conic_opacity=f(P, 4), rgb=f(P, 3), tiles=u(P),
+              point_list=u(max(n_inst, 1)), ranges=u(tiles, 2), n_contrib=u(H * W))
     _lib.check(L_.gs_debug_export(P, W, H, geom.data_ptr(), binning.data_ptr() if binning.numel() else None,
-                                  img.data_ptr(), num_rendered, st["means2D"].data_ptr(),
+                                  img.data_ptr(), n_inst, st["means2D"].data_ptr(),
                                   st["depths"].data_ptr(), st["conic_opacity"].data_ptr(),
                                   st["rgb"].data_ptr(), st["tiles"].data_ptr(),
                                   st["point_list"].data_ptr(), st["ranges"].data_ptr(),
                                   st["n_contrib"].data_ptr(), s), "debug export")
     torch.cuda.synchronize()
     out = {k: v.cpu().numpy() for k, v in st.items()}
-    out["point_list"] = out["point_list"][:num_rendered].view(np.uint32)
+    out["point_list"] = out["point_list"][:n_inst].view(np.uint32)
     out["tiles"] = out["tiles"].view(np.uint32)
     out["ranges"] = out["ranges"].view(np.uint32).reshape(-1)
     out["n_contrib"] = out["n_contrib"].view(np.uint32)
+    out["num_instances"] = n_inst
     return out
+
+
+def check_tile_lists(st_g, st_o, W, H):
+    """The binned tile lists against the reference's: every tile's list is the
+    reference's list (same (depth, index) order) minus instances whose
+    Gaussian reaches alpha >= 1/255 at no pixel of the tile (checked in float64
+    at every pixel centre, CR/forward.cu:350-360).  Also maps each pixel's
+    last contributor back to a Gaussian id and compares it with the
+    reference's.  Returns the fraction of instances dropped."""
+    rg = st_g["ranges"].reshape(-1, 2).astype(np.int64)
+    ro = np.asarray(st_o.ranges, np.int64).reshape(-1, 2)
+    pg, po = st_g["point_list"], np.asarray(st_o.point_list)
+    m2 = np.asarray(st_o.means2D, np.float64)
+    co = np.asarray(st_o.conic_opacity, np.float64)
+    gx = (W + 15) // 16
+    dropped = 0
+    for t in range(rg.shape[0]):
+        lo_list = po[ro[t, 0]:ro[t, 1]]
+        g_list = pg[rg[t, 0]:rg[t, 1]]
+        keep = np.isin(lo_list, g_list)
+        assert keep.sum() == len(g_list), f"tile {t}: instances not in the reference's list"
+        np.testing.assert_array_equal(lo_list[keep], g_list)
+        drop = lo_list[~keep].astype(np.int64)
+        dropped += len(drop)
+        if len(drop):
+            tx, ty = t % gx, t // gx
+            xs = np.arange(tx * 16, min(tx * 16 + 16, W), dtype=np.float64)
+            ys = np.arange(ty * 16, min(ty * 16 + 16, H), dtype=np.float64)
+            px, py = np.meshgrid(xs, ys)
+            dx = m2[drop, 0, None, None] - px[None]
+            dy = m2[drop, 1, None, None] - py[None]
+            a, b, c, op = (co[drop, k, None, None] for k in range(4))
+            power = -0.5 * (a * dx * dx + c * dy * dy) - b * dx * dy
+            alpha = np.minimum(0.99, op * np.exp(power))
+            blends = (power <= 0) & (alpha >= 1.0 / 255.0)
+            assert not blends.any(), f"tile {t}: a dropped instance blends"
+    # last contributor, as a Gaussian id
+    n_g = st_g["n_contrib"].astype(np.int64)
+    n_o = np.asarray(st_o.n_contrib, np.int64)
+    pix = np.arange(W * H)
+    tile = (pix // W // 16) * gx + (pix % W) // 16
+    gid_g = np.where(n_g > 0, pg[np.maximum(rg[tile, 0] + n_g - 1, 0).clip(0, max(len(pg) - 1, 0))] if len(pg) else -1, -1)
+    gid_o = np.where(n_o > 0, po[np.maximum(ro[tile, 0] + n_o - 1, 0).clip(0, max(len(po) - 1, 0))] if len(po) else -1, -1)
+    assert np.mean(gid_g == gid_o) >= 0.999
+    return dropped / max(len(po), 1)
 
 
 def psnr(a, b, peak=1.0):

@@ -45,7 +45,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_sizes():
     L = _lib.load()
-    assert L.gs_version() == _lib.ABI_VERSION == 3
+    assert L.gs_version() == _lib.ABI_VERSION == 4
     assert L.gs_geom_buffer_bytes(1) >= 64  # one 64-B render record at least
     for a, b in [(1000, 2000), (10_000, 300_000)]:
         assert L.gs_geom_buffer_bytes(b) > L.gs_geom_buffer_bytes(a)
@@ -61,11 +61,11 @@ def test_invalid_arguments_report_errors_without_gpu():
     import ctypes
     n = ctypes.c_int64(0)
     code = L.gs_forward_plan(ctypes.byref(g), ctypes.byref(c), 0, 0, 0, None, None, None,
-                             ctypes.byref(n), None)
+                             ctypes.byref(n), None, None)
     assert code < 0 and b"P must be" in L.gs_last_error()
     g = _lib.GsGaussians(P=10, F=7)
     code = L.gs_forward_plan(ctypes.byref(g), ctypes.byref(c), 0, 0, 0, None, None, None,
-                             ctypes.byref(n), None)
+                             ctypes.byref(n), None, None)
     assert code < 0 and b"feature width" in L.gs_last_error()
 
 
