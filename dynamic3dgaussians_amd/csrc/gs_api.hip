@@ -289,7 +289,7 @@ int gs_forward_render(const gs_gaussians* g, const gs_camera* cam, int debug, in
     const bool known = g_plan.image == image && g_plan.L == L;
     {
       StageTimer t(s, GS_STAGE_SORT);
-      launch_tile_sort(ta, known ? g_plan.max_len : -1, s);
+      launch_tile_sort(ta, known ? g_plan.max_len : -1, L, s);
     }
     if (int e = check("tile sort", debug, s)) return e;
   }

@@ -65,7 +65,8 @@ constexpr int TB_BLOCKS = 256;
 constexpr int TB_THREADS = 512;
 constexpr int TB_BINS = 16384;    // LDS tile bins per pass (64 KiB)
 constexpr int TS_CAP = 3584;      // per-tile LDS sort capacity (2 x 28 KiB of u64 keys)
-constexpr int TS_THREADS = 256;
+constexpr int TS_CAP_LONG = 9600; // long-tile launch: 2 x 75 KiB (+ 8 KiB radix state), one workgroup per CU
+constexpr int TS_WIDE_MEAN = 1024; // mean tile length from which the sort uses 512-thread workgroups
 
 // Geometry buffer (per-Gaussian state kept from forward to backward).
 struct GeomLayout {

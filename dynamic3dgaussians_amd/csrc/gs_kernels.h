@@ -118,7 +118,7 @@ void launch_tile_plan(const TileArgs& a, int prefiltered, hipStream_t s);
 // render: bucket the instances by tile, then sort every tile by (depth, id).
 // max_len = the plan header's longest tile (host copy), or -1 if unknown.
 void launch_tile_bucket(const TileArgs& a, hipStream_t s);
-void launch_tile_sort(const TileArgs& a, int64_t max_len, hipStream_t s);
+void launch_tile_sort(const TileArgs& a, int64_t max_len, int64_t L, hipStream_t s);
 
 bool launch_render_fwd(const RenderArgs& a, hipStream_t s);
 bool launch_render_bwd(const RenderBwdArgs& a, hipStream_t s);

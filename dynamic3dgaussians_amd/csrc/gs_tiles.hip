@@ -215,18 +215,21 @@ __device__ inline uint64_t match_digit8(uint32_t d, uint64_t valid) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+template <int NT>
 struct RadixSmem {
-  uint32_t wcnt[4][256];  // per-wave digit counts, then per-wave bases
-  uint32_t wsum[4];
+  static constexpr int TS_WAVES = NT / 64;
+  uint32_t wcnt[TS_WAVES][256];  // per-wave digit counts, then per-wave bases
+  uint32_t wsum[4];              // digit-scan partials (the first 256 threads)
   int skip, unsorted;
   uint32_t dmin, dmax;  // depth-bit range of the tile
 };
 
-template <class KP>
-__device__ __attribute__((always_inline)) KP tile_radix_sort(KP A, KP B, int n, RadixSmem& sm) {
+template <class KP, int TS_THREADS>
+__device__ __attribute__((always_inline)) KP tile_radix_sort(KP A, KP B, int n, RadixSmem<TS_THREADS>& sm) {
+  constexpr int TS_WAVES = TS_THREADS / 64;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint64_t lt = (1ull << lane) - 1ull;
-  const int q = (n + 3) >> 2;
+  const int q = (n + TS_WAVES - 1) / TS_WAVES;
   const int w0 = min(n, wave * q), w1 = min(n, w0 + q);
   KP src = A, dst = B;
   // Sort on depth bits relative to the tile's minimum: positive float bits
@@ -245,8 +248,7 @@ __device__ __attribute__((always_inline)) KP tile_radix_sort(KP A, KP B, int n, 
   const uint32_t dmin = sm.dmin, span = sm.dmax - dmin;
   const int nbits = span ? 32 - __builtin_clz(span) : 0;
   for (int shift = 0; shift < nbits; shift += 8) {
-#pragma unroll
-    for (int w = 0; w < 4; ++w) sm.wcnt[w][tid] = 0;
+    for (int i = tid; i < TS_WAVES * 256; i += TS_THREADS) (&sm.wcnt[0][0])[i] = 0;
     if (tid == 0) sm.skip = 0;
     __syncthreads();
     for (int i0 = w0; i0 < w1; i0 += 64) {
@@ -256,26 +258,37 @@ __device__ __attribute__((always_inline)) KP tile_radix_sort(KP A, KP B, int n, 
       if (valid) atomicAdd(&sm.wcnt[wave][(((uint32_t)(src[i] >> 32) - dmin) >> shift) & 255u], 1u);
     }
     __syncthreads();
-    const uint32_t c0 = sm.wcnt[0][tid], c1 = sm.wcnt[1][tid], c2 = sm.wcnt[2][tid], c3 = sm.wcnt[3][tid];
-    const uint32_t tot = c0 + c1 + c2 + c3;
-    if (tot == (uint32_t)n) sm.skip = 1;
-    // exclusive scan of the digit totals over the 256 threads
-    uint32_t inc = tot;
+    // digit d = tid (first 256 threads): total over the waves, exclusive
+    // scan over the digits, then per-(wave, digit) bases
+    uint32_t c[TS_WAVES];
+    uint32_t tot = 0, inc = 0;
+    if (tid < 256) {
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(inc, o, 64);
-      if (lane >= o) inc += y;
+      for (int w = 0; w < TS_WAVES; ++w) {
+        c[w] = sm.wcnt[w][tid];
+        tot += c[w];
+      }
+      if (tot == (uint32_t)n) sm.skip = 1;
+      inc = tot;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += y;
+      }
+      if (lane == 63) sm.wsum[wave] = inc;
     }
-    if (lane == 63) sm.wsum[wave] = inc;
     __syncthreads();
-    uint32_t ex = inc - tot;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) ex += w < wave ? sm.wsum[w] : 0u;
     const bool skip = sm.skip != 0;
-    sm.wcnt[0][tid] = ex;
-    sm.wcnt[1][tid] = ex + c0;
-    sm.wcnt[2][tid] = ex + c0 + c1;
-    sm.wcnt[3][tid] = ex + c0 + c1 + c2;
+    if (tid < 256) {
+      uint32_t ex = inc - tot;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) ex += w < wave ? sm.wsum[w] : 0u;
+#pragma unroll
+      for (int w = 0; w < TS_WAVES; ++w) {
+        sm.wcnt[w][tid] = ex;
+        ex += c[w];
+      }
+    }
     __syncthreads();
     if (skip) continue;  // uniform: one digit holds every key
     for (int i0 = w0; i0 < w1; i0 += 64) {
@@ -317,27 +330,30 @@ __device__ __attribute__((always_inline)) KP tile_radix_sort(KP A, KP B, int n, 
   return src;
 }
 
-__global__ __launch_bounds__(TS_THREADS) void tile_sort_kernel(const uint2* __restrict__ ranges,
-                                                               uint64_t* __restrict__ keys,
-                                                               uint64_t* __restrict__ keys2,
-                                                               uint32_t* __restrict__ plist, int cap) {
+// One tile per workgroup of NT threads (tiles of length lo < n <= hi; the
+// others exit).  Keys sorted in LDS up to `cap` (the launch's dynamic LDS),
+// in global memory beyond.
+template <int NT>
+__global__ __launch_bounds__(NT) void tile_sort_kernel(const uint2* __restrict__ ranges,
+                                                       uint64_t* __restrict__ keys, uint64_t* __restrict__ keys2,
+                                                       uint32_t* __restrict__ plist, int cap, int lo, int hi) {
   extern __shared__ uint64_t s_key[];  // 2 x cap keys
-  __shared__ RadixSmem sm;
+  __shared__ RadixSmem<NT> sm;
   const uint2 r = ranges[blockIdx.x];
   const int n = (int)(r.y - r.x);
-  if (n == 0) return;
+  if (n == 0 || n <= lo || n > hi) return;
   if (n == 1) {
     if (threadIdx.x == 0) plist[r.x] = (uint32_t)keys[r.x];
     return;
   }
   if (n <= cap) {
-    for (int i = threadIdx.x; i < n; i += TS_THREADS) s_key[i] = keys[r.x + i];
+    for (int i = threadIdx.x; i < n; i += NT) s_key[i] = keys[r.x + i];
     __syncthreads();
-    const uint64_t* out = tile_radix_sort<uint64_t*>(s_key, s_key + cap, n, sm);
-    for (int i = threadIdx.x; i < n; i += TS_THREADS) plist[r.x + i] = (uint32_t)out[i];
+    const uint64_t* out = tile_radix_sort<uint64_t*, NT>(s_key, s_key + cap, n, sm);
+    for (int i = threadIdx.x; i < n; i += NT) plist[r.x + i] = (uint32_t)out[i];
   } else {  // longer than the LDS capacity of this launch: sort in global memory
-    const uint64_t* out = tile_radix_sort<uint64_t*>(keys + r.x, keys2 + r.x, n, sm);
-    for (int i = threadIdx.x; i < n; i += TS_THREADS) plist[r.x + i] = (uint32_t)out[i];
+    const uint64_t* out = tile_radix_sort<uint64_t*, NT>(keys + r.x, keys2 + r.x, n, sm);
+    for (int i = threadIdx.x; i < n; i += NT) plist[r.x + i] = (uint32_t)out[i];
   }
 }
 
@@ -364,11 +380,34 @@ void launch_tile_bucket(const TileArgs& a, hipStream_t s) {
   }
 }
 
-void launch_tile_sort(const TileArgs& a, int64_t max_len, hipStream_t s) {
+template <int NT>
+static void tile_sort_launches(const TileArgs& a, int64_t max_len, hipStream_t s) {
+  const dim3 grid(a.num_tiles), block(NT);
+  const int big = 0x7FFFFFFF;
   // LDS sized to the longest tile when the plan's header is known on the host
-  const int cap = (max_len >= 0 && max_len < TS_CAP) ? (int)max_len : TS_CAP;
-  hipLaunchKernelGGL(tile_sort_kernel, dim3(a.num_tiles), dim3(TS_THREADS), 2 * sizeof(uint64_t) * (cap > 0 ? cap : 1),
-                     s, a.ranges, a.keys, a.keys2, a.plist, cap > 0 ? cap : 1);
+  if (max_len >= 0 && max_len <= TS_CAP) {
+    const int cap = max_len > 0 ? (int)max_len : 1;
+    hipLaunchKernelGGL(tile_sort_kernel<NT>, grid, block, 2 * sizeof(uint64_t) * cap, s, a.ranges, a.keys,
+                       a.keys2, a.plist, cap, 0, big);
+    return;
+  }
+  // Long tiles (large scenes): the common tiles keep TS_CAP-sized LDS and
+  // several workgroups per CU; the long ones follow in a second launch with
+  // up to the whole 160 KiB per workgroup (global memory beyond TS_CAP_LONG).
+  hipLaunchKernelGGL(tile_sort_kernel<NT>, grid, block, 2 * sizeof(uint64_t) * TS_CAP, s, a.ranges, a.keys,
+                     a.keys2, a.plist, TS_CAP, 0, TS_CAP);
+  const int cap2 = (max_len >= 0 && max_len < TS_CAP_LONG) ? (int)max_len : TS_CAP_LONG;
+  hipLaunchKernelGGL(tile_sort_kernel<NT>, grid, block, 2 * sizeof(uint64_t) * cap2, s, a.ranges, a.keys,
+                     a.keys2, a.plist, cap2, TS_CAP, big);
+}
+
+void launch_tile_sort(const TileArgs& a, int64_t max_len, int64_t L, hipStream_t s) {
+  // workgroup size by the mean tile length: 256 threads keep short tiles'
+  // per-pass overhead low (bench camera: ~660 keys per tile), 512 split long
+  // tiles' passes over twice the waves (1080p / 1M Gaussians: ~1800)
+  const int64_t mean = a.num_tiles > 0 ? L / a.num_tiles : 0;
+  if (L >= 0 && mean >= TS_WIDE_MEAN) tile_sort_launches<512>(a, max_len, s);
+  else tile_sort_launches<256>(a, max_len, s);
 }
 
 }  // namespace gs
