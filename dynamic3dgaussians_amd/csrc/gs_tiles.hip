@@ -140,9 +140,10 @@ __global__ __launch_bounds__(OFF_T) void tile_offsets_kernel(const uint32_t* __r
                                                              uint2* __restrict__ ranges,
                                                              uint32_t* __restrict__ meta, int prefiltered) {
   __shared__ unsigned long long s_sum[OFF_T / 64];
+  __shared__ unsigned long long s_lref;
   __shared__ uint32_t s_max;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (tid == 0) s_max = 0;
+  if (tid == 0) { s_max = 0; s_lref = 0; }
   const int per = (T + OFF_T - 1) / OFF_T;
   const int a0 = min(T, tid * per), a1 = min(T, a0 + per);
   unsigned long long sum = 0;
@@ -162,6 +163,13 @@ __global__ __launch_bounds__(OFF_T) void tile_offsets_kernel(const uint32_t* __r
   if (lane == 63) s_sum[wave] = inc;
   __syncthreads();
   atomicMax(&s_max, mx);
+  // the reference's num_rendered: sum of the per-block tiles_touched sums
+  if (tid < TB_BLOCKS) {
+    unsigned long long v = bsum[tid];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) atomicAdd(&s_lref, v);
+  }
   unsigned long long woff = 0, total = 0;
 #pragma unroll
   for (int w = 0; w < OFF_T / 64; ++w) {
@@ -178,8 +186,7 @@ __global__ __launch_bounds__(OFF_T) void tile_offsets_kernel(const uint32_t* __r
   }
   __syncthreads();
   if (tid == 0) {
-    unsigned long long lref = 0;
-    for (int bb = 0; bb < TB_BLOCKS; ++bb) lref += bsum[bb];
+    const unsigned long long lref = s_lref;
     // ranges are 32-bit, as in the reference
     const uint32_t ovf = (total > 0xFFFFFFFFull || lref > 0xFFFFFFFFull) ? 2u : 0u;
     meta[M_L] = (uint32_t)total;
