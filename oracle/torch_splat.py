@@ -5,8 +5,8 @@ Only tests/ may import this module, as a checker.  It restates the
 rasterizer's forward -- preprocess (CR/forward.cu:174-260: projection,
 computeCov3D :129-163, computeCov2D :75-124, getRect CR/auxiliary.h:46-56)
 and the per-pixel front-to-back blend (CR/forward.cu:330-380) -- as dense
-float64 tensor algebra over every (pixel, Gaussian) pair, so that torch
-autograd differentiates it.  That gives gradients derived independently of
+float64 tensor algebra over every (pixel, Gaussian) pair of each 16x16 tile
+and its tile list, so that torch autograd differentiates it.  That gives gradients derived independently of
 both the reference's hand-written backward (CR/backward.cu) and the C oracle
 (oracle/gs_oracle.c): `tests/test_gpu_autograd.py` checks the HIP backward
 against them.
@@ -17,7 +17,8 @@ term -- are the ones "fixed" removes; the forward quirks Q7 unnormalised
 quaternion, Q8 z <= 0 culling, Q9 asymmetric clamp, Q14 unnormalised depth
 are reproduced).  Discrete decisions (tile membership by the radius rect,
 alpha >= 1/255, the T < 1e-4 stop) are made without gradient, like the
-reference.  Memory is O(pixels x Gaussians) per pixel chunk: small scenes only.
+reference.  Autograd keeps every tile's pairs: O(256 x tile instances)
+memory, small scenes only.
 """
 from __future__ import annotations
 
@@ -120,7 +121,7 @@ def preprocess(means3D, scales, rotations, view, proj, tanfovx, tanfovy, cx, cy,
 
 
 def render(means3D, colors, opacity, scales, rotations, view, proj, tanfovx, tanfovy, cx, cy, W, H, bg,
-           features=None, means2D=None, scale_modifier=1.0, chunk=1024):
+           features=None, means2D=None, scale_modifier=1.0):
     """-> (color [3,H,W], depth [1,H,W], features [F,H,W] or None,
     alpha = 1 - T_final [1,H,W]), float64, differentiable in every float
     input (means2D: the NDC offset leaf)."""
@@ -136,34 +137,55 @@ def render(means3D, colors, opacity, scales, rotations, view, proj, tanfovx, tan
     col = colors[order]
     feat = features[order] if features is not None else None
     rmin_x, rmin_y, rmax_x, rmax_y = (r[order] for r in pre["rect"])
-    ys, xs = torch.meshgrid(torch.arange(H, dtype=torch.float64), torch.arange(W, dtype=torch.float64),
-                            indexing="ij")
-    pix_x, pix_y = xs.reshape(-1), ys.reshape(-1)
-    out_c, out_d, out_f, out_a = [], [], [], []
-    for s in range(0, W * H, chunk):
-        qx, qy = pix_x[s:s + chunk, None], pix_y[s:s + chunk, None]
-        tx_, ty_ = (qx // TILE), (qy // TILE)
-        member = (tx_ >= rmin_x) & (tx_ < rmax_x) & (ty_ >= rmin_y) & (ty_ < rmax_y)
-        dx, dy = px[None] - qx, py[None] - qy
-        power = -0.5 * (con[:, 0] * dx * dx + con[:, 2] * dy * dy) - con[:, 1] * dx * dy
-        alpha = torch.clamp(op[None] * torch.exp(power), max=0.99)
-        with torch.no_grad():
-            valid = member & (power <= 0) & (alpha >= 1.0 / 255.0)
-        a = torch.where(valid, alpha, torch.zeros_like(alpha))
-        one_m = 1.0 - a
-        T_excl = torch.cumprod(torch.cat([torch.ones_like(one_m[:, :1]), one_m[:, :-1]], 1), 1)
-        with torch.no_grad():
-            stop = valid & (T_excl * one_m < 1e-4)
-            keep = torch.cumsum(stop.int(), 1) == 0
-        w = a * T_excl * keep
-        T_final = torch.prod(torch.where(keep, one_m, torch.ones_like(one_m)), 1)
-        out_c.append(w @ col + T_final[:, None] * bg[None])
-        out_d.append(w @ z)
-        out_a.append(1.0 - T_final)
-        if feat is not None:
-            out_f.append(w @ feat)
-    color = torch.cat(out_c, 0).T.reshape(3, H, W)
-    depth = torch.cat(out_d, 0).reshape(1, H, W)
-    fmap = torch.cat(out_f, 0).T.reshape(-1, H, W) if feat is not None else None
-    alpha = torch.cat(out_a, 0).reshape(1, H, W)
+    # per 16x16 tile: the tile's pixels against the Gaussians whose rect
+    # contains it (the reference's tile lists), dense over those pairs
+    gx, gy = (W + TILE - 1) // TILE, (H + TILE - 1) // TILE
+    Fd = feat.shape[1] if feat is not None else 0
+    fmap = None
+    rows_c, rows_d, rows_a, rows_f, where = [], [], [], [], []
+    for ty in range(gy):
+        for tx in range(gx):
+            x0, y0 = tx * TILE, ty * TILE
+            x1, y1 = min(x0 + TILE, W), min(y0 + TILE, H)
+            ys, xs = torch.meshgrid(torch.arange(y0, y1, dtype=torch.float64),
+                                    torch.arange(x0, x1, dtype=torch.float64), indexing="ij")
+            qx, qy = xs.reshape(-1, 1), ys.reshape(-1, 1)
+            m = torch.nonzero((tx >= rmin_x) & (tx < rmax_x) & (ty >= rmin_y) & (ty < rmax_y)).squeeze(1)
+            if m.numel() == 0:
+                c = bg[None].expand(qx.shape[0], 3)
+                rows_c.append(c); rows_d.append(torch.zeros(qx.shape[0], dtype=means3D.dtype))
+                rows_a.append(torch.zeros(qx.shape[0], dtype=means3D.dtype))
+                if feat is not None:
+                    rows_f.append(torch.zeros(qx.shape[0], Fd, dtype=means3D.dtype))
+                where.append((x0, y0, x1, y1))
+                continue
+            dx, dy = px[m][None] - qx, py[m][None] - qy
+            cm = con[m]
+            power = -0.5 * (cm[:, 0] * dx * dx + cm[:, 2] * dy * dy) - cm[:, 1] * dx * dy
+            alpha = torch.clamp(op[m][None] * torch.exp(power), max=0.99)
+            with torch.no_grad():
+                valid = (power <= 0) & (alpha >= 1.0 / 255.0)
+            a = torch.where(valid, alpha, torch.zeros_like(alpha))
+            one_m = 1.0 - a
+            T_excl = torch.cumprod(torch.cat([torch.ones_like(one_m[:, :1]), one_m[:, :-1]], 1), 1)
+            with torch.no_grad():
+                stop = valid & (T_excl * one_m < 1e-4)
+                keep = torch.cumsum(stop.int(), 1) == 0
+            w = a * T_excl * keep
+            T_final = torch.prod(torch.where(keep, one_m, torch.ones_like(one_m)), 1)
+            rows_c.append(w @ col[m] + T_final[:, None] * bg[None])
+            rows_d.append(w @ z[m])
+            rows_a.append(1.0 - T_final)
+            if feat is not None:
+                rows_f.append(w @ feat[m])
+            where.append((x0, y0, x1, y1))
+    # assemble (index_put keeps the graph)
+    pix = torch.cat([(torch.arange(y0, y1)[:, None] * W + torch.arange(x0, x1)[None]).reshape(-1)
+                     for (x0, y0, x1, y1) in where])
+    color = torch.zeros(H * W, 3, dtype=means3D.dtype).index_put((pix,), torch.cat(rows_c, 0)).T.reshape(3, H, W)
+    depth = torch.zeros(H * W, dtype=means3D.dtype).index_put((pix,), torch.cat(rows_d, 0)).reshape(1, H, W)
+    alpha = torch.zeros(H * W, dtype=means3D.dtype).index_put((pix,), torch.cat(rows_a, 0)).reshape(1, H, W)
+    if feat is not None:
+        fmap = torch.zeros(H * W, Fd, dtype=means3D.dtype).index_put((pix,), torch.cat(rows_f, 0)).T.reshape(
+            Fd, H, W)
     return color, depth, fmap, alpha
