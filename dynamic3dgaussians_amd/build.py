@@ -35,11 +35,9 @@ VARIANT_FLAGS = {"": [], "stats": ["-DGS_STATS"],
                  "exp_nofeat": ["-DGS_EXP_NO_FEAT_ATOMIC"], "exp_noacc": ["-DGS_EXP_NO_ACC_ATOMIC"],
                  "exp_noatomic": ["-DGS_EXP_NO_FEAT_ATOMIC", "-DGS_EXP_NO_ACC_ATOMIC"],
                  "exp_fwd_noload": ["-DGS_EXP_FWD_NO_FEAT_LOAD"], "exp_fwd_nomfma": ["-DGS_EXP_FWD_NO_MFMA"],
-                 "exp_bwd_nodlf": ["-DGS_EXP_BWD_NO_DLF"], "exp_bwd_nomfma": ["-DGS_EXP_BWD_NO_MFMA"],
                  "exp_occ5": ["-DGS_EXP_FWD_LDS_PAD=18000"], "exp_occ3": ["-DGS_EXP_FWD_LDS_PAD=40000"],
-                 "exp_fwd_valu": ["-DGS_EXP_FWD_VALU_FEAT"], "exp_bwd_valu": ["-DGS_EXP_BWD_VALU_FEAT"],
-                 "exp_boxcull": ["-DGS_EXP_BOX_CULL"],
-                 "exp_fwd_wpe5": ["-DGS_FWD_WPE=5"], "exp_fwd_wpe6": ["-DGS_FWD_WPE=6"]}
+                 "exp_fwd_valu": ["-DGS_EXP_FWD_VALU_FEAT"],
+                 "exp_wg1": ["-DGS_WPB_FWD=1"], "exp_wg4": ["-DGS_WPB_BWD=4"], "exp_bwd_wpe3": ["-DGS_BWD_WPE=3"],  "exp_fwd_wpe5": ["-DGS_FWD_WPE=5"], "exp_fwd_wpe6": ["-DGS_FWD_WPE=6"]}
 ARCH = os.environ.get("GSPLAT_OFFLOAD_ARCH", "gfx950")
 
 # Per-file flags.  The preprocess kernels are compiled without FMA

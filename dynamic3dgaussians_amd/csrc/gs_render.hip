@@ -30,6 +30,18 @@ namespace gs {
 
 constexpr float ALPHA_MIN = 1.0f / 255.0f;
 constexpr int CHUNK = 64;
+// Waves per workgroup in the blend kernels.  Each wave owns one 16x4 strip
+// and never synchronises with the others.  Measured (bench camera, F = 32):
+// the forward is faster with a tile per workgroup (its 4 waves gather the
+// same records through one CU's L1: 0.202 vs 0.223 ms), the backward with a
+// wave per workgroup (its 12 KiB of LDS are released the moment its strip is
+// done: 0.330 vs 0.342 ms).
+#ifndef GS_WPB_FWD
+#define GS_WPB_FWD 4
+#endif
+#ifndef GS_WPB_BWD
+#define GS_WPB_BWD 1
+#endif
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float float4_t __attribute__((ext_vector_type(4)));
 
@@ -80,13 +92,15 @@ __device__ inline void swap32(float a, float b, float& lo, float& hi) {
   hi = bits_f(r[1]);
 }
 
-// Gather the record of list entry i (all 16 fields).  The index is clamped
+// Gather the fields of list entry i's record the blend kernels use.  The index is clamped
 // to the last entry of the (non-empty) range, so the loads are unconditional:
 // lanes past the end re-read a valid record and are masked out by the caller.
 // (A conditional update of a register struct made the compiler keep it in
 // scratch memory.)
 struct RecRegs {
-  float4 q0, q1, q2, q3;
+  float4 q0, q1;
+  float2 q2;  // b, depth
+  float tq;   // cull threshold
   uint32_t gid;
 };
 __device__ inline RecRegs load_rec(const uint32_t* __restrict__ point_list, const float* __restrict__ rec,
@@ -96,8 +110,8 @@ __device__ inline RecRegs load_rec(const uint32_t* __restrict__ point_list, cons
   const float4* p = reinterpret_cast<const float4*>(rec + (size_t)r.gid * REC);
   r.q0 = p[0];  // x, y, conic a, conic b
   r.q1 = p[1];  // conic c, opacity, r, g
-  r.q2 = p[2];  // b, depth, ext x, ext y
-  r.q3 = p[3];  // radius, cull threshold tq, -, -
+  r.q2 = reinterpret_cast<const float2*>(p)[4];  // b, depth (R_EX, R_EY, R_RAD unused)
+  r.tq = reinterpret_cast<const float*>(p)[R_TQ];
   return r;
 }
 
@@ -117,10 +131,33 @@ __device__ inline float gauss_power(float dx, float dy, const float4& h) {
 // conic and threshold tq: exact up to tq's margin, so it culls the Gaussians
 // whose bounding box touches the strip but whose ellipse does not.
 __device__ inline bool strip_culled(const RecRegs& q, float sx0, float sx1, float sy0, float sy1) {
-#ifdef GS_EXP_BOX_CULL
-  return q.q0.x + q.q2.z < sx0 || q.q0.x - q.q2.z > sx1 || q.q0.y + q.q2.w < sy0 || q.q0.y - q.q2.w > sy1;
-#endif
-  return rect_culled(q.q0.x, q.q0.y, q.q0.z, q.q0.w, q.q1.x, q.q3.y, sx0, sx1, sy0, sy1);
+  return rect_culled(q.q0.x, q.q0.y, q.q0.z, q.q0.w, q.q1.x, q.tq, sx0, sx1, sy0, sy1);
+}
+
+// ------------------------------------------------------------------ bf16 split products
+// fp32 contractions on the bf16 matrix cores (16x the fp32 MFMA rate): every
+// operand is split x = hi + lo into two bf16 (x - hi is exact in fp32) and
+// a*b is summed as hi*hi + hi*lo + lo*hi with fp32 accumulation, ~2^-17
+// relative per product (the dropped lo*lo and the split residues).
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ inline float4_t mfma_bf16(const bf16x8& a, const bf16x8& b, float4_t c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ inline void split_bf16(const float (&x)[8], bf16x8& hi, bf16x8& lo) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const __bf16 h = (__bf16)x[j];
+    hi[j] = h;
+    lo[j] = (__bf16)(x[j] - (float)h);
+  }
+}
+// 3-term split product (a_hi b_hi + a_hi b_lo + a_lo b_hi) accumulated into c
+__device__ inline float4_t mfma3(const bf16x8& ah, const bf16x8& al, const bf16x8& bh, const bf16x8& bl,
+                                 float4_t c) {
+  c = mfma_bf16(ah, bh, c);
+  c = mfma_bf16(ah, bl, c);
+  return mfma_bf16(al, bh, c);
 }
 
 // ------------------------------------------------------------------ forward
@@ -131,7 +168,7 @@ __device__ inline bool strip_culled(const RecRegs& q, float sx0, float sx1, floa
 #define GS_FWD_ATTR
 #endif
 template <int F, int COMPAT>
-__global__ __launch_bounds__(256) GS_FWD_ATTR void render_fwd_kernel(
+__global__ __launch_bounds__(64 * GS_WPB_FWD) GS_FWD_ATTR void render_fwd_kernel(
     int W, int H, int grid_x, int num_tiles, const uint2* __restrict__ ranges,
     const uint32_t* __restrict__ point_list, const float* __restrict__ rec,
     const float* __restrict__ feats, const float* __restrict__ bg, float* __restrict__ out_color,
@@ -144,10 +181,16 @@ __global__ __launch_bounds__(256) GS_FWD_ATTR void render_fwd_kernel(
   constexpr int FB = MF ? F / 32 : 1;        // 32-channel blocks
   constexpr int NSF = (!MF && F > 0) ? F : 1;
   // per record: (x, y, -a/2, -b) (-c/2, opacity, r, g) (b, depth, -, -)
-  __shared__ float4 s_rec[4][CHUNK][3];
+  __shared__ float4 s_rec[GS_WPB_FWD][CHUNK][3];
 
-  const int tile = xcd_remap(blockIdx.x, num_tiles);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // strip item = tile * 4 + wave; consecutive items share an XCD (and its L2)
+  const int lane = threadIdx.x & 63, lw = threadIdx.x >> 6;  // lw: LDS slot of the wave
+#if GS_WPB_FWD == 4
+  const int tile = xcd_remap(blockIdx.x, num_tiles), wave = lw;
+#else
+  const int item = xcd_remap(blockIdx.x, num_tiles * (4 / GS_WPB_FWD)) * GS_WPB_FWD + lw;
+  const int tile = item >> 2, wave = item & 3;
+#endif
   const int tx = tile % grid_x, ty = tile / grid_x;
   const int px = tx * TILE + (lane & 15), py = ty * TILE + wave * WAVE_ROWS + (lane >> 4);
   const bool inside = px < W && py < H;
@@ -204,9 +247,9 @@ __global__ __launch_bounds__(256) GS_FWD_ATTR void render_fwd_kernel(
     const bool keep = (c0 + lane < range.y) && !strip_culled(q, sx0, sx1, sy0, sy1);
     {
       const float4 h = half_conic(q.q0, q.q1);
-      s_rec[wave][lane][0] = make_float4(q.q0.x, q.q0.y, h.x, h.y);
-      s_rec[wave][lane][1] = make_float4(h.z, q.q1.y, q.q1.z, q.q1.w);
-      s_rec[wave][lane][2] = q.q2;
+      s_rec[lw][lane][0] = make_float4(q.q0.x, q.q0.y, h.x, h.y);
+      s_rec[lw][lane][1] = make_float4(h.z, q.q1.y, q.q1.z, q.q1.w);
+      s_rec[lw][lane][2] = make_float4(q.q2.x, q.q2.y, 0.f, 0.f);
     }
     const uint32_t chunk_gid = q.gid;  // lane j: id of the chunk's j-th record
     uint64_t mask = __ballot(keep);
@@ -227,9 +270,9 @@ __global__ __launch_bounds__(256) GS_FWD_ATTR void render_fwd_kernel(
       }
       STAT(3, 1);
       STAT_INC(st_it);
-      const float4 r0 = s_rec[wave][j][0];
-      const float4 r1 = s_rec[wave][j][1];
-      const float4 r2 = s_rec[wave][j][2];
+      const float4 r0 = s_rec[lw][j][0];
+      const float4 r1 = s_rec[lw][j][1];
+      const float4 r2 = s_rec[lw][j][2];
       const float dx = r0.x - pfx, dy = r0.y - pfy;
       const float power = gauss_power(dx, dy, make_float4(r0.z, r0.w, r1.x, 0.f));
       const float alpha = fminf(0.99f, r1.y * fast_exp(power));
@@ -353,91 +396,64 @@ blend_done:
 }
 
 // ------------------------------------------------------------------ backward
-
-// Reduce N per-lane components over the wave and add them with one atomic
-// wave-instruction per 64 components: components [0, A_FEAT) go to the
-// per-Gaussian record acc[g][0..A_FEAT), features to dsem[g][0..F).
-template <int N, int OFF = 0>
-__device__ inline void commit(const float (&v)[N], float* __restrict__ acc_g, float* __restrict__ dsem_g,
-                              int lane) {
-  constexpr int n = (N - OFF) < 64 ? (N - OFF) : 64;
-  float t[64];
-#pragma unroll
-  for (int c = 0; c < n; ++c) t[c] = v[OFF + c];
-  const float s = wave_reduce_transposed<n>(t, lane);
-  const int comp = OFF + bitrev6(lane);
-#ifdef GS_EXP_NO_ACC_ATOMIC
-  if (comp < OFF + n && s == 12345.f) acc_g[comp] = s;
-#else
-  if (comp < OFF + n) atomicAdd(comp < A_FEAT ? acc_g + comp : dsem_g + (comp - A_FEAT), s);
-#endif
-  if constexpr (OFF + 64 < N) commit<N, OFF + 64>(v, acc_g, dsem_g, lane);
-}
-
-// dL/dsemantic of a batch of WB (<= 16) Gaussians: C[g][ch] = sum over the
-// wave's 64 pixels of w[g][pix] * dLf[pix][ch] on v_mfma_f32_16x16x4_f32
-// (A[g = l&15][k = l>>4] from the batch weights in LDS, B from registers,
-// C row (l>>4)*4 + r, column l&15), then one atomic per (Gaussian, channel).
-__device__ inline float4_t mfma16(float a, float b, float4_t c) {
-  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-}
-template <int F, int WB>
-__device__ inline void flush_feature_batch(const float (*w)[68], const uint32_t* bgid, const float (&Bs)[F / 16][16],
-                                           float* __restrict__ dsem, int lane, int rows) {
-  float a[16];
-#pragma unroll
-  for (int s = 0; s < 16; ++s) a[s] = w[lane & 15][4 * s + (lane >> 4)];
-#pragma unroll
-  for (int cb = 0; cb < F / 16; ++cb) {
-    float4_t c = float4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < 16; ++s) c = mfma16(a[s], Bs[cb][s], c);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = (lane >> 4) * 4 + r;
-      if (row < rows) {
-#ifdef GS_EXP_NO_FEAT_ATOMIC
-        if (c[r] == 12345.f) dsem[(size_t)bgid[row] * F + cb * 16 + (lane & 15)] = c[r];
-#else
-        atomicAdd(dsem + (size_t)bgid[row] * F + cb * 16 + (lane & 15), c[r]);
-#endif
-      }
-    }
-  }
-}
-
+//
+// Every per-Gaussian sum of the backward is a contraction over the wave's 64
+// pixels of one of two per-(Gaussian, pixel) weights with per-pixel
+// constants:
+//   w = alpha T            (dL/dcolour, dL/ddepth, dL/dfeature):
+//       sum_pix w * {dL/dC_r, dL/dC_g, dL/dC_b, dL/dD, dL/dF_ch}
+//   u = G dL/dopacity_pix  (dL/dopacity, dL/dmean2D, dL/dconic):
+//       sum_pix u * {1, dx, dy, dx^2, dx dy, dy^2}  with dx = mean_x - px;
+//       dx = m' - X/2 for the strip-centred pixel coordinate X = 2(px - cx)
+//       (an odd integer), so these follow from the per-pixel monomials
+//       {1, X, Y, X^2, XY, Y^2} (exact in bf16) and the Gaussian's m'.
+// A wave parks w and u of 16 contributing Gaussians in LDS and contracts the
+// batch on the matrix cores (v_mfma_f32_16x16x32_bf16, K = pixels) instead of
+// reducing each Gaussian's sums over the wave with cross-lane VALU work.
+// Operands are split into two bf16 (split_bf16; the monomials are exact, so
+// their products take two terms).
+// Waves per SIMD the backward asks the register allocator for: 3 (<= 168
+// VGPRs) where that fits without spilling, measured 0.336 vs 0.388 ms at 2
+// waves on the bench camera (F = 32); the widest instantiations keep 2.
 template <int F, int COMPAT>
-__global__ __launch_bounds__(256) void render_bwd_kernel(
+constexpr int bwd_waves_per_simd() {
+#ifdef GS_BWD_WPE
+  return GS_BWD_WPE;
+#else
+  return (F < 32 || (F == 32 && COMPAT == COMPAT_REFERENCE)) ? 3 : 2;
+#endif
+}
+template <int F, int COMPAT>
+__global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu(bwd_waves_per_simd<F, COMPAT>(), 8))) void render_bwd_kernel(
     int W, int H, int grid_x, int num_tiles, const uint2* __restrict__ ranges,
     const uint32_t* __restrict__ point_list, const float* __restrict__ rec,
     const float* __restrict__ feats, const float* __restrict__ bg, const float* __restrict__ alphas,
     const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dpix,
     const float* __restrict__ dL_dfeat, const float* __restrict__ dL_ddepth,
     const float* __restrict__ dL_dalpha, float* __restrict__ acc, float* __restrict__ dsem) {
-#ifdef GS_EXP_BWD_VALU_FEAT
-  constexpr bool MF = false;
-#else
-  constexpr bool MF = (F == 32 || F == 64);
-#endif
-  constexpr int FB = MF ? F / 32 : 1;
-  constexpr int NV = MF ? A_FEAT : A_FEAT + F;  // components reduced on the VALU
-  constexpr int WB = 16;                        // Gaussians per MFMA batch
-  constexpr int CB = MF ? F / 16 : 1;           // 16-channel blocks
+  constexpr int WB = 16;                      // Gaussians per matrix batch
+  constexpr int CB = F >= 16 ? F / 16 : 0;    // 16-channel feature blocks with their own accumulators
+  constexpr int CB1 = CB > 0 ? CB : 1;
+  constexpr int FW = F < 16 ? F : 0;          // feature rows 4.. of the colour block (F = 4, 8)
   constexpr bool FIXED_FEAT = (COMPAT != COMPAT_REFERENCE) && F > 0;
-  constexpr int NF_REG = (!MF && F > 0) ? F : 1;
-  __shared__ float4 s_rec[4][CHUNK][4];  // the record's 3 float4 + half conic
-  // batch weights w[g][pixel] (row pad 4: the 16x16x4 A reads are conflict-free)
-  __shared__ float s_w[MF ? 4 : 1][MF ? WB : 1][68];
-  __shared__ uint32_t s_bgid[MF ? 4 : 1][WB];
+  // per record: (x, y, -a/2, -b) (-c/2, opacity, r, g) (b, depth, -, -)
+  __shared__ float4 s_rec[GS_WPB_BWD][CHUNK][3];
+  // batch weights [slot][pixel] (row pad 4: the operand reads are conflict-free)
+  __shared__ float s_w[GS_WPB_BWD][WB][68];
+  __shared__ float s_u[GS_WPB_BWD][WB][68];
+  __shared__ float4 s_slot[GS_WPB_BWD][WB];  // (mean x - cx, mean y - cy, opacity, id bits)
 
-  const int tile = xcd_remap(blockIdx.x, num_tiles);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // strip item = tile * 4 + wave; consecutive items share an XCD (and its L2)
+  const int lane = threadIdx.x & 63, lw = threadIdx.x >> 6;  // lw: LDS slot of the wave
+  const int item = xcd_remap(blockIdx.x, num_tiles * (4 / GS_WPB_BWD)) * GS_WPB_BWD + lw;
+  const int tile = item >> 2, wave = item & 3;
   const int tx = tile % grid_x, ty = tile / grid_x;
   const int px = tx * TILE + (lane & 15), py = ty * TILE + wave * WAVE_ROWS + (lane >> 4);
   const bool inside = px < W && py < H;
   const float pfx = (float)px, pfy = (float)py;
   const float sx0 = (float)(tx * TILE), sx1 = sx0 + 15.0f;
   const float sy0 = (float)(ty * TILE + wave * WAVE_ROWS), sy1 = sy0 + 3.0f;
+  const float cx = sx0 + 7.5f, cy = sy0 + 1.5f;  // strip centre
   const uint2 range = ranges[tile];
   const size_t HW = (size_t)H * W, pix = inside ? (size_t)py * W + px : 0;
 
@@ -452,41 +468,176 @@ __global__ __launch_bounds__(256) void render_bwd_kernel(
   const float dLd = inside && dL_ddepth ? dL_ddepth[pix] : 0.f;
   const float dLa = inside && dL_dalpha ? dL_dalpha[pix] : 0.f;
   const float bg_dot = bg[0] * dLp[0] + bg[1] * dLp[1] + bg[2] * dLp[2];
-
-  // Upstream feature gradients.  VALU path: one register per channel.
-  // MFMA path (v_mfma_f32_16x16x4_f32, K = pixels): the B operands of
-  // dL/df = W . dLf, lane l / step s / block cb holding
-  // dLf[pixel 4s + (l>>4)][channel 16cb + (l&15)], transposed through LDS.
-  float dLf[NF_REG];
-  float Bs[MF ? CB : 1][MF ? 16 : 1];
-  float dLf_own[FIXED_FEAT && MF ? F : 1];  // fixed mode also needs f . dLf per pixel
-  if constexpr (MF) {
-    // B operands straight from the CHW image: lane l, step s reads channel
-    // 16cb + (l&15) at strip pixel 4s + (l>>4) (4 lanes share a 16-B run of
-    // one row); the loads are first needed at the first batch flush.
+  float dLf_own[FIXED_FEAT ? F : 1];  // fixed mode: f . dL/dF feeds dL/dalpha
+  if constexpr (FIXED_FEAT) {
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const int p = 4 * s + (lane >> 4);
-      const int qx = tx * TILE + (p & 15), qy = ty * TILE + wave * WAVE_ROWS + (p >> 4);
-      const bool qin = qx < W && qy < H;
-      const size_t qpix = qin ? (size_t)qy * W + qx : 0;
+    for (int c = 0; c < F; ++c) dLf_own[c] = inside && dL_dfeat ? dL_dfeat[(size_t)c * HW + pix] : 0.f;
+  }
+
+  // Constant matrix operands.  Lane l, k-step s (pixels 32s .. 32s+31) holds
+  // pixels p = 32s + 8(l>>4) + j, j = 0..7 (one row of the strip, p & 15 =
+  // 8((l>>4)&1) + j, p >> 4 = 2s + (l>>5)):
+  //   Xw: row l&15 of the colour block: 0..2 dL/dC, 3 dL/dD, 4.. dL/dF (F < 16)
+  //   Bf: dL/dF[p][16cb + (l&15)] (F >= 16; B operand of the feature blocks)
+  bf16x8 Xwh[2], Xwl[2];
+  bf16x8 Bfh[CB1][2], Bfl[CB1][2];
+  const int qy0 = ty * TILE + wave * WAVE_ROWS + (lane >> 5);
+  const int qx0 = tx * TILE + 8 * ((lane >> 4) & 1);
+  {
+    const int row = lane & 15;
+    const float* src = nullptr;
+    if (row < 3) src = dL_dpix ? dL_dpix + (size_t)row * HW : nullptr;
+    else if (row == 3) src = dL_ddepth;
+    else if (row - 4 < FW) src = dL_dfeat ? dL_dfeat + (size_t)(row - 4) * HW : nullptr;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int qy = qy0 + 2 * s;
+      float xw[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int qx = qx0 + j;
+        const bool qin = qx < W && qy < H;
+        xw[j] = (src && qin) ? src[(size_t)qy * W + qx] : 0.f;
+      }
+      split_bf16(xw, Xwh[s], Xwl[s]);
 #pragma unroll
       for (int cb = 0; cb < CB; ++cb) {
-#ifdef GS_EXP_BWD_NO_DLF
-        Bs[cb][s] = (float)cb;
+        const float* fsrc = dL_dfeat ? dL_dfeat + (size_t)(16 * cb + row) * HW : nullptr;
+        float xf[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int qx = qx0 + j;
+          const bool qin = qx < W && qy < H;
+          xf[j] = (fsrc && qin) ? fsrc[(size_t)qy * W + qx] : 0.f;
+        }
+        split_bf16(xf, Bfh[cb][s], Bfl[cb][s]);
+      }
+    }
+  }
+
+  // Contract the batch's nb slots and commit their sums (one atomic per
+  // (Gaussian, component); slots >= nb hold stale weights whose results are
+  // dropped -- the matrix rows are independent).
+  auto flush = [&](int nb) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int g = lane & 15;
+    bf16x8 Wh[2], Wl[2], Uh[2], Ul[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int p0 = 32 * s + 8 * (lane >> 4);
+      float x[8], y[8];
+      const float4 a0 = *reinterpret_cast<const float4*>(&s_w[lw][g][p0]);
+      const float4 a1 = *reinterpret_cast<const float4*>(&s_w[lw][g][p0 + 4]);
+      const float4 b0 = *reinterpret_cast<const float4*>(&s_u[lw][g][p0]);
+      const float4 b1 = *reinterpret_cast<const float4*>(&s_u[lw][g][p0 + 4]);
+      x[0] = a0.x; x[1] = a0.y; x[2] = a0.z; x[3] = a0.w; x[4] = a1.x; x[5] = a1.y; x[6] = a1.z; x[7] = a1.w;
+      y[0] = b0.x; y[1] = b0.y; y[2] = b0.z; y[3] = b0.w; y[4] = b1.x; y[5] = b1.y; y[6] = b1.z; y[7] = b1.w;
+      split_bf16(x, Wh[s], Wl[s]);
+      split_bf16(y, Uh[s], Ul[s]);
+    }
+    // colour / depth (/ small features): C[row][slot] = sum_p Xw[row][p] w[slot][p]
+    float4_t cw = float4_t{0.f, 0.f, 0.f, 0.f};
+    float4_t cu = float4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      // geometry rows: the monomials 1, X, Y, X^2, XY, Y^2 of the lane's
+      // pixels (X = 2 (px - cx) = 2 (8((l>>4)&1) + j) - 15, Y = 2 (2s + (l>>5)) - 3)
+      bf16x8 xu;
+      {
+        // recomputed at every flush (an opaque copy of the lane index keeps
+        // the compiler from hoisting them into 8 loop-long registers):
+        // row value = a + X (b + c X) with (a, b, c) = (1,0,0), (0,1,0),
+        // (Y,0,0), (0,0,1), (0,Y,0), (Y^2,0,0) for rows 0..5, else 0
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const int row = ln & 15;
+        const float Y = (float)(4 * s + 2 * (ln >> 5) - 3);
+        const float ca = row == 0 ? 1.f : row == 2 ? Y : row == 5 ? Y * Y : 0.f;
+        const float cb = row == 1 ? 1.f : row == 4 ? Y : 0.f;
+        const float cc = row == 3 ? 1.f : 0.f;
+        const float X0 = (float)(16 * ((ln >> 4) & 1) - 15);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float X = X0 + (float)(2 * j);
+          xu[j] = (__bf16)fmaf(X, fmaf(cc, X, cb), ca);
+        }
+      }
+      cw = mfma3(Xwh[s], Xwl[s], Wh[s], Wl[s], cw);
+      cu = mfma_bf16(xu, Uh[s], cu);
+      cu = mfma_bf16(xu, Ul[s], cu);
+    }
+    // lane l < 16 holds rows 0..3 of slot l; rows 4, 5 of cu come from lane l + 16
+    const float s_xy = __shfl_down(cu[0], 16, 64);
+    const float s_yy = __shfl_down(cu[1], 16, 64);
+    // lanes 0..15 turn slot l's sums into its 10 accumulator components and
+    // park them as [slot][component] in the batch's (consumed) u rows, so
+    // that each atomic wave-instruction below adds whole 40-B component
+    // records (~7 cache lines) instead of one component of 16 Gaussians.
+    float* s_out = &s_u[lw][0][0];
+    if (lane < 16) {
+      const float4 sl = s_slot[lw][lane];
+      const float mx = sl.x, my = sl.y, op = sl.z;
+      const float S1 = cu[0], Sx = cu[1], Sy = cu[2], Sxx = cu[3];
+      // sum u dx = m' S1 - Sx/2, sum u dx^2 = m'^2 S1 - m' Sx + Sxx/4, ...
+      const float ux = fmaf(mx, S1, -0.5f * Sx), uy = fmaf(my, S1, -0.5f * Sy);
+      const float uxx = fmaf(mx, fmaf(mx, S1, -Sx), 0.25f * Sxx);
+      const float uyy = fmaf(my, fmaf(my, S1, -Sy), 0.25f * s_yy);
+      const float uxy = fmaf(mx, fmaf(my, S1, -0.5f * Sy), fmaf(-0.5f * my, Sx, 0.25f * s_xy));
+      float* o = s_out + A_FEAT * lane;
+      o[A_MX] = op * ux;
+      o[A_MY] = op * uy;
+      o[A_CA] = op * uxx;
+      o[A_CB] = op * uxy;
+      o[A_CC] = op * uyy;
+      o[A_OP] = S1;
+      o[A_R] = cw[0];
+      o[A_G] = cw[1];
+      o[A_B] = cw[2];
+      o[A_DEPTH] = cw[3];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int i = lane; i < WB * A_FEAT; i += 64) {
+      const int slot = i / A_FEAT;
+#ifdef GS_EXP_NO_ACC_ATOMIC
+      if (slot < nb && s_out[i] == 12345.f) acc[(size_t)A_FEAT * f_bits(s_slot[lw][slot].w) + (i - A_FEAT * slot)] = 0.f;
 #else
-        Bs[cb][s] = qin && dL_dfeat ? dL_dfeat[(size_t)(cb * 16 + (lane & 15)) * HW + qpix] : 0.f;
+      if (slot < nb) atomicAdd(acc + (size_t)A_FEAT * f_bits(s_slot[lw][slot].w) + (i - A_FEAT * slot), s_out[i]);
+#endif
+    }
+    if constexpr (FW > 0) {
+      // rows 4 .. 4+FW of the colour block: lanes 16..47, row (l>>4)*4 + r
+      if (lane >= 16 && g < nb) {
+        const uint32_t gid = f_bits(s_slot[lw][g].w);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int ch = (lane >> 4) * 4 + r - 4;
+          if (ch < FW) atomicAdd(dsem + (size_t)gid * F + ch, cw[r]);
+        }
+      }
+    }
+    // features: C[slot][ch] = sum_p w[slot][p] dL/dF[p][ch]; lane l holds
+    // channel 16cb + (l&15) of slots (l>>4)*4 + r
+#pragma unroll
+    for (int cb = 0; cb < CB; ++cb) {
+      float4_t cf = float4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) cf = mfma3(Wh[s], Wl[s], Bfh[cb][s], Bfl[cb][s], cf);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int slot = (lane >> 4) * 4 + r;
+#ifdef GS_EXP_NO_FEAT_ATOMIC
+        if (slot < nb && cf[r] == 12345.f) dsem[(size_t)f_bits(s_slot[lw][slot].w) * F + 16 * cb + g] = 0.f;
+#else
+        if (slot < nb) atomicAdd(dsem + (size_t)f_bits(s_slot[lw][slot].w) * F + 16 * cb + g, cf[r]);
 #endif
       }
     }
-    if constexpr (FIXED_FEAT) {
-#pragma unroll
-      for (int c = 0; c < F; ++c) dLf_own[c] = inside && dL_dfeat ? dL_dfeat[(size_t)c * HW + pix] : 0.f;
-    }
-  } else {
-#pragma unroll
-    for (int c = 0; c < NF_REG; ++c) dLf[c] = (F > 0 && inside && dL_dfeat) ? dL_dfeat[c * HW + pix] : 0.f;
-  }
+  };
 
   // The reference carries per-channel "accum_rec" recurrences
   // (CR/backward.cu:560-615): for every channel k with colour c_k and upstream
@@ -497,7 +648,7 @@ __global__ __launch_bounds__(256) void render_bwd_kernel(
   //   Q <- Q + la*(last_cdot - Q),   dL/dalpha = cdot - Q  -- the same value
   // with fewer operations (fp32 reassociation only).
   float Q = 0.f, lcd = 0.f, la = 0.f;
-  int nb = 0;  // MFMA batch fill
+  int nb = 0;  // batch fill
 
   const uint32_t wmax = __builtin_amdgcn_readfirstlane(wave_max_u(last));
   const uint32_t top = range.x + wmax;  // exclusive end of this wave's walk
@@ -512,10 +663,12 @@ __global__ __launch_bounds__(256) void render_bwd_kernel(
   for (uint32_t hi = top; hi > range.x;) {
     const uint32_t c0 = hi > range.x + CHUNK ? hi - CHUNK : range.x;
     const bool keep = (c0 + lane < hi) && !strip_culled(q, sx0, sx1, sy0, sy1);
-    s_rec[wave][lane][0] = q.q0;
-    s_rec[wave][lane][1] = q.q1;
-    s_rec[wave][lane][2] = q.q2;
-    s_rec[wave][lane][3] = half_conic(q.q0, q.q1);
+    {
+      const float4 h = half_conic(q.q0, q.q1);
+      s_rec[lw][lane][0] = make_float4(q.q0.x, q.q0.y, h.x, h.y);
+      s_rec[lw][lane][1] = make_float4(h.z, q.q1.y, q.q1.z, q.q1.w);
+      s_rec[lw][lane][2] = make_float4(q.q2.x, q.q2.y, 0.f, 0.f);
+    }
     const uint32_t chunk_gid = q.gid;  // lane j: id of the chunk's j-th record
     uint64_t mask = __ballot(keep);
     STAT(8, 1);
@@ -529,12 +682,12 @@ __global__ __launch_bounds__(256) void render_bwd_kernel(
       const int j = 63 - __builtin_clzll(mask);
       mask &= ~(1ull << j);
       const uint32_t k = c0 + j - range.x;  // position in the tile list
-      const float4 r0 = s_rec[wave][j][0];
-      const float4 r1 = s_rec[wave][j][1];
-      const float4 r2 = s_rec[wave][j][2];
+      const float4 r0 = s_rec[lw][j][0];
+      const float4 r1 = s_rec[lw][j][1];
+      const float4 r2 = s_rec[lw][j][2];
       const float dx = r0.x - pfx, dy = r0.y - pfy;
       const float op = r1.y;
-      const float power = gauss_power(dx, dy, s_rec[wave][j][3]);
+      const float power = gauss_power(dx, dy, make_float4(r0.z, r0.w, r1.x, 0.f));
       const float G = fast_exp(power);
       const float alpha = fminf(0.99f, op * G);
       const bool valid = (k < last) && !(power > 0.0f) && !(alpha < ALPHA_MIN);
@@ -543,82 +696,48 @@ __global__ __launch_bounds__(256) void render_bwd_kernel(
       STAT(12, wave_any(valid));
       STAT(13, __builtin_popcountll(__ballot(valid)));
       if (!wave_any(valid)) continue;
-      const uint32_t gid = __builtin_amdgcn_readlane(chunk_gid, j);
-      // Invalid lanes keep dch = dL_dopa = Gv = 0, which zeroes every
-      // contribution below without per-component selects.
-      float dch = 0.f, dL_dopa = 0.f, Gv = 0.f;
+      // Invalid lanes park w = u = 0, which zeroes their contributions.
+      float w = 0.f, u = 0.f;
       if (valid) {
         const float rinv = fast_rcp(1.f - alpha);
         T = T * rinv;
-        dch = alpha * T;
+        w = alpha * T;
         float cdot = fmaf(r2.y, dLd, fmaf(r2.x, dLp[2], fmaf(r1.w, dLp[1], r1.z * dLp[0]))) + dLa;
         if constexpr (FIXED_FEAT) {
           // fixed mode: the features feed dL/dalpha (Q5 fixed)
+          const uint32_t gid = __builtin_amdgcn_readlane(chunk_gid, j);
           const float* f = feats + (size_t)gid * F;
           float fd = 0.f;
-          if constexpr (MF) {
 #pragma unroll
-            for (int c = 0; c < F; ++c) fd = fmaf(f[c], dLf_own[c], fd);
-          } else {
-#pragma unroll
-            for (int c = 0; c < NF_REG; ++c) fd = fmaf(f[c], dLf[c], fd);
-          }
+          for (int c = 0; c < F; ++c) fd = fmaf(f[c], dLf_own[c], fd);
           cdot += fd;
         }
         Q = fmaf(la, lcd - Q, Q);
-        dL_dopa = fmaf(-T_final * rinv, bg_dot, (cdot - Q) * T);
+        const float dL_dopa = fmaf(-T_final * rinv, bg_dot, (cdot - Q) * T);
         lcd = cdot;
         la = alpha;
-        Gv = G;
+        u = G * dL_dopa;
       }
-      float v[NV];
-      v[A_R] = dch * dLp[0];
-      v[A_G] = dch * dLp[1];
-      v[A_B] = dch * dLp[2];
-      v[A_DEPTH] = dch * dLd;
-      if constexpr (!MF) {
-#pragma unroll
-        for (int c = 0; c < NF_REG; ++c) if (A_FEAT + c < NV) v[A_FEAT + c] = dch * dLf[c];
-      }
-      // dL/dG -> mean2D and conic (CR/backward.cu:616-630).  Those are linear
-      // in e = dL/dG * G times dx, dy, dx^2, dx dy, dy^2 with per-Gaussian
-      // factors (conic, -1/2, ndc scale), so the wave sums only the five
-      // basis terms; preprocess_bwd applies the factors once per Gaussian.
-      const float e = (op * dL_dopa) * Gv;
-      const float ex = e * dx, ey = e * dy;
-      v[A_MX] = ex;
-      v[A_MY] = ey;
-      v[A_CA] = ex * dx;
-      v[A_CB] = ex * dy;
-      v[A_CC] = ey * dy;
-      v[A_OP] = Gv * dL_dopa;
-      commit<NV>(v, acc + (size_t)A_FEAT * gid, dsem + (size_t)F * gid, lane);
-      if constexpr (MF) {
-        s_w[wave][nb][lane] = dch;
-        if (lane == 0) s_bgid[wave][nb] = gid;
-        if (++nb == WB) {
-#ifndef GS_EXP_BWD_NO_MFMA
-          flush_feature_batch<F, WB>(s_w[wave], s_bgid[wave], Bs, dsem, lane, WB);
-#endif
-          nb = 0;
-        }
+      s_w[lw][nb][lane] = w;
+      s_u[lw][nb][lane] = u;
+      if (lane == 0)
+        s_slot[lw][nb] = make_float4(r0.x - cx, r0.y - cy, op, bits_f(__builtin_amdgcn_readlane(chunk_gid, j)));
+      if (++nb == WB) {
+        flush(WB);
+        nb = 0;
       }
     }
     hi = c0;
   }
   STAT_WAVE(17, 25, st_it);
-  if constexpr (MF) {
-    // rows >= nb hold stale weights; MFMA rows are independent, so they only
-    // produce results that are not committed
-    if (nb > 0) flush_feature_batch<F, WB>(s_w[wave], s_bgid[wave], Bs, dsem, lane, nb);
-  }
+  if (nb > 0) flush(nb);
 }
 
 // ------------------------------------------------------------------ dispatch
 
 template <int F>
 static void fwd_f(const RenderArgs& a, hipStream_t s) {
-  dim3 grid(a.num_tiles), block(256);
+  dim3 grid(a.num_tiles * (4 / GS_WPB_FWD)), block(64 * GS_WPB_FWD);
 #ifdef GS_EXP_FWD_LDS_PAD
   const size_t pad = GS_EXP_FWD_LDS_PAD;  // occupancy experiment: unused dynamic LDS
 #else
@@ -636,7 +755,7 @@ static void fwd_f(const RenderArgs& a, hipStream_t s) {
 
 template <int F>
 static void bwd_f(const RenderBwdArgs& a, hipStream_t s) {
-  dim3 grid(a.num_tiles), block(256);
+  dim3 grid(a.num_tiles * (4 / GS_WPB_BWD)), block(64 * GS_WPB_BWD);
   if (a.compat == COMPAT_REFERENCE)
     hipLaunchKernelGGL((render_bwd_kernel<F, COMPAT_REFERENCE>), grid, block, 0, s, a.W, a.H, a.grid_x,
                        a.num_tiles, a.ranges, a.point_list, a.rec, a.feats, a.bg, a.alphas, a.n_contrib,
