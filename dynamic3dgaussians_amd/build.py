@@ -37,7 +37,7 @@ VARIANT_FLAGS = {"": [], "stats": ["-DGS_STATS"],
                  "exp_fwd_noload": ["-DGS_EXP_FWD_NO_FEAT_LOAD"], "exp_fwd_nomfma": ["-DGS_EXP_FWD_NO_MFMA"],
                  "exp_occ5": ["-DGS_EXP_FWD_LDS_PAD=18000"], "exp_occ3": ["-DGS_EXP_FWD_LDS_PAD=40000"],
                  "exp_fwd_valu": ["-DGS_EXP_FWD_VALU_FEAT"],
-                 "exp_wg1": ["-DGS_WPB_FWD=1"], "exp_wg4": ["-DGS_WPB_BWD=4"], "exp_bwd_wpe3": ["-DGS_BWD_WPE=3"],  "exp_fwd_wpe5": ["-DGS_FWD_WPE=5"], "exp_fwd_wpe6": ["-DGS_FWD_WPE=6"]}
+                 "exp_wg1": ["-DGS_WPB_FWD=1"], "exp_tilegroup": ["-DGS_XCD_TILE_GROUP"], "exp_acc10": ["-DGS_ACC_STRIDE=10"], "exp_wg4": ["-DGS_WPB_BWD=4"], "exp_bwd_wpe3": ["-DGS_BWD_WPE=3"],  "exp_fwd_wpe5": ["-DGS_FWD_WPE=5"], "exp_fwd_wpe6": ["-DGS_FWD_WPE=6"]}
 ARCH = os.environ.get("GSPLAT_OFFLOAD_ARCH", "gfx950")
 
 # Per-file flags.  The preprocess kernels are compiled without FMA

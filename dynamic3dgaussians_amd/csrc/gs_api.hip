@@ -192,7 +192,7 @@ size_t gs_binning_buffer_bytes(int64_t L) { return BinLayout(L > 0 ? L : 0).tota
 size_t gs_image_buffer_bytes(int32_t W, int32_t H) { return ImgLayout(W, H).total; }
 size_t gs_backward_scratch_bytes(int64_t P, int32_t F) {
   (void)F;
-  return align_up(sizeof(float) * (size_t)A_FEAT * (size_t)(P > 0 ? P : 0), 256) + 256;
+  return align_up(sizeof(float) * (size_t)ACC_STRIDE * (size_t)(P > 0 ? P : 0), 256) + 256;
 }
 
 int gs_forward_plan(const gs_gaussians* g, const gs_camera* cam, int prefiltered, int debug, int compat,
@@ -331,7 +331,7 @@ int gs_backward(const gs_gaussians* g, const gs_camera* cam, const int32_t* radi
   const BinLayout bl(L);
   const ImgLayout il(W, H);
   float* acc = static_cast<float*>(scratch);
-  (void)hipMemsetAsync(acc, 0, sizeof(float) * (size_t)A_FEAT * P, s);
+  (void)hipMemsetAsync(acc, 0, sizeof(float) * (size_t)ACC_STRIDE * P, s);
   if (g->F > 0) (void)hipMemsetAsync(dL_dsemantic, 0, sizeof(float) * (size_t)g->F * P, s);
   RenderBwdArgs ra{};
   ra.W = W; ra.H = H; ra.grid_x = gx; ra.num_tiles = gx * gy; ra.F = g->F; ra.compat = compat;

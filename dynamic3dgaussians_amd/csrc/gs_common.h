@@ -38,6 +38,13 @@ enum AccField {
   A_MX = 0, A_MY = 1, A_CA = 2, A_CB = 3, A_CC = 4, A_OP = 5,
   A_R = 6, A_G = 7, A_B = 8, A_DEPTH = 9, A_FEAT = 10,
 };
+// A Gaussian's accumulation record occupies one aligned 64-B segment: float
+// atomics execute at the memory side per 64-B segment, so a record that
+// straddles two segments costs two requests per commit.
+#ifndef GS_ACC_STRIDE
+#define GS_ACC_STRIDE 16
+#endif
+constexpr int ACC_STRIDE = GS_ACC_STRIDE;
 
 constexpr int COMPAT_REFERENCE = 0;
 constexpr int COMPAT_FIXED = 1;
@@ -155,14 +162,32 @@ __device__ inline bool rect_culled(float mx, float my, float a, float b, float c
   return m > tq;  // NaN keeps the Gaussian
 }
 
-// XCD-aware block -> work-item remap (bijective for any n).  Consecutive
-// work items land on the same XCD (shared L2) instead of being dealt
-// round-robin over the 8 XCDs (cdna_hip_programming.md T1).
-__device__ inline int xcd_remap(int bid, int n) {
-  const int q = n / 8, r = n % 8;
-  const int xcd = bid % 8, slot = bid / 8;
-  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
-  return base + slot;
+// Block -> strip-item map of the blend kernels (item = tile * 4 + strip).
+//
+// Workgroups are dealt round-robin to the 8 XCDs (blockIdx % 8).  The
+// contiguous remap of cdna_hip_programming.md T1 (consecutive items on one
+// XCD) was measured SLOWER here (bench camera, F = 32: fwd 199 vs 182 us,
+// bwd 292 vs 274 us): it hands each XCD a horizontal band of the image, and
+// the bands through the scene centre carry most of the blend work, so the
+// XCDs owning them finish last.  Plain dispatch order interleaves tiles over
+// the XCDs (tile % 8 with a tile per workgroup) and balances the load.
+//
+// GS_XCD_TILE_GROUP (experiment): keep a tile's 4 strip workgroups on one XCD
+// (one L2 fill of the tile's records instead of up to 4) while tiles stay
+// interleaved over the XCDs.  Bijective: the tail (tiles past the last full
+// group of 8) keeps plain order.
+__device__ inline int strip_item(int bid, int num_tiles, int wpb) {
+#ifdef GS_XCD_TILE_GROUP
+  if (wpb == 1) {
+    const int full = (num_tiles / 8) * 8;
+    if (bid < full * 4) {
+      const int xcd = bid % 8, slot = bid / 8;
+      return ((slot / 4) * 8 + xcd) * 4 + (slot % 4);
+    }
+  }
+#endif
+  (void)num_tiles;
+  return bid * wpb;
 }
 
 __device__ inline float bits_f(uint32_t u) { return __uint_as_float(u); }

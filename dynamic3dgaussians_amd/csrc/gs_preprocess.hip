@@ -375,7 +375,7 @@ __device__ inline void cov3d_bwd(V3 scale, float mod, float4 rot, const float d[
 __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdArgs a) {
   const int g = blockIdx.x * 256 + threadIdx.x;
   if (g >= a.P) return;
-  const float* acc = a.acc + (size_t)A_FEAT * g;
+  const float* acc = a.acc + (size_t)ACC_STRIDE * g;
   const bool vis = a.radii[g] > 0;
   // blend gradients -> output tensors (zero for culled Gaussians: never touched)
   // dL/dmean2D = sum over pixels of dL/dG * dG/d(offset) * ndc scale

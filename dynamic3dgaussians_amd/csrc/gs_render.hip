@@ -183,14 +183,10 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) GS_FWD_ATTR void render_fwd_kernel
   // per record: (x, y, -a/2, -b) (-c/2, opacity, r, g) (b, depth, -, -)
   __shared__ float4 s_rec[GS_WPB_FWD][CHUNK][3];
 
-  // strip item = tile * 4 + wave; consecutive items share an XCD (and its L2)
+  // strip item = tile * 4 + wave (dispatch order, see strip_item)
   const int lane = threadIdx.x & 63, lw = threadIdx.x >> 6;  // lw: LDS slot of the wave
-#if GS_WPB_FWD == 4
-  const int tile = xcd_remap(blockIdx.x, num_tiles), wave = lw;
-#else
-  const int item = xcd_remap(blockIdx.x, num_tiles * (4 / GS_WPB_FWD)) * GS_WPB_FWD + lw;
+  const int item = strip_item(blockIdx.x, num_tiles, GS_WPB_FWD) + lw;
   const int tile = item >> 2, wave = item & 3;
-#endif
   const int tx = tile % grid_x, ty = tile / grid_x;
   const int px = tx * TILE + (lane & 15), py = ty * TILE + wave * WAVE_ROWS + (lane >> 4);
   const bool inside = px < W && py < H;
@@ -443,9 +439,9 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
   __shared__ float s_u[GS_WPB_BWD][WB][68];
   __shared__ float4 s_slot[GS_WPB_BWD][WB];  // (mean x - cx, mean y - cy, opacity, id bits)
 
-  // strip item = tile * 4 + wave; consecutive items share an XCD (and its L2)
+  // strip item = tile * 4 + wave (dispatch order, see strip_item)
   const int lane = threadIdx.x & 63, lw = threadIdx.x >> 6;  // lw: LDS slot of the wave
-  const int item = xcd_remap(blockIdx.x, num_tiles * (4 / GS_WPB_BWD)) * GS_WPB_BWD + lw;
+  const int item = strip_item(blockIdx.x, num_tiles, GS_WPB_BWD) + lw;
   const int tile = item >> 2, wave = item & 3;
   const int tx = tile % grid_x, ty = tile / grid_x;
   const int px = tx * TILE + (lane & 15), py = ty * TILE + wave * WAVE_ROWS + (lane >> 4);
@@ -604,9 +600,9 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
     for (int i = lane; i < WB * A_FEAT; i += 64) {
       const int slot = i / A_FEAT;
 #ifdef GS_EXP_NO_ACC_ATOMIC
-      if (slot < nb && s_out[i] == 12345.f) acc[(size_t)A_FEAT * f_bits(s_slot[lw][slot].w) + (i - A_FEAT * slot)] = 0.f;
+      if (slot < nb && s_out[i] == 12345.f) acc[(size_t)ACC_STRIDE * f_bits(s_slot[lw][slot].w) + (i - A_FEAT * slot)] = 0.f;
 #else
-      if (slot < nb) atomicAdd(acc + (size_t)A_FEAT * f_bits(s_slot[lw][slot].w) + (i - A_FEAT * slot), s_out[i]);
+      if (slot < nb) atomicAdd(acc + (size_t)ACC_STRIDE * f_bits(s_slot[lw][slot].w) + (i - A_FEAT * slot), s_out[i]);
 #endif
     }
     if constexpr (FW > 0) {
