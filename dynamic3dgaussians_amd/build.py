@@ -34,9 +34,7 @@ VARIANT_FLAGS = {"": [], "stats": ["-DGS_STATS"],
                  # timing experiments only (results are wrong by construction)
                  "exp_nofeat": ["-DGS_EXP_NO_FEAT_ATOMIC"], "exp_noacc": ["-DGS_EXP_NO_ACC_ATOMIC"],
                  "exp_noatomic": ["-DGS_EXP_NO_FEAT_ATOMIC", "-DGS_EXP_NO_ACC_ATOMIC"],
-                 "exp_fwd_noload": ["-DGS_EXP_FWD_NO_FEAT_LOAD"], "exp_fwd_nomfma": ["-DGS_EXP_FWD_NO_MFMA"],
                  "exp_occ5": ["-DGS_EXP_FWD_LDS_PAD=18000"], "exp_occ3": ["-DGS_EXP_FWD_LDS_PAD=40000"],
-                 "exp_fwd_valu": ["-DGS_EXP_FWD_VALU_FEAT"],
                  "exp_wg1": ["-DGS_WPB_FWD=1"], "exp_tilegroup": ["-DGS_XCD_TILE_GROUP"], "exp_acc10": ["-DGS_ACC_STRIDE=10"], "exp_wg4": ["-DGS_WPB_BWD=4"], "exp_bwd_wpe3": ["-DGS_BWD_WPE=3"],  "exp_fwd_wpe5": ["-DGS_FWD_WPE=5"], "exp_fwd_wpe6": ["-DGS_FWD_WPE=6"]}
 ARCH = os.environ.get("GSPLAT_OFFLOAD_ARCH", "gfx950")
 
@@ -73,6 +71,8 @@ def _deps() -> list[str]:
 def is_stale() -> bool:
     if not os.path.exists(LIB):
         return True
+    if VARIANT not in VARIANT_FLAGS:
+        return False  # a frozen snapshot (e.g. "old" = a previous product build for A/B timing)
     t = os.path.getmtime(LIB)
     return any(os.path.getmtime(f) > t for f in _deps())
 

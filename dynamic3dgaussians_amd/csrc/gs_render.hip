@@ -80,10 +80,6 @@ __device__ inline float fast_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.
 // 1/x as one v_rcp_f32 (1 ulp).
 __device__ inline float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
 
-__device__ inline f32x16 mfma32(float a, float b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
-}
-
 // Swap the upper half of `a` with the lower half of `b`:
 // lo = [a_lo, b_lo], hi = [a_hi, b_hi].
 __device__ inline void swap32(float a, float b, float& lo, float& hi) {
@@ -144,6 +140,9 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 __device__ inline float4_t mfma_bf16(const bf16x8& a, const bf16x8& b, float4_t c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
+__device__ inline f32x16 mfma32_bf16(const bf16x8& a, const bf16x8& b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
 __device__ inline void split_bf16(const float (&x)[8], bf16x8& hi, bf16x8& lo) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -176,12 +175,19 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) GS_FWD_ATTR void render_fwd_kernel
     uint32_t* __restrict__ n_contrib) {
   // Features: 8 / 16 channels on the VALU (v_pk_fma_f32 with the Gaussian's
   // row in SGPRs, requested at the top of the iteration); 32 / 64 channels on
-  // the matrix cores (measured faster at 32: 223 vs 227 us on the bench scene).
+  // the matrix cores: a wave parks the weights w = alpha T of 16 blending
+  // Gaussians in LDS and contracts the batch as out_feature^T[ch][pix] +=
+  // sum_g feat[g][ch] w[g][pix] (v_mfma_f32_32x32x16_bf16, K = Gaussians,
+  // bf16-split operands: 6 matrix instructions per 16 Gaussians and 32
+  // channels instead of 16 fp32 v_mfma_f32_32x32x2_f32).
   constexpr bool MF = (F == 32 || F == 64);
   constexpr int FB = MF ? F / 32 : 1;        // 32-channel blocks
   constexpr int NSF = (!MF && F > 0) ? F : 1;
+  constexpr int WBF = 16;                    // Gaussians per matrix batch
   // per record: (x, y, -a/2, -b) (-c/2, opacity, r, g) (b, depth, -, -)
   __shared__ float4 s_rec[GS_WPB_FWD][CHUNK][3];
+  // batch weights [slot][pixel] (row pad 4: conflict-free writes and reads)
+  __shared__ float s_fw[GS_WPB_FWD][MF ? WBF : 1][68];
 
   // strip item = tile * 4 + wave (dispatch order, see strip_item)
   const int lane = threadIdx.x & 63, lw = threadIdx.x >> 6;  // lw: LDS slot of the wave
@@ -199,6 +205,7 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) GS_FWD_ATTR void render_fwd_kernel
   float SF[NSF];
 #pragma unroll
   for (int c = 0; c < NSF; ++c) SF[c] = 0.f;
+  // acc[2 fb + blk]: out_feature^T block (channels 32 fb .., strip pixels 32 blk ..)
   f32x16 acc[2 * FB];
 #pragma unroll
   for (int i = 0; i < 2 * FB; ++i) acc[i] = f32x16{0};
@@ -206,30 +213,54 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) GS_FWD_ATTR void render_fwd_kernel
   // lane still blending (the reference's !done); an integer, not a bool, so
   // that it lives in a VGPR instead of exec-mask bookkeeping across the loops
   uint32_t live = inside ? 1u : 0u;
-  // MFMA pairing: a blended Gaussian waits for a partner; a completed pair's
-  // feature rows are loaded one pair ahead of its MFMAs (latency hiding).
-  int pend = 0;
-  uint32_t pend_gid = 0;
-  float pend_w = 0.f;
-  int have_prev = 0;
-  float pa[FB], pb0 = 0.f, pb1 = 0.f;
+  int nb = 0;          // batch fill
+  uint32_t gidv = 0;   // lane k < nb: id of the batch's k-th Gaussian
+
+  // Contract the batch's nb Gaussians.  A[ch][k] = feat[gid_k][32 fb + ch]
+  // (lane l: channel l&31, k = 8(l>>5) + j), B[k][pix] = w[k][pix] (lane l:
+  // pixel (l&31) + 32 blk); slots k >= nb are zeroed on both sides.
+  auto flush = [&](int n) {
+    // an opaque copy of the lane index keeps the compiler from hoisting the
+    // flush's address arithmetic into loop-long registers
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const int h = ln >> 5;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
-  for (int fb = 0; fb < FB; ++fb) pa[fb] = 0.f;
-  auto push_pair = [&](float b0, float b1, const float (&an)[FB]) {
-    if (have_prev) {
-#ifndef GS_EXP_FWD_NO_MFMA
+    for (int fb = 0; fb < FB; ++fb) {
+      bf16x8 Ah, Al;
+      {
+        float fa[8];
 #pragma unroll
-      for (int fb = 0; fb < FB; ++fb) {
-        acc[2 * fb] = mfma32(pa[fb], pb0, acc[2 * fb]);
-        acc[2 * fb + 1] = mfma32(pa[fb], pb1, acc[2 * fb + 1]);
+        for (int j = 0; j < 8; ++j) {
+          const int k = 8 * h + j;
+          const uint32_t g = (uint32_t)__shfl((int)gidv, k, 64);
+          fa[j] = k < n ? feats[(size_t)g * F + fb * 32 + (ln & 31)] : 0.f;
+        }
+        split_bf16(fa, Ah, Al);
       }
-#endif
-    }
 #pragma unroll
-    for (int fb = 0; fb < FB; ++fb) pa[fb] = an[fb];
-    pb0 = b0;
-    pb1 = b1;
-    have_prev = 1;
+      for (int blk = 0; blk < 2; ++blk) {
+        bf16x8 Bh, Bl;
+        {
+          float x[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int k = 8 * h + j;
+            x[j] = k < n ? s_fw[lw][k][(ln & 31) + 32 * blk] : 0.f;
+          }
+          split_bf16(x, Bh, Bl);
+        }
+        acc[2 * fb + blk] = mfma32_bf16(Ah, Bh, acc[2 * fb + blk]);
+        acc[2 * fb + blk] = mfma32_bf16(Ah, Bl, acc[2 * fb + blk]);
+        acc[2 * fb + blk] = mfma32_bf16(Al, Bh, acc[2 * fb + blk]);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   };
 
   const uint32_t lastv = range.y > range.x ? range.y - 1 : range.x;
@@ -296,31 +327,16 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) GS_FWD_ATTR void render_fwd_kernel
         for (int c = 0; c < NSF; ++c) asm volatile("" ::"s"(fcur[c]));
       }
       if (F > 0 && wave_any(blend)) {
-        {
-          const uint32_t gid = __builtin_amdgcn_readlane(chunk_gid, j);
-          if constexpr (MF) {
-            if (pend == 0) {
-              pend = 1;
-              pend_gid = gid;
-              pend_w = w;
-            } else {
-              const uint32_t ga = lane < 32 ? pend_gid : gid;
-              float b0, b1, an[FB];
-              swap32(pend_w, w, b0, b1);
-#pragma unroll
-#ifdef GS_EXP_FWD_NO_FEAT_LOAD
-              for (int fb = 0; fb < FB; ++fb) an[fb] = (float)(ga & 7);
-#else
-              for (int fb = 0; fb < FB; ++fb) an[fb] = feats[(size_t)ga * F + fb * 32 + (lane & 31)];
-#endif
-              push_pair(b0, b1, an);
-              pend = 0;
-            }
-          } else {
-            (void)gid;
-#pragma unroll
-            for (int c = 0; c < NSF; ++c) SF[c] = fmaf(fcur[c], w, SF[c]);
+        if constexpr (MF) {
+          s_fw[lw][nb][lane] = w;  // 0 on non-blending lanes
+          gidv = lane == nb ? __builtin_amdgcn_readlane(chunk_gid, j) : gidv;
+          if (++nb == WBF) {
+            flush(WBF);
+            nb = 0;
           }
+        } else {
+#pragma unroll
+          for (int c = 0; c < NSF; ++c) SF[c] = fmaf(fcur[c], w, SF[c]);
         }
       }
       if (!wave_any(live != 0u)) goto blend_done;
@@ -329,20 +345,7 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) GS_FWD_ATTR void render_fwd_kernel
 blend_done:
   STAT_WAVE(16, 20, st_it);
   if constexpr (MF) {
-    if (pend) {
-      float b0, b1, an[FB];
-      swap32(pend_w, 0.0f, b0, b1);
-#pragma unroll
-      for (int fb = 0; fb < FB; ++fb) an[fb] = lane < 32 ? feats[(size_t)pend_gid * F + fb * 32 + lane] : 0.0f;
-      push_pair(b0, b1, an);
-    }
-    if (have_prev) {
-#pragma unroll
-      for (int fb = 0; fb < FB; ++fb) {
-        acc[2 * fb] = mfma32(pa[fb], pb0, acc[2 * fb]);
-        acc[2 * fb + 1] = mfma32(pa[fb], pb1, acc[2 * fb + 1]);
-      }
-    }
+    if (nb > 0) flush(nb);
   }
   const size_t HW = (size_t)H * W;
   if (inside) {
