@@ -9,11 +9,23 @@ namespace gs {
 
 // Binning tile = 16x16 pixels, identical to the reference (CR/config.h:18-19)
 // so that tiles_touched / num_rendered / sort keys agree with it.  Inside a
-// tile the blend kernels use 4 waves of 16x4 pixels each.
+// tile the blend kernels use 4 waves of 64 pixels each ("strips").
 constexpr int TILE = 16;
 constexpr int TILE_PIX = TILE * TILE;
 constexpr int WAVE = 64;
-constexpr int WAVE_ROWS = 4;  // a wave covers 16 x 4 pixels of its tile
+// Strip shape: 8 x 8 (default) or 16 x 4 (-DGS_STRIP_16X4).  A square strip
+// has the shortest perimeter, so fewer Gaussians reach it: on the bench
+// camera 3.43 M (Gaussian, strip) survivors at 8 x 8 vs 3.81 M at 16 x 4 for
+// the same 115 M blended (Gaussian, pixel) pairs (tools/strip_survey.py).
+#ifdef GS_STRIP_16X4
+constexpr int STRIP_W = 16, STRIP_H = 4;
+#else
+constexpr int STRIP_W = 8, STRIP_H = 8;
+#endif
+constexpr int STRIPS_X = TILE / STRIP_W;  // strips per tile row
+// top-left pixel of strip `s` (0..3) of tile (tx, ty)
+__host__ __device__ inline int strip_x0(int tx, int s) { return tx * TILE + (s % STRIPS_X) * STRIP_W; }
+__host__ __device__ inline int strip_y0(int ty, int s) { return ty * TILE + (s / STRIPS_X) * STRIP_H; }
 
 // Per-Gaussian render record written by preprocess: one 64-B line, read by
 // the blend kernels with a single wave-uniform s_load_dwordx16.

@@ -194,11 +194,12 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) GS_FWD_ATTR void render_fwd_kernel
   const int item = strip_item(blockIdx.x, num_tiles, GS_WPB_FWD) + lw;
   const int tile = item >> 2, wave = item & 3;
   const int tx = tile % grid_x, ty = tile / grid_x;
-  const int px = tx * TILE + (lane & 15), py = ty * TILE + wave * WAVE_ROWS + (lane >> 4);
+  const int qx0 = strip_x0(tx, wave), qy0 = strip_y0(ty, wave);  // lane = strip pixel (lane % STRIP_W, lane / STRIP_W)
+  const int px = qx0 + lane % STRIP_W, py = qy0 + lane / STRIP_W;
   const bool inside = px < W && py < H;
   const float pfx = (float)px, pfy = (float)py;
-  const float sx0 = (float)(tx * TILE), sx1 = sx0 + 15.0f;
-  const float sy0 = (float)(ty * TILE + wave * WAVE_ROWS), sy1 = sy0 + 3.0f;
+  const float sx0 = (float)qx0, sx1 = sx0 + (float)(STRIP_W - 1);
+  const float sy0 = (float)qy0, sy1 = sy0 + (float)(STRIP_H - 1);
   const uint2 range = ranges[tile];
 
   float T = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f, Dp = 0.f;
@@ -224,7 +225,7 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) GS_FWD_ATTR void render_fwd_kernel
     // flush's address arithmetic into loop-long registers
     int ln = lane;
     asm volatile("" : "+v"(ln));
-    const int h = ln >> 5;
+    const int h = (ln >> 5) & 1;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -377,7 +378,7 @@ blend_done:
 #pragma unroll
     for (int blk = 0; blk < 2; ++blk) {
       const int p = (lane & 31) + 32 * blk;
-      const int qx = tx * TILE + (p & 15), qy = ty * TILE + wave * WAVE_ROWS + (p >> 4);
+      const int qx = qx0 + p % STRIP_W, qy = qy0 + p / STRIP_W;
       if (qx < W && qy < H) {
         const size_t pix = (size_t)qy * W + qx;
         const float Tp = blk ? t_hi : t_lo;
@@ -447,12 +448,13 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
   const int item = strip_item(blockIdx.x, num_tiles, GS_WPB_BWD) + lw;
   const int tile = item >> 2, wave = item & 3;
   const int tx = tile % grid_x, ty = tile / grid_x;
-  const int px = tx * TILE + (lane & 15), py = ty * TILE + wave * WAVE_ROWS + (lane >> 4);
+  const int qx0 = strip_x0(tx, wave), qy0 = strip_y0(ty, wave);  // lane = strip pixel (lane % STRIP_W, lane / STRIP_W)
+  const int px = qx0 + lane % STRIP_W, py = qy0 + lane / STRIP_W;
   const bool inside = px < W && py < H;
   const float pfx = (float)px, pfy = (float)py;
-  const float sx0 = (float)(tx * TILE), sx1 = sx0 + 15.0f;
-  const float sy0 = (float)(ty * TILE + wave * WAVE_ROWS), sy1 = sy0 + 3.0f;
-  const float cx = sx0 + 7.5f, cy = sy0 + 1.5f;  // strip centre
+  const float sx0 = (float)qx0, sx1 = sx0 + (float)(STRIP_W - 1);
+  const float sy0 = (float)qy0, sy1 = sy0 + (float)(STRIP_H - 1);
+  const float cx = sx0 + 0.5f * (STRIP_W - 1), cy = sy0 + 0.5f * (STRIP_H - 1);  // strip centre
   const uint2 range = ranges[tile];
   const size_t HW = (size_t)H * W, pix = inside ? (size_t)py * W + px : 0;
 
@@ -474,14 +476,13 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
   }
 
   // Constant matrix operands.  Lane l, k-step s (pixels 32s .. 32s+31) holds
-  // pixels p = 32s + 8(l>>4) + j, j = 0..7 (one row of the strip, p & 15 =
-  // 8((l>>4)&1) + j, p >> 4 = 2s + (l>>5)):
+  // strip pixels p = 32s + 8(l>>4) + j, j = 0..7 (8 consecutive pixels of one
+  // strip row: column p % STRIP_W, row p / STRIP_W):
   //   Xw: row l&15 of the colour block: 0..2 dL/dC, 3 dL/dD, 4.. dL/dF (F < 16)
   //   Bf: dL/dF[p][16cb + (l&15)] (F >= 16; B operand of the feature blocks)
   bf16x8 Xwh[2], Xwl[2];
   bf16x8 Bfh[CB1][2], Bfl[CB1][2];
-  const int qy0 = ty * TILE + wave * WAVE_ROWS + (lane >> 5);
-  const int qx0 = tx * TILE + 8 * ((lane >> 4) & 1);
+  const int kp0 = 8 * (lane >> 4);  // first strip pixel of the lane at k-step 0
   {
     const int row = lane & 15;
     const float* src = nullptr;
@@ -490,11 +491,12 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
     else if (row - 4 < FW) src = dL_dfeat ? dL_dfeat + (size_t)(row - 4) * HW : nullptr;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      const int qy = qy0 + 2 * s;
+      const int p8 = 32 * s + kp0;
+      const int qy = qy0 + p8 / STRIP_W;
       float xw[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int qx = qx0 + j;
+        const int qx = qx0 + p8 % STRIP_W + j;
         const bool qin = qx < W && qy < H;
         xw[j] = (src && qin) ? src[(size_t)qy * W + qx] : 0.f;
       }
@@ -505,7 +507,7 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
         float xf[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const int qx = qx0 + j;
+          const int qx = qx0 + p8 % STRIP_W + j;
           const bool qin = qx < W && qy < H;
           xf[j] = (fsrc && qin) ? fsrc[(size_t)qy * W + qx] : 0.f;
         }
@@ -542,7 +544,8 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       // geometry rows: the monomials 1, X, Y, X^2, XY, Y^2 of the lane's
-      // pixels (X = 2 (px - cx) = 2 (8((l>>4)&1) + j) - 15, Y = 2 (2s + (l>>5)) - 3)
+      // pixels (X = 2 (px - cx) = 2 col - (STRIP_W - 1), Y = 2 row - (STRIP_H - 1)
+      // for strip pixel p = 32s + 8(l>>4) + j)
       bf16x8 xu;
       {
         // recomputed at every flush (an opaque copy of the lane index keeps
@@ -552,11 +555,12 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
         int ln = lane;
         asm volatile("" : "+v"(ln));
         const int row = ln & 15;
-        const float Y = (float)(4 * s + 2 * (ln >> 5) - 3);
+        const int p8 = 32 * s + 8 * ((ln >> 4) & 3);
+        const float Y = (float)(2 * (p8 / STRIP_W) - (STRIP_H - 1));
         const float ca = row == 0 ? 1.f : row == 2 ? Y : row == 5 ? Y * Y : 0.f;
         const float cb = row == 1 ? 1.f : row == 4 ? Y : 0.f;
         const float cc = row == 3 ? 1.f : 0.f;
-        const float X0 = (float)(16 * ((ln >> 4) & 1) - 15);
+        const float X0 = (float)(2 * (p8 % STRIP_W) - (STRIP_W - 1));
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float X = X0 + (float)(2 * j);
