@@ -42,7 +42,7 @@ from dynamic3dgaussians_amd.camera import camera_rig  # noqa: E402
 from dynamic3dgaussians_amd.distributed import GradBucket  # noqa: E402
 from dynamic3dgaussians_amd.optim import FusedAdam  # noqa: E402
 from dynamic3dgaussians_amd.rasterizer import (GaussianRasterizationSettings,  # noqa: E402
-                                               GaussianRasterizer)
+                                               GaussianRasterizer, GradientSink)
 from dynamic3dgaussians_amd.scene import make_gaussians  # noqa: E402
 
 METRIC = "rendered Mpix/s fwd+bwd (1/8 GPU) at 300k Gaussians; PSNR vs ref"
@@ -117,7 +117,7 @@ def params2rendervar(params, label):
     return rv
 
 
-def make_settings(cams, dev, compat):
+def make_settings(cams, dev, compat, sink=None):
     out = []
     for c in cams:
         out.append(GaussianRasterizationSettings(
@@ -126,7 +126,7 @@ def make_settings(cams, dev, compat):
             viewmatrix=torch.from_numpy(c.viewmatrix.copy()).to(dev),
             projmatrix=torch.from_numpy(c.projmatrix.copy()).to(dev), sh_degree=0,
             campos=torch.from_numpy(c.campos.copy()).to(dev), prefiltered=False, debug=False,
-            confidence=None, compat=compat))
+            confidence=None, compat=compat, grad_sink=sink))
     return out
 
 
@@ -235,7 +235,13 @@ def main():
 
     rig = camera_rig(args.cams * world, args.width, args.height, seed=args.seed)
     my_cams = rig[rank * args.cams:(rank + 1) * args.cams]
-    settings = make_settings(my_cams, dev, args.compat)
+    # The per-camera gradients of a step are summed inside the backward
+    # kernels (GradientSink: GS_FLAG_ACCUMULATE into per-stream buffers)
+    # instead of autograd adding 7 gradient tensors per camera into the
+    # leaves; GS_BENCH_SINK=0 restores autograd's accumulation.
+    use_sink = os.environ.get("GS_BENCH_SINK", "1") != "0"
+    sink = GradientSink() if use_sink else None
+    settings = make_settings(my_cams, dev, args.compat, sink)
     params, label = make_params(args, dev)
     # the CPU-baseline / PSNR leg renders the initial scene (independent of the
     # optimizer steps taken by warmup and timing)
@@ -289,6 +295,8 @@ def main():
 
     def step():
         opt.zero_grad(set_to_none=False)
+        if sink is not None:
+            sink.reset()
         rv = params2rendervar(params, label)
         # The activations are shared by all cameras of the step: render from
         # detached leaves, let autograd sum the per-camera gradients on them,
@@ -316,8 +324,9 @@ def main():
                 torch.autograd.backward(outs, grads)
         for st in streams:
             main.wait_stream(st)
-        keys = [k for k in leaves if k != "means2D" and leaves[k].grad is not None]
-        torch.autograd.backward([rv[k] for k in keys], [leaves[k].grad for k in keys])
+        summed = sink.gradients() if sink is not None else {k: v.grad for k, v in leaves.items()}
+        keys = [k for k in leaves if k != "means2D" and summed.get(k) is not None]
+        torch.autograd.backward([rv[k] for k in keys], [summed[k] for k in keys])
         bucket.all_reduce()
         opt.step()
 
@@ -380,6 +389,7 @@ def main():
                                f"{W_}x{H_}, F={args.features} semantic channels, colors_precomp; "
                                "fwd+bwd per camera + grad all-reduce + Adam",
                    "optimizer": optim_kind, "streams": n_streams,
+                   "grad_sum": "in-kernel (GradientSink)" if use_sink else "autograd",
                    "gaussians": args.gaussians, "cams_per_rank": args.cams, "width": W_,
                    "height": H_, "feature_channels": args.features, "compat": args.compat,
                    "parallelism": f"camera-sharded dp{world}"},

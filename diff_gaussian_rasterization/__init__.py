@@ -6,7 +6,7 @@ import sys as _sys
 
 from dynamic3dgaussians_amd import _C  # noqa: F401
 from dynamic3dgaussians_amd.rasterizer import (GaussianRasterizationSettings,  # noqa: F401
-                                               GaussianRasterizer, _RasterizeGaussians,
+                                               GaussianRasterizer, GradientSink, _RasterizeGaussians,
                                                cpu_deep_copy_tuple, rasterize_gaussians)
 from dynamic3dgaussians_amd._C import get_default_compat, set_default_compat  # noqa: F401
 

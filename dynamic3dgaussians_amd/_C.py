@@ -111,7 +111,7 @@ class _Inputs:
                            colors_precomp=_ptr(self.colors), semantic_feature=_ptr(self.sem),
                            opacities=_ptr(self.opacity), scales=_ptr(self.scales),
                            rotations=_ptr(self.rotations), cov3D_precomp=_ptr(self.cov3D),
-                           scale_modifier=self.scale_modifier, _pad=0, grad_mask=None)
+                           scale_modifier=self.scale_modifier, flags=0, grad_mask=None)
 
 
 def _camera(dev, background, viewmatrix, projmatrix, campos, c_x, c_y, tan_fovx, tan_fovy, W, H):
@@ -180,12 +180,24 @@ def rasterize_gaussians(background, means3D, colors, semantic_feature, opacity, 
     return (num_rendered, out_color, feature_map, out_depth, out_alpha, radii, geom, binning, img)
 
 
+def _buffer_shapes(P, F, M):
+    return dict(dmeans2D=(P, 3), dcolors=(P, 3), dsem=(P, F), dopacity=(P, 1), dmeans3D=(P, 3),
+                dcov3D=(P, 6), dsh=(P, M, 3), dscales=(P, 3), drot=(P, 4))
+
+
+def backward_buffers(P, F, M, device) -> dict:
+    """Uninitialised gradient outputs of rasterize_gaussians_backward (F = the
+    compiled feature width, M = SH coefficients per Gaussian)."""
+    return {k: torch.empty(*shape, dtype=torch.float32, device=device)
+            for k, shape in _buffer_shapes(P, F, M).items()}
+
+
 def rasterize_gaussians_backward(background, means3D, radii, colors, semantic_feature, scales,
                                  rotations, scale_modifier, cov3D_precomp, viewmatrix, projmatrix,
                                  c_x, c_y, tan_fovx, tan_fovy, dL_dout_color, dL_dout_feature,
                                  dL_dout_depth, dL_dout_alpha, sh, degree, campos, geomBuffer, R,
                                  binningBuffer, imageBuffer, alphas, debug, *, compat=None,
-                                 grad_mask=None):
+                                 grad_mask=None, out=None, accumulate=False):
     """RasterizeGaussiansBackwardCUDA (DGR/rasterize_points.cu:128-225).
 
     Camera scalars are consumed in this positional order, exactly as the
@@ -197,6 +209,12 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, semantic_fe
     optional per-Gaussian [P] mask fused into the kernel, equal to the
     reference wrapper's `grad * label` (__init__.py:159-173) on every returned
     gradient except dL_dmeans2D and dL_dsemantic.
+
+    `out` / `accumulate` (keyword-only, no reference analogue): caller-owned
+    gradient buffers (a dict with the keys of `backward_buffers`) written in
+    place, and with `accumulate=True` ADDED to (GS_FLAG_ACCUMULATE) -- the
+    multi-camera gradient sink (rasterizer.GradientSink).  Accumulating calls
+    into the same buffers must be ordered on one stream.
     """
     L_ = _lib.load()
     cm = _compat_code(compat)
@@ -230,12 +248,18 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, semantic_fe
         if dLf.size(0) < inp.F:
             dLf = torch.cat([dLf, torch.zeros(inp.F - dLf.size(0), H, W, **f32)]).contiguous()
     radii_c = radii.to(device=dev, dtype=torch.int32).contiguous()
-    out = dict(
-        dmeans2D=torch.empty(P, 3, **f32), dcolors=torch.empty(P, 3, **f32),
-        dsem=torch.empty(P, inp.F, **f32), dopacity=torch.empty(P, 1, **f32),
-        dmeans3D=torch.empty(P, 3, **f32), dcov3D=torch.empty(P, 6, **f32),
-        dsh=torch.empty(P, inp.M, 3, **f32), dscales=torch.empty(P, 3, **f32),
-        drot=torch.empty(P, 4, **f32))
+    if out is None:
+        if accumulate:
+            raise ValueError("accumulate=True needs the caller's gradient buffers (out=...)")
+        out = backward_buffers(P, inp.F, inp.M, dev)
+    else:
+        for k, shape in _buffer_shapes(P, inp.F, inp.M).items():
+            t = out[k]
+            if (tuple(t.shape) != shape or t.dtype != torch.float32 or t.device != dev
+                    or not t.is_contiguous()):
+                raise RuntimeError(f"gradient buffer {k} must be a contiguous fp32 {shape} tensor on {dev}")
+        if accumulate:
+            g.flags = _lib.GS_FLAG_ACCUMULATE
     scratch = torch.empty(L_.gs_backward_scratch_bytes(P, inp.F), dtype=torch.uint8, device=dev)
     stream = _stream(dev)
     p = lambda t: t.data_ptr() if (t is not None and t.numel()) else None  # noqa: E731

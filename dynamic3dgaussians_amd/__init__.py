@@ -11,7 +11,7 @@ Layout:
   scene.py        synthetic scenes for tests and the benchmark
   distributed.py  camera-sharded data parallelism with one RCCL all-reduce
 """
-from .rasterizer import (GaussianRasterizationSettings, GaussianRasterizer,  # noqa: F401
+from .rasterizer import (GaussianRasterizationSettings, GaussianRasterizer, GradientSink,  # noqa: F401
                          _RasterizeGaussians, rasterize_gaussians)
 from ._C import set_default_compat, get_default_compat  # noqa: F401
 

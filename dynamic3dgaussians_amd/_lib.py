@@ -16,7 +16,8 @@ _lock = threading.Lock()
 _lib = None
 
 c_void_p = ctypes.c_void_p
-ABI_VERSION = 4  # include/gsplat_hip.h GS_ABI_VERSION
+ABI_VERSION = 5  # include/gsplat_hip.h GS_ABI_VERSION
+GS_FLAG_ACCUMULATE = 1  # include/gsplat_hip.h
 c_int32, c_int64, c_float, c_size_t = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_size_t
 
 GS_COMPAT = {"reference": 0, "fixed": 1}
@@ -28,7 +29,7 @@ class GsGaussians(ctypes.Structure):
                 ("means3D", c_void_p), ("shs", c_void_p), ("colors_precomp", c_void_p),
                 ("semantic_feature", c_void_p), ("opacities", c_void_p), ("scales", c_void_p),
                 ("rotations", c_void_p), ("cov3D_precomp", c_void_p),
-                ("scale_modifier", c_float), ("_pad", c_int32),
+                ("scale_modifier", c_float), ("flags", ctypes.c_uint32),
                 ("grad_mask", c_void_p)]
 
 

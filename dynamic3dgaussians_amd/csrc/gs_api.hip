@@ -332,7 +332,10 @@ int gs_backward(const gs_gaussians* g, const gs_camera* cam, const int32_t* radi
   const ImgLayout il(W, H);
   float* acc = static_cast<float*>(scratch);
   (void)hipMemsetAsync(acc, 0, sizeof(float) * (size_t)ACC_STRIDE * P, s);
-  if (g->F > 0) (void)hipMemsetAsync(dL_dsemantic, 0, sizeof(float) * (size_t)g->F * P, s);
+  const bool accumulate = (g->flags & GS_FLAG_ACCUMULATE) != 0;
+  // the blend kernel adds the feature gradients atomically: zero first unless
+  // the output already holds the sums to add to
+  if (g->F > 0 && !accumulate) (void)hipMemsetAsync(dL_dsemantic, 0, sizeof(float) * (size_t)g->F * P, s);
   RenderBwdArgs ra{};
   ra.W = W; ra.H = H; ra.grid_x = gx; ra.num_tiles = gx * gy; ra.F = g->F; ra.compat = compat;
   ra.ranges = at<uint2>(image, il.ranges);
@@ -351,6 +354,7 @@ int gs_backward(const gs_gaussians* g, const gs_camera* cam, const int32_t* radi
   if (int e = check("render backward", debug, s)) return e;
   PreprocessBwdArgs b{};
   b.P = P; b.D = g->D; b.M = g->M; b.F = g->F; b.W = W; b.H = H; b.compat = compat;
+  b.accumulate = accumulate ? 1 : 0;
   b.means3D = g->means3D; b.radii = radii; b.shs = g->shs; b.clamped = at<uint8_t>(geom, gl.clamped);
   b.scales = g->scales; b.rotations = g->rotations;
   b.cov3D = g->cov3D_precomp ? g->cov3D_precomp : at<float>(geom, gl.cov3D);

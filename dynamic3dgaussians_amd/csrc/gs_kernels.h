@@ -32,6 +32,7 @@ struct PreprocessArgs {
 
 struct PreprocessBwdArgs {
   int P, D, M, F, W, H, compat;
+  int accumulate;  // add into the gradient outputs (GS_FLAG_ACCUMULATE)
   const float* means3D;
   const int* radii;
   const float* shs;
@@ -85,7 +86,7 @@ struct RenderBwdArgs {
   const float* dL_ddepth;
   const float* dL_dalpha;
   float* acc;   // P x 10 blend gradients, zeroed by the caller
-  float* dsem;  // P x F semantic-feature gradients (the output), zeroed by the caller
+  float* dsem;  // P x F semantic-feature gradients (the output), zeroed (or holding earlier sums) by the caller
 };
 
 void launch_preprocess_fwd(const PreprocessArgs& a, hipStream_t s);

@@ -276,9 +276,15 @@ void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t
 // computeColorFromSH backward (backward.cu:20-139): writes dL/dsh (all M
 // coefficients, zero beyond the active degree) and adds the view-direction
 // term to dmean.
+// Gradient store of preprocess_bwd: overwrite, or add to the caller's sums
+// (GS_FLAG_ACCUMULATE).
+__device__ inline void gput(float* p, float v, int accumulate) { *p = accumulate ? *p + v : v; }
+
+// SH backward; dsh is stored as (value * dRGB) * mk -- the reference's
+// `grad * label` rounding (DGR/__init__.py:159-173) -- written or added.
 __device__ inline void sh_bwd(int deg, int M, V3 mean, V3 cp, const float* __restrict__ shs, int g,
                               uint8_t clampbits, const float dcolor[3], float* __restrict__ dsh_out,
-                              float dmean[3]) {
+                              float dmean[3], float mk, int accumulate) {
   const float dox = mean.x - cp.x, doy = mean.y - cp.y, doz = mean.z - cp.z;
   const float len = sqrtf(dox * dox + doy * doy + doz * doz);
   const float x = dox / len, y = doy / len, z = doz / len;
@@ -289,11 +295,12 @@ __device__ inline void sh_bwd(int deg, int M, V3 mean, V3 cp, const float* __res
   for (int ch = 0; ch < 3; ++ch) dRGB[ch] = dcolor[ch] * (((clampbits >> ch) & 1) ? 0.0f : 1.0f);
   float ddx[3] = {0, 0, 0}, ddy[3] = {0, 0, 0}, ddz[3] = {0, 0, 0};
   const int ncoef = (deg + 1) * (deg + 1);
-  for (int i = ncoef; i < M; ++i) { ds[3 * i] = 0.f; ds[3 * i + 1] = 0.f; ds[3 * i + 2] = 0.f; }
+  if (!accumulate)
+    for (int i = ncoef; i < M; ++i) { ds[3 * i] = 0.f * mk; ds[3 * i + 1] = 0.f * mk; ds[3 * i + 2] = 0.f * mk; }
 #pragma unroll
   for (int ch = 0; ch < 3; ++ch) {
 #define S(i) sh[3 * (i) + ch]
-#define WR(i, v) ds[3 * (i) + ch] = (v) * dRGB[ch]
+#define WR(i, v) gput(ds + 3 * (i) + ch, ((v) * dRGB[ch]) * mk, accumulate)
     WR(0, SH_C0);
     if (deg > 0) {
       WR(1, -SH_C1 * y); WR(2, SH_C1 * z); WR(3, -SH_C1 * x);
@@ -390,14 +397,17 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdArgs a
     am0 = (-con.z * sex - con.w * sey) * (0.5f * (float)a.W);
     am1 = (-cc * sey - con.w * sex) * (0.5f * (float)a.H);
   }
-  a.dmeans2D[3 * g] = am0; a.dmeans2D[3 * g + 1] = am1; a.dmeans2D[3 * g + 2] = 0.f;
+  const int ac = a.accumulate;
+  gput(a.dmeans2D + 3 * g, am0, ac); gput(a.dmeans2D + 3 * g + 1, am1, ac);
+  if (!ac) a.dmeans2D[3 * g + 2] = 0.f;
   const float dcol[3] = {acc[A_R], acc[A_G], acc[A_B]};
   // Q12 label mask (DGR/__init__.py:159-173), applied at store time exactly as
   // the reference's elementwise `grad * label` (the chain rule uses unmasked dcol).
   const bool masked = a.grad_mask != nullptr;
   const float mk = masked ? a.grad_mask[g] : 1.f;
-  a.dcolors[3 * g] = dcol[0] * mk; a.dcolors[3 * g + 1] = dcol[1] * mk; a.dcolors[3 * g + 2] = dcol[2] * mk;
-  a.dopacity[g] = acc[A_OP] * mk;
+  gput(a.dcolors + 3 * g, dcol[0] * mk, ac); gput(a.dcolors + 3 * g + 1, dcol[1] * mk, ac);
+  gput(a.dcolors + 3 * g + 2, dcol[2] * mk, ac);
+  gput(a.dopacity + g, acc[A_OP] * mk, ac);
   float dm[3] = {0.f, 0.f, 0.f};
   float dcov[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   float dscale[3] = {0.f, 0.f, 0.f}, drot[4] = {0.f, 0.f, 0.f, 0.f};
@@ -473,28 +483,27 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdArgs a
     dm[0] += (v[2] - v[3] * mul3) * dd;
     dm[1] += (v[6] - v[7] * mul3) * dd;
     dm[2] += (v[10] - v[11] * mul3) * dd;
-    if (a.shs) sh_bwd(a.D, a.M, mean, ld3(a.campos), a.shs, g, a.clamped[g], dcol, a.dsh, dm);
+    if (a.shs) sh_bwd(a.D, a.M, mean, ld3(a.campos), a.shs, g, a.clamped[g], dcol, a.dsh, dm, mk, ac);
     if (a.scales) cov3d_bwd(ld3(a.scales + 3 * g), a.scale_modifier,
                             reinterpret_cast<const float4*>(a.rotations)[g], dcov, dscale, drot);
-  } else if (a.M > 0) {
-    float* ds = a.dsh + (size_t)g * a.M * 3;
-    for (int i = 0; i < 3 * a.M; ++i) ds[i] = 0.f;
   }
-  if (vis && !a.shs && a.M > 0) {
+  if ((!vis || !a.shs) && a.M > 0 && !ac) {  // no SH gradient: zeros (masked like the rest)
     float* ds = a.dsh + (size_t)g * a.M * 3;
-    for (int i = 0; i < 3 * a.M; ++i) ds[i] = 0.f;
+    for (int i = 0; i < 3 * a.M; ++i) ds[i] = 0.f * mk;
   }
-  if (masked && a.M > 0) {
-    float* ds = a.dsh + (size_t)g * a.M * 3;
-    for (int i = 0; i < 3 * a.M; ++i) ds[i] *= mk;
-  }
-  a.dmeans3D[3 * g] = dm[0] * mk; a.dmeans3D[3 * g + 1] = dm[1] * mk; a.dmeans3D[3 * g + 2] = dm[2] * mk;
 #pragma unroll
-  for (int i = 0; i < 6; ++i) a.dcov3D[6 * g + i] = dcov[i] * mk;
-  a.dscales[3 * g] = dscale[0] * mk; a.dscales[3 * g + 1] = dscale[1] * mk;
-  a.dscales[3 * g + 2] = dscale[2] * mk;
-  reinterpret_cast<float4*>(a.drot)[g] =
-      make_float4(drot[0] * mk, drot[1] * mk, drot[2] * mk, drot[3] * mk);
+  for (int i = 0; i < 3; ++i) gput(a.dmeans3D + 3 * g + i, dm[i] * mk, ac);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) gput(a.dcov3D + 6 * g + i, dcov[i] * mk, ac);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) gput(a.dscales + 3 * g + i, dscale[i] * mk, ac);
+  if (ac) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a.drot[4 * g + i] += drot[i] * mk;
+  } else {
+    reinterpret_cast<float4*>(a.drot)[g] =
+        make_float4(drot[0] * mk, drot[1] * mk, drot[2] * mk, drot[3] * mk);
+  }
 }
 
 void launch_preprocess_bwd(const PreprocessBwdArgs& a, hipStream_t s) {

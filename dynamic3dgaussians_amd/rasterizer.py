@@ -136,6 +136,17 @@ class _RasterizeGaussians(torch.autograd.Function):
         fuse = (label is not None and label.dim() == 1 and label.numel() == means3D.size(0)
                 and label.dtype in _FUSABLE_LABEL_DTYPES)
         kw = dict(compat=ctx.compat, grad_mask=label if fuse else None)
+        sink = getattr(rs, "grad_sink", None)
+        if sink is not None and (label is None or fuse):
+            # multi-camera step: the kernels add this camera's gradients into
+            # the sink's buffers of the current stream; autograd gets None
+            P = means3D.size(0)
+            F = _C._feature_width(semantic_feature.numel() // max(P, 1)) if (
+                semantic_feature is not None and semantic_feature.numel()) else 0
+            M = sh.size(1) if sh.numel() else 0
+            kw["out"], kw["accumulate"] = sink._claim(means3D.device, P, F, M, ctx.sem_shape)
+            _C.rasterize_gaussians_backward(*args, **kw)
+            return (None,) * len(ctx.needs_input_grad)
         if rs.debug:
             cpu_args = cpu_deep_copy_tuple(args)
             try:
@@ -189,6 +200,80 @@ class GaussianRasterizationSettings(NamedTuple):
     debug: bool = False
     confidence: Optional[torch.Tensor] = None
     compat: Optional[str] = None
+    grad_sink: Optional["GradientSink"] = None  # multi-camera gradient sum (no reference analogue)
+
+
+class GradientSink:
+    """Sums the per-Gaussian gradients of many rasterizations -- the cameras of
+    one multi-camera training step -- inside the backward kernels.
+
+    With `GaussianRasterizationSettings(..., grad_sink=sink)`, the backward of
+    every rasterization writes (first camera of the step on a stream) or adds
+    (GS_FLAG_ACCUMULATE, the following ones) its gradients into per-stream
+    buffers owned by the sink and hands autograd None for the Gaussian
+    inputs, instead of returning a fresh gradient set per camera that autograd
+    then adds into the leaves (one elementwise add per camera and parameter).
+    `gradients()` returns the sums.  The reference has no counterpart: its
+    training loop steps once per camera (train.py:422-433); the sum equals
+    what autograd accumulates over the same cameras up to fp32 reordering
+    (tests/test_gpu_streams.py).  Gradients whose label is not fusable into
+    the kernel (see _RasterizeGaussians.backward) bypass the sink.
+
+    Per-stream slots: autograd runs a camera's backward on its forward's
+    stream, and the accumulation is a non-atomic read-modify-write, so each
+    stream sums into its own buffers.
+    """
+    # backward buffer -> GaussianRasterizer argument name
+    NAMES = {"dmeans3D": "means3D", "dmeans2D": "means2D", "dsh": "shs", "dcolors": "colors_precomp",
+             "dsem": "semantic_feature", "dopacity": "opacities", "dscales": "scales",
+             "drot": "rotations", "dcov3D": "cov3D_precomp"}
+
+    def __init__(self):
+        self._slots = {}
+        self._sem_shape = None
+
+    def reset(self) -> None:
+        """Start a new sum (the next backward on each stream overwrites)."""
+        for slot in self._slots.values():
+            slot["fresh"] = True
+
+    def _claim(self, device, P, F, M, sem_shape):
+        key = (device, torch.cuda.current_stream(device).cuda_stream)
+        slot = self._slots.get(key)
+        if slot is None or slot["shape"] != (P, F, M):
+            slot = {"bufs": _C.backward_buffers(P, F, M, device), "shape": (P, F, M), "fresh": True}
+            self._slots[key] = slot
+        accumulate = not slot["fresh"]
+        slot["fresh"] = False
+        self._sem_shape = sem_shape
+        return slot["bufs"], accumulate
+
+    def gradients(self) -> dict:
+        """Summed gradients by GaussianRasterizer argument name (means3D,
+        means2D, shs, colors_precomp, semantic_feature, opacities, scales,
+        rotations, cov3D_precomp); absent inputs are left out.  Call on a
+        stream ordered after every accumulating stream.  With one stream the
+        tensors alias the sink's buffers: valid until the next reset()."""
+        live = [s for s in self._slots.values() if not s["fresh"]]
+        if not live:
+            return {}
+        out = {}
+        for k, name in self.NAMES.items():
+            t = live[0]["bufs"][k]
+            for slot in live[1:]:
+                t = t + slot["bufs"][k]
+            out[name] = t
+        P, F, M = live[0]["shape"]
+        if M == 0:
+            del out["shs"]
+        if self._sem_shape is None or F == 0:
+            del out["semantic_feature"]
+        else:
+            n = 1
+            for d in self._sem_shape[1:]:
+                n *= d
+            out["semantic_feature"] = out["semantic_feature"][:, :n].reshape(self._sem_shape)
+        return out
 
 
 _UNSET = object()

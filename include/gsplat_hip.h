@@ -34,13 +34,23 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 4
+#define GS_ABI_VERSION 5
 
 /* compat modes: numerics of the as-shipped reference vs corrected ones */
 #define GS_COMPAT_REFERENCE 0
 #define GS_COMPAT_FIXED 1
 
-typedef void *gs_stream_t; /* a hipStream_t (NULL = legacy default stream) */
+typedef void *gs_stream_t;
+
+/* gs_gaussians.flags.  GS_FLAG_ACCUMULATE (gs_backward only; no reference
+ * analogue): ADD this call's gradients into the dL_d* outputs instead of
+ * overwriting them, so the cameras of a multi-camera step sum into one set
+ * of buffers without an elementwise add per camera and parameter.  The
+ * outputs must hold valid sums (e.g. the first camera's, written without the
+ * flag); calls accumulating into the same outputs must be ordered on one
+ * stream (the non-atomic read-modify-write of the per-Gaussian outputs is
+ * not safe across concurrent streams). */
+#define GS_FLAG_ACCUMULATE 1u /* a hipStream_t (NULL = legacy default stream) */
 
 /* Per-Gaussian inputs (device pointers, fp32, row-major/contiguous).
  * Mirrors the tensor arguments of RasterizeGaussiansCUDA
@@ -59,7 +69,7 @@ typedef struct gs_gaussians {
   const float *rotations;         /* P x 4 (r,x,y,z) or NULL */
   const float *cov3D_precomp;     /* P x 6 or NULL */
   float scale_modifier;
-  int32_t _pad;
+  uint32_t flags;                 /* GS_FLAG_* (0 = the reference's semantics) */
   /* Optional per-Gaussian gradient mask (P floats or NULL), used by
    * gs_backward only: dL/d{means3D, sh, colors, opacity, scales, rotations,
    * cov3D} are multiplied by it, exactly as the reference's Python autograd

@@ -50,3 +50,60 @@ def test_multi_stream_cameras_match_one_stream():
     for k in a:
         rel = ((a[k] - b[k]).norm() / a[k].norm().clamp_min(1e-30)).item()
         assert rel < 1e-5, (k, rel)
+
+
+def _sink_vs_autograd(n_streams, use_sh, P=12000, W=144, H=112, cams=5, F=32):
+    """Summed gradients of `cams` cameras: GradientSink (in-kernel
+    accumulation) vs autograd's accumulation on the leaves."""
+    from dynamic3dgaussians_amd.rasterizer import GradientSink
+    dev = torch.device("cuda", 0)
+    g = make_gaussians(P, F=F, seed=3, device=dev)
+    gen = torch.Generator(device=dev).manual_seed(2)
+    sh = torch.randn(P, 16, 3, device=dev, generator=gen) * 0.2
+    label = (torch.rand(P, device=dev, generator=gen) > 0.3).float()
+    up = [torch.randn(3, H, W, device=dev, generator=gen), torch.randn(1, H, W, device=dev, generator=gen),
+          torch.randn(F, H, W, device=dev, generator=gen)]
+    rig = camera_rig(cams, W, H)
+    main = torch.cuda.current_stream(dev)
+    streams = [main] + [torch.cuda.Stream(device=dev) for _ in range(n_streams - 1)]
+    names = ["means3D", "opacities", "scales", "rotations", "semantic_feature"] + (["shs"] if use_sh else ["colors_precomp"])
+    src = dict(means3D=g["means3D"], opacities=g["opacities"], scales=g["scales"], rotations=g["rotations"],
+               semantic_feature=g["semantic_feature"], shs=sh, colors_precomp=g["colors"])
+    out = {}
+    sink = GradientSink()
+    for mode in ("autograd", "sink"):
+        leaves = {k: src[k].clone().requires_grad_(True) for k in names}
+        m2 = torch.zeros_like(leaves["means3D"], requires_grad=True)
+        for st in streams:
+            st.wait_stream(main)
+        sink.reset()
+        for i, c in enumerate(rig):
+            rs = GaussianRasterizationSettings(
+                image_height=H, image_width=W, tanfovx=c.tanfovx, tanfovy=c.tanfovy, c_x=c.c_x, c_y=c.c_y,
+                bg=torch.zeros(3, device=dev), viewmatrix=torch.from_numpy(c.viewmatrix.copy()).to(dev),
+                projmatrix=torch.from_numpy(c.projmatrix.copy()).to(dev), sh_degree=3 if use_sh else 0,
+                campos=torch.from_numpy(c.campos.copy()).to(dev), compat="reference",
+                grad_sink=sink if mode == "sink" else None)
+            with torch.cuda.stream(streams[i % n_streams]):
+                im, radius, feat, depth, _ = GaussianRasterizer(rs)(means2D=m2, label=label, **leaves)
+                torch.autograd.backward([im, depth, feat], up)
+        for st in streams:
+            main.wait_stream(st)
+        if mode == "sink":
+            gr = sink.gradients()
+            out[mode] = {k: gr[k].clone() for k in names + ["means2D"]}
+            assert all(leaves[k].grad is None for k in names)  # autograd added nothing
+        else:
+            out[mode] = {k: leaves[k].grad.clone() for k in names}
+            out[mode]["means2D"] = m2.grad.clone()
+    torch.cuda.synchronize()
+    return out["autograd"], out["sink"]
+
+
+@pytest.mark.parametrize("n_streams,use_sh", [(1, False), (3, False), (2, True)])
+def test_gradient_sink_matches_autograd_sum(n_streams, use_sh):
+    a, b = _sink_vs_autograd(n_streams, use_sh)
+    for k in a:
+        assert a[k].shape == b[k].shape, k
+        rel = ((a[k] - b[k]).norm() / a[k].norm().clamp_min(1e-30)).item()
+        assert rel < 1e-5, (k, rel)
