@@ -62,6 +62,8 @@ def parse():
     ap.add_argument("--compat", default="reference", choices=["reference", "fixed"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--step-times", action="store_true",
+                    help="also report host timestamps of the timed steps (diagnostic)")
     return ap.parse_args()
 
 
@@ -348,8 +350,10 @@ def main():
     torch.cuda.synchronize()
     _lib.timing_enable(True, stages=[dom])
     t0 = time.perf_counter()
+    host_marks = []
     for _ in range(args.steps):
         step()
+        host_marks.append(time.perf_counter())
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -398,6 +402,9 @@ def main():
         "instances_per_cam": int(np.mean([L for L, _, _ in inst])),
         "num_rendered_per_cam": int(np.mean([R for _, _, R in inst])),
     }
+    if args.step_times:
+        result["host_step_ms"] = [round((b - a) * 1e3, 3) for a, b in zip([t0] + host_marks, host_marks)]
+        result["tail_ms"] = round((t0 + elapsed - host_marks[-1]) * 1e3, 3) if world == 1 else None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cb, psnr = cpu_baseline(args, params0, label, my_cams[0], settings[0], dev)
         result["cpu_baseline"] = cb
