@@ -161,13 +161,19 @@ __device__ inline float4_t mfma3(const bf16x8& ah, const bf16x8& al, const bf16x
 
 // ------------------------------------------------------------------ forward
 
-#ifdef GS_FWD_WPE  // occupancy experiment: request GS_FWD_WPE waves per SIMD
-#define GS_FWD_ATTR __attribute__((amdgpu_waves_per_eu(GS_FWD_WPE, 8)))
+// Waves per SIMD the forward asks the register allocator for: 4 for the
+// matrix-core feature widths (the two-survivor loop would otherwise settle
+// at 130 registers = 3 waves), else the compiler's choice.
+template <int F>
+constexpr int fwd_waves_per_simd() {
+#ifdef GS_FWD_WPE
+  return GS_FWD_WPE;
 #else
-#define GS_FWD_ATTR
+  return F == 32 ? 4 : 1;
 #endif
+}
 template <int F, int COMPAT>
-__global__ __launch_bounds__(64 * GS_WPB_FWD) GS_FWD_ATTR void render_fwd_kernel(
+__global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu(fwd_waves_per_simd<F>(), 8))) void render_fwd_kernel(
     int W, int H, int grid_x, int num_tiles, const uint2* __restrict__ ranges,
     const uint32_t* __restrict__ point_list, const float* __restrict__ rec,
     const float* __restrict__ feats, const float* __restrict__ bg, float* __restrict__ out_color,
@@ -187,7 +193,7 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) GS_FWD_ATTR void render_fwd_kernel
   // per record: (x, y, -a/2, -b) (-c/2, opacity, r, g) (b, depth, -, -)
   __shared__ float4 s_rec[GS_WPB_FWD][CHUNK][3];
   // batch weights [slot][pixel] (row pad 4: conflict-free writes and reads)
-  __shared__ float s_fw[GS_WPB_FWD][MF ? WBF : 1][68];
+  __shared__ float s_fw[GS_WPB_FWD][MF ? WBF + 1 : 1][68];  // +1: a pair may overfill by one
 
   // strip item = tile * 4 + wave (dispatch order, see strip_item)
   const int lane = threadIdx.x & 63, lw = threadIdx.x >> 6;  // lw: LDS slot of the wave
@@ -285,6 +291,64 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) GS_FWD_ATTR void render_fwd_kernel
     STAT(1, range.y - c0 < CHUNK ? range.y - c0 : CHUNK);
     STAT(2, __builtin_popcountll(mask));
     q = load_rec(point_list, rec, c0 + CHUNK + lane, lastv);  // prefetch (clamped)
+#ifndef GS_FWD_NO_PAIR
+    if constexpr (F == 0 || MF) {
+      // Two survivors per iteration: their exponents are evaluated side by
+      // side (independent work for the issue slots), then blended in order.
+      // A missing second survivor gets power = +1 (never blends).
+      auto blend_step = [&](int j, const float4& r1, const float4& r2, float power, float alpha) {
+        const float test_T = T * (1 - alpha);
+        const bool cand = live != 0u && !(power > 0.0f) && !(alpha < ALPHA_MIN);
+        const bool fin = cand && test_T < 0.0001f;  // saturated: not blended, lane done
+        const bool blend = cand && !fin;
+        live = fin ? 0u : live;
+        const float w = blend ? alpha * T : 0.0f;
+        C0 = fmaf(r1.z, w, C0);
+        C1 = fmaf(r1.w, w, C1);
+        C2 = fmaf(r2.x, w, C2);
+        Dp = fmaf(r2.y, w, Dp);
+        T = blend ? test_T : T;
+        last = blend ? c0 + j - range.x + 1 : last;
+        if constexpr (MF) {
+          if (wave_any(blend)) {  // park it; the batch is flushed after the pair
+            s_fw[lw][nb][lane] = w;  // 0 on non-blending lanes
+            gidv = lane == nb ? __builtin_amdgcn_readlane(chunk_gid, j) : gidv;
+            ++nb;
+          }
+        }
+      };
+      while (mask) {
+        const int ja = __builtin_ctzll(mask);
+        mask &= mask - 1;
+        const bool two = mask != 0;
+        const int jb = two ? __builtin_ctzll(mask) : ja;
+        if (two) mask &= mask - 1;
+        STAT(3, two ? 2 : 1);
+        const float4 a0 = s_rec[lw][ja][0], a1 = s_rec[lw][ja][1], a2 = s_rec[lw][ja][2];
+        const float4 b0 = s_rec[lw][jb][0], b1 = s_rec[lw][jb][1], b2 = s_rec[lw][jb][2];
+        const float pa = gauss_power(a0.x - pfx, a0.y - pfy, make_float4(a0.z, a0.w, a1.x, 0.f));
+        float pb = gauss_power(b0.x - pfx, b0.y - pfy, make_float4(b0.z, b0.w, b1.x, 0.f));
+        pb = two ? pb : 1.0f;
+        const float ala = fminf(0.99f, a1.y * fast_exp(pa));
+        const float alb = fminf(0.99f, b1.y * fast_exp(pb));
+        blend_step(ja, a1, a2, pa, ala);
+        blend_step(jb, b1, b2, pb, alb);
+        if constexpr (MF) {
+          if (nb >= WBF) {  // 16 or 17 parked: contract 16, carry the 17th to slot 0
+            flush(WBF);
+            if (nb > WBF) {
+              s_fw[lw][0][lane] = s_fw[lw][WBF][lane];
+              const uint32_t g16 = __builtin_amdgcn_readlane(gidv, WBF);
+              gidv = lane == 0 ? g16 : gidv;
+            }
+            nb -= WBF;
+          }
+        }
+        if (!wave_any(live != 0u)) goto blend_done;
+      }
+    } else
+#endif
+    {
     while (mask) {
       const int j = __builtin_ctzll(mask);
       mask &= ~(1ull << j);
@@ -341,6 +405,7 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) GS_FWD_ATTR void render_fwd_kernel
         }
       }
       if (!wave_any(live != 0u)) goto blend_done;
+    }
     }
   }
 blend_done:
