@@ -10,9 +10,9 @@
 // MI355X design -- no global sort at all:
 //  1. plan   (tile_hist_kernel): TB_BLOCKS workgroups each histogram the
 //     instances of a contiguous slice of the Gaussians over the tiles in LDS
-//     and write one column of a [tile][block] count matrix;
-//     (tile_rowscan_kernel) turns every row into per-block offsets inside
-//     the tile and a tile total; (tile_offsets_kernel, one workgroup) scans
+//     and write one row of a [block][tile] count matrix (contiguous);
+//     (tile_rowscan_kernel) turns every tile column into per-block offsets
+//     inside the tile and a tile total; (tile_offsets_kernel, one workgroup) scans
 //     the totals into ranges[tile], finds the longest tile and lists tiles
 //     too long for the LDS sort.  Its header {L, max length, #long tiles}
 //     is the one device->host read of the forward (the reference's
@@ -47,7 +47,7 @@ __global__ __launch_bounds__(TB_THREADS) void tile_hist_kernel(TileArgs a, int t
   __shared__ uint32_t s_rect[TB_THREADS / 64];
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   for (int i = tid; i < nt; i += TB_THREADS)
-    s_bin[i] = WRITE ? a.ranges[t0 + i].x + a.thist[(size_t)(t0 + i) * TB_BLOCKS + b] : 0u;
+    s_bin[i] = WRITE ? a.ranges[t0 + i].x + a.thist[(size_t)b * a.num_tiles + t0 + i] : 0u;
   __syncthreads();
   const int per = (a.P + TB_BLOCKS - 1) / TB_BLOCKS;
   const int g0 = b * per, g1 = min(a.P, g0 + per);
@@ -96,7 +96,7 @@ __global__ __launch_bounds__(TB_THREADS) void tile_hist_kernel(TileArgs a, int t
     for (int o = 32; o > 0; o >>= 1) rect_n += __shfl_xor(rect_n, o, 64);
     if (lane == 0) s_rect[tid >> 6] = rect_n;
     __syncthreads();
-    for (int i = tid; i < nt; i += TB_THREADS) a.thist[(size_t)(t0 + i) * TB_BLOCKS + b] = s_bin[i];
+    for (int i = tid; i < nt; i += TB_THREADS) a.thist[(size_t)b * a.num_tiles + t0 + i] = s_bin[i];
     if (tid == 0 && t0 == 0) {
       uint32_t sum = 0;
       for (int w2 = 0; w2 < TB_THREADS / 64; ++w2) sum += s_rect[w2];
@@ -105,32 +105,44 @@ __global__ __launch_bounds__(TB_THREADS) void tile_hist_kernel(TileArgs a, int t
   }
 }
 
-// Row scan of the [tile][block] count matrix, one workgroup per tile:
-// per-block offset inside the tile, and the tile total.
-static_assert(TB_BLOCKS == 256, "tile_rowscan_kernel scans one count per thread");
-__global__ __launch_bounds__(TB_BLOCKS) void tile_rowscan_kernel(uint32_t* __restrict__ thist,
-                                                                 uint32_t* __restrict__ ttotal) {
-  __shared__ uint32_t s_w[TB_BLOCKS / 64];
-  const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  uint32_t* row = thist + (size_t)t * TB_BLOCKS;
-  const uint32_t v = row[tid];
-  uint32_t inc = v;
+// Column scan of the [block][tile] count matrix (each plan/bucket workgroup
+// reads and writes its own row contiguously): for every tile, the exclusive
+// scan over the blocks (each block's offset inside the tile) and the tile
+// total.  A workgroup takes RS_T tiles; thread (bg, tt) walks blocks
+// 16 bg .. 16 bg + 15 of tile tt (16 tiles x 4 B = one 64-B piece per block
+// row and load), the 16 block-group partial sums are scanned through LDS.
+static_assert(TB_BLOCKS == 256, "tile_rowscan_kernel: 16 block groups of 16 blocks");
+constexpr int RS_T = 16;
+__global__ __launch_bounds__(256) void tile_rowscan_kernel(uint32_t* __restrict__ thist,
+                                                           uint32_t* __restrict__ ttotal, int T) {
+  __shared__ uint32_t s_part[16][RS_T];
+  const int tid = threadIdx.x, tt = tid % RS_T, bg = tid / RS_T;
+  const int t = blockIdx.x * RS_T + tt;
+  const bool ok = t < T;
+  uint32_t v[16];
+  uint32_t sum = 0;
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(inc, o, 64);
-    if (lane >= o) inc += y;
+  for (int i = 0; i < 16; ++i) {
+    v[i] = ok ? thist[(size_t)(16 * bg + i) * T + t] : 0u;
+    sum += v[i];
   }
-  if (lane == 63) s_w[wave] = inc;
+  s_part[bg][tt] = sum;
   __syncthreads();
-  uint32_t woff = 0, tot = 0;
+  uint32_t off = 0, tot = 0;
 #pragma unroll
-  for (int w = 0; w < TB_BLOCKS / 64; ++w) {
-    const uint32_t x = s_w[w];
-    if (w < wave) woff += x;
+  for (int g = 0; g < 16; ++g) {
+    const uint32_t x = s_part[g][tt];
+    off += g < bg ? x : 0u;
     tot += x;
   }
-  row[tid] = woff + inc - v;
-  if (tid == 0) ttotal[t] = tot;
+  if (ok) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      thist[(size_t)(16 * bg + i) * T + t] = off;
+      off += v[i];
+    }
+    if (bg == 0) ttotal[t] = tot;
+  }
 }
 
 // One workgroup: exclusive scan of the tile totals into ranges, and the header.
@@ -373,7 +385,7 @@ void launch_tile_plan(const TileArgs& a, int prefiltered, hipStream_t s) {
     hipLaunchKernelGGL(tile_hist_kernel<false>, dim3(TB_BLOCKS), dim3(TB_THREADS), sizeof(uint32_t) * nt, s, a,
                        t0, nt);
   }
-  hipLaunchKernelGGL(tile_rowscan_kernel, dim3(T), dim3(TB_BLOCKS), 0, s, a.thist, a.ttotal);
+  hipLaunchKernelGGL(tile_rowscan_kernel, dim3((T + RS_T - 1) / RS_T), dim3(256), 0, s, a.thist, a.ttotal, T);
   hipLaunchKernelGGL(tile_offsets_kernel, dim3(1), dim3(OFF_T), 0, s, a.ttotal, T, a.bsum, a.ranges, a.meta,
                      prefiltered);
 }
