@@ -318,7 +318,10 @@ def main():
         for i, s in enumerate(settings):
             with torch.cuda.stream(streams[i % len(streams)]):
                 ras = GaussianRasterizer(s)
-                im, radius, feat, depth, _ = ras(**rvl)
+                if up_feat is not None:  # G3 call (label + semantic_feature)
+                    im, radius, feat, depth, _ = ras(**rvl)
+                else:                    # G2 call (label only)
+                    im, radius, depth, _ = ras(**rvl)
                 outs, grads = [im, depth], [up_color, up_depth]
                 if up_feat is not None:
                     outs.append(feat)
