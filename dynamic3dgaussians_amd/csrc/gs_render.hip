@@ -99,16 +99,22 @@ struct RecRegs {
   float tq;   // cull threshold
   uint32_t gid;
 };
-__device__ inline RecRegs load_rec(const uint32_t* __restrict__ point_list, const float* __restrict__ rec,
-                                   uint32_t i, uint32_t last_valid) {
+__device__ inline uint32_t load_gid(const uint32_t* __restrict__ point_list, uint32_t i, uint32_t last_valid) {
+  return point_list[i < last_valid ? i : last_valid];
+}
+__device__ inline RecRegs load_rec_gid(const float* __restrict__ rec, uint32_t gid) {
   RecRegs r;
-  r.gid = point_list[i < last_valid ? i : last_valid];
-  const float4* p = reinterpret_cast<const float4*>(rec + (size_t)r.gid * REC);
+  r.gid = gid;
+  const float4* p = reinterpret_cast<const float4*>(rec + (size_t)gid * REC);
   r.q0 = p[0];  // x, y, conic a, conic b
   r.q1 = p[1];  // conic c, opacity, r, g
   r.q2 = reinterpret_cast<const float2*>(p)[4];  // b, depth (R_EX, R_EY, R_RAD unused)
   r.tq = reinterpret_cast<const float*>(p)[R_TQ];
   return r;
+}
+__device__ inline RecRegs load_rec(const uint32_t* __restrict__ point_list, const float* __restrict__ rec,
+                                   uint32_t i, uint32_t last_valid) {
+  return load_rec_gid(rec, load_gid(point_list, i, last_valid));
 }
 
 // Gaussian exponent at pixel offset (dx, dy) from the conic scaled once per
@@ -271,8 +277,14 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
   };
 
   const uint32_t lastv = range.y > range.x ? range.y - 1 : range.x;
+  // Records are prefetched one chunk ahead and their list ids two chunks
+  // ahead, so the id -> record dependent load never waits inside a chunk.
   RecRegs q;
-  if (range.y > range.x) q = load_rec(point_list, rec, range.x + lane, lastv);
+  uint32_t gnext = 0;
+  if (range.y > range.x) {
+    q = load_rec(point_list, rec, range.x + lane, lastv);
+    gnext = load_gid(point_list, range.x + CHUNK + lane, lastv);
+  }
   STAT_DECL(st_it);
   STAT(6, 1);
   STAT(7, range.y - range.x);
@@ -290,7 +302,8 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
     STAT(0, 1);
     STAT(1, range.y - c0 < CHUNK ? range.y - c0 : CHUNK);
     STAT(2, __builtin_popcountll(mask));
-    q = load_rec(point_list, rec, c0 + CHUNK + lane, lastv);  // prefetch (clamped)
+    q = load_rec_gid(rec, gnext);                                 // next chunk (clamped)
+    gnext = load_gid(point_list, c0 + 2 * CHUNK + lane, lastv);    // the one after
 #ifndef GS_FWD_NO_PAIR
     if constexpr (F == 0 || MF) {
       // Two survivors per iteration: their exponents are evaluated side by
@@ -723,10 +736,14 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
   STAT(14, 1);
   STAT(15, wmax);
   STAT_DECL(st_it);
+  // records one chunk ahead, list ids two chunks ahead (see the forward)
   RecRegs q;
+  uint32_t gnext = 0;
   if (top > range.x) {
     const uint32_t c0 = top > range.x + CHUNK ? top - CHUNK : range.x;
     q = load_rec(point_list, rec, c0 + lane, top - 1);
+    const uint32_t n0 = c0 > range.x + CHUNK ? c0 - CHUNK : range.x;
+    gnext = load_gid(point_list, n0 + lane, top - 1);
   }
   for (uint32_t hi = top; hi > range.x;) {
     const uint32_t c0 = hi > range.x + CHUNK ? hi - CHUNK : range.x;
@@ -744,7 +761,9 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
     STAT(10, __builtin_popcountll(mask));
     {
       const uint32_t n0 = c0 > range.x + CHUNK ? c0 - CHUNK : range.x;
-      q = load_rec(point_list, rec, n0 + lane, top - 1);  // prefetch the next (lower) chunk
+      const uint32_t nn0 = n0 > range.x + CHUNK ? n0 - CHUNK : range.x;
+      q = load_rec_gid(rec, gnext);                        // the next (lower) chunk
+      gnext = load_gid(point_list, nn0 + lane, top - 1);   // the one after
     }
     while (mask) {
       const int j = 63 - __builtin_clzll(mask);
