@@ -81,7 +81,10 @@ __host__ __device__ inline int64_t sort_blocks(int64_t n) {
 // contiguous slice of the Gaussians and histogram their instances over (a
 // range of at most TB_BINS) tiles in LDS.
 constexpr int TB_BLOCKS = 256;
-constexpr int TB_THREADS = 512;
+#ifndef GS_TB_THREADS
+#define GS_TB_THREADS 1024
+#endif
+constexpr int TB_THREADS = GS_TB_THREADS;
 constexpr int TB_BINS = 16384;    // LDS tile bins per pass (64 KiB)
 constexpr int TS_CAP = 3584;      // per-tile LDS sort capacity (2 x 28 KiB of u64 keys)
 constexpr int TS_CAP_LONG = 9600; // long-tile launch: 2 x 75 KiB (+ 8 KiB radix state), one workgroup per CU
