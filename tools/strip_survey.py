@@ -18,6 +18,8 @@ layouts={
  '16x4': (yy//4).astype(int),
  '8x8': ((yy//8)*2+(xx//8)).astype(int),
  '4x16': (xx//4).astype(int),
+ '16x8': (yy//8).astype(int),
+ '16x16': np.zeros_like(xx).astype(int),
 }
 res={k:[0,0] for k in layouts}; pairs=0
 CH=100000
@@ -33,7 +35,9 @@ for s in range(0,len(pl),CH):
     ok=(power<=0)&(al>=1/255.)&(px<W)&(py<H)
     pairs+=ok.sum()
     for k,lab in layouts.items():
-        for q in range(4):
+        for q in range(lab.max()+1):
             res[k][0]+=ok[:,lab==q].any(1).sum()
 print('instances',len(pl),'pairs',pairs, time.time()-t0)
-for k,v in res.items(): print(k,'survivors',v[0],'slots',v[0]*64,'util',pairs/(v[0]*64))
+for k,v in res.items():
+    npx = 256 // (layouts[k].max() + 1)
+    print(k,'survivors',v[0],'pixel slots',v[0]*npx,'util',pairs/(v[0]*npx))
