@@ -107,12 +107,50 @@ def build(force: bool = False, verbose: bool = False) -> str:
     return LIB
 
 
+NATIVE_SRC = os.path.join(CSRC, "gs_torch_binding.cpp")
+NATIVE = os.path.join(OUT_DIR, "_gs_native.so")
+
+
+def native_is_stale() -> bool:
+    if not os.path.exists(NATIVE):
+        return True
+    t = os.path.getmtime(NATIVE)
+    return any(os.path.getmtime(f) > t for f in (NATIVE_SRC, os.path.join(INCLUDE, "gsplat_hip.h"), LIB))
+
+
+def build_native(force: bool = False, verbose: bool = False) -> str:
+    """The C++ fast path of the `_C` binding (csrc/gs_torch_binding.cpp): a
+    torch extension (host code only) linked against libgsplat_hip.so, written
+    to lib/_gs_native.so next to it (rpath $ORIGIN)."""
+    if VARIANT:
+        return ""
+    if not force and not native_is_stale():
+        return NATIVE
+    from torch.utils import cpp_extension  # heavy import, only when building
+    bdir = os.path.join(OUT_DIR, "native_obj")
+    os.makedirs(bdir, exist_ok=True)
+    os.environ.setdefault("MAX_JOBS", "4")
+    cpp_extension.load(name="_gs_native", sources=[NATIVE_SRC], build_directory=bdir,
+                       extra_include_paths=[INCLUDE], extra_cflags=["-O2"],
+                       # rpath $ORIGIN (lib/) and $ORIGIN/.. (the build dir's parent, lib/),
+                       # escaped for ninja ($$) and the shell ('')
+                       extra_ldflags=[f"-L{OUT_DIR}", "-lgsplat_hip", "-Wl,-rpath,'$$ORIGIN:$$ORIGIN/..'"],
+                       with_cuda=False, verbose=verbose, is_python_module=True)
+    built = os.path.join(bdir, "_gs_native.so")
+    tmp = NATIVE + ".tmp"
+    shutil.copyfile(built, tmp)
+    os.replace(tmp, NATIVE)
+    return NATIVE
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-v", "--verbose", action="store_true")
     args = ap.parse_args()
     print(build(force=args.force, verbose=args.verbose))
+    if not VARIANT:
+        print(build_native(force=args.force, verbose=args.verbose))
 
 
 if __name__ == "__main__":

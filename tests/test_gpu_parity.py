@@ -305,3 +305,48 @@ def test_absent_upstream_gradients_are_zeros():
         assert a.shape == b.shape
         if a.size:
             assert H.rel_l2(b, a) <= 1e-5 or np.abs(a).max() == 0
+
+
+
+def test_native_binding_matches_ctypes_binding():
+    """The C++ fast path (lib/_gs_native.so) and the ctypes binding drive the
+    same C ABI: identical forward outputs, and the same gradients (label mask,
+    padded feature width, SH, caller buffers with the accumulate flag)."""
+    from dynamic3dgaussians_amd import _C as C
+    assert C.native_loaded()
+    inp = H.scene(P=3000, F=20, sh_degree=2, use_sh=True, W=96, H=80)
+    grads = H.upstream_grads(80, 96, 20)
+    mask = torch.from_numpy((np.arange(3000) % 3 != 0).astype(np.float32)).to(H.DEV)
+    res = {}
+    keep = C._native
+    try:
+        for mode in ("native", "ctypes"):
+            C._native = keep if mode == "native" else None
+            f = H.gpu_forward(inp)
+            fw = [f[0]] + [t.cpu().numpy() for t in f[1:6]]
+            num_rendered, color, feat, depth, alpha, radii, geom, binning, img = f
+            dc, df, dd, da = [t.to(H.DEV) for t in grads]
+            d = lambda k: H._to(inp[k], H.DEV)  # noqa: E731
+            args = (d("bg"), d("means3D"), radii, d("colors"), d("semantic_feature"), d("scales"),
+                    d("rotations"), inp["scale_modifier"], d("cov3D_precomp"), d("viewmatrix"),
+                    d("projmatrix"), *H.bwd_cam4(inp, True), dc, df, dd, da, d("sh"), inp["degree"],
+                    d("campos"), geom, num_rendered, binning, img, alpha, False)
+            b = C.rasterize_gaussians_backward(*args, grad_mask=mask)
+            bufs = C.backward_buffers(3000, 32, inp["sh"].shape[1], H.DEV)
+            C.rasterize_gaussians_backward(*args, grad_mask=mask, out=bufs)
+            C.rasterize_gaussians_backward(*args, grad_mask=mask, out=bufs, accumulate=True)
+            torch.cuda.synchronize()
+            res[mode] = (fw, [t.cpu().numpy() for t in b], {k: v.cpu().numpy() for k, v in bufs.items()})
+    finally:
+        C._native = keep
+    (fa, ba, xa), (fb, bb, xb) = res["native"], res["ctypes"]
+    assert fa[0] == fb[0]
+    for a, b in zip(fa[1:], fb[1:]):
+        np.testing.assert_array_equal(a, b)
+    # fp32 atomics: the summation order may differ between runs
+    for a, b in zip(ba, bb):
+        assert H.rel_l2(a, b) <= 1e-5 or np.abs(b).max() == 0
+    for k in xa:
+        assert H.rel_l2(xa[k], xb[k]) <= 1e-5 or np.abs(xb[k]).max() == 0, k
+    # the accumulated buffers hold twice the single call's gradients
+    assert H.rel_l2(xa["dmeans3D"], 2 * ba[4]) <= 1e-5
