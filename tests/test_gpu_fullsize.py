@@ -1,0 +1,153 @@
+"""GPU parity at BASELINE.json's full sizes (the bench's synthetic scene).
+
+* configs[0] (10k Gaussians, SH degree 0, 256x256), configs[1] (100k, 800x800)
+  and one camera of configs[2] (300k, 800x800, F = 32): forward and backward
+  of the HIP path against the CPU oracle on the same seeded scene, with the
+  tolerances of tests/test_gpu_parity.py (images PSNR >= 80 dB and >= 99.9 %
+  of pixels within 1e-4; radii, num_rendered and tile lists bit-exact;
+  <= 0.1 % of pixels with a different last contributor) and gradients
+  relative L2 <= 1e-4 over the Gaussians whose footprint has no flipped
+  decision (over all Gaussians too in fixed mode).
+* configs[4] (1M Gaussians, 1920x1080, F = 32) is beyond what the
+  single-threaded oracle finishes in a test's time, so it is checked through
+  properties that do not depend on an oracle run:
+    - the forward is deterministic (two runs bit-identical);
+    - every tile list is in the reference's (depth, index) order, the ranges
+      tile the instance array contiguously, n_contrib never exceeds its tile's
+      list;
+    - coverage identity (fixed mode, colours and features all 1, bg 0): every
+      colour and feature channel equals the written alpha 1 - T (to 5e-5);
+    - the backward is linear in the upstream gradients:
+      bwd(g1 + 0.5 g2) = bwd(g1) + 0.5 bwd(g2) (relative L2 <= 1e-4; fp32
+      atomics reorder the sums).
+The oracle is only the checker here."""
+import numpy as np
+import pytest
+import torch
+
+from tests import _harness as H
+from tests.test_gpu_parity import GRAD_NAMES, _cmp_forward
+
+pytestmark = pytest.mark.gpu
+
+
+def _fwd_bwd_vs_oracle(inp, compat, F):
+    g, o = _cmp_forward(inp, compat, F)
+    P, W, Hh = inp["means3D"].shape[0], inp["image_width"], inp["image_height"]
+    st_g = H.export_state(P, W, Hh, g)
+    frac = H.check_tile_lists(st_g, o[6], W, Hh)  # bit-exact lists, <= 0.1 % flipped pixels
+    assert 0.0 <= frac < 1.0
+    # gradients over the Gaussians whose footprint has no
+    # flipped decision.  In reference mode (Q1: the backward starts from
+    # T = 1, so T grows to ~1/T_final ~ 1e4 at saturated pixels) one flipped
+    # last contributor rescales its whole pixel's gradients; measured on
+    # configs[2]: 2 of 640,000 pixels flipped, every one of the 10 Gaussians
+    # holding > 98 % of the squared difference covers one of them, and the
+    # rest agree to <= 5e-6 (fixed mode: <= 1.3e-5 over all Gaussians).
+    flipped = H.flipped_pixels(st_g, o[6], W, Hh)
+    keep = ~H.covers_pixels(o[6], o[5], flipped, W)
+    assert keep.mean() >= 0.99
+    grads = H.upstream_grads(Hh, W, F)
+    gb = H.gpu_backward(inp, g, grads, compat)
+    ob = H.oracle_backward(inp, o, grads, compat)
+    for name, a, b in zip(GRAD_NAMES, gb, ob):
+        assert a.shape == b.shape, name
+        if b.size == 0 or not np.any(b):
+            assert not np.any(a) or np.abs(a).max() < 1e-6, name
+            continue
+        assert H.rel_l2(a[keep], b[keep]) <= 1e-4, (name, H.rel_l2(a[keep], b[keep]))
+        if compat == "fixed" or flipped.size == 0:
+            assert H.rel_l2(a, b) <= 1e-4, (name, H.rel_l2(a, b))
+
+
+def test_config0_sh0_256():
+    inp = H.scene(P=10_000, W=256, H=256, use_sh=True, sh_degree=0, scale_mult=1.0)
+    _fwd_bwd_vs_oracle(inp, "reference", 0)
+
+
+def test_config1_100k_800():
+    inp = H.scene(P=100_000, W=800, H=800, scale_mult=1.0)
+    _fwd_bwd_vs_oracle(inp, "reference", 0)
+
+
+@pytest.mark.parametrize("compat", ["reference", "fixed"])
+def test_config2_300k_800_f32(compat):
+    inp = H.scene(P=300_000, F=32, W=800, H=800, scale_mult=1.0)
+    _fwd_bwd_vs_oracle(inp, compat, 32)
+
+
+# ---------------------------------------------------------------- configs[4]
+
+C5 = dict(P=1_000_000, F=32, W=1920, H=1080, scale_mult=1.0)
+
+
+def test_config4_deterministic_sorted_lists():
+    inp = H.scene(**C5)
+    P, W, Hh = C5["P"], C5["W"], C5["H"]
+    a = H.gpu_forward(inp)
+    b = H.gpu_forward(inp)
+    assert a[0] == b[0]
+    for i in (1, 2, 3, 5):
+        assert torch.equal(a[i], b[i]), i
+    st = H.export_state(P, W, Hh, a)
+    sb = H.export_state(P, W, Hh, b)
+    np.testing.assert_array_equal(st["n_contrib"], sb["n_contrib"])
+    np.testing.assert_array_equal(st["point_list"], sb["point_list"])
+    rg = st["ranges"].reshape(-1, 2).astype(np.int64)
+    lens = rg[:, 1] - rg[:, 0]
+    assert (lens >= 0).all()
+    n = int(lens.sum())
+    assert n == st["num_instances"] <= a[0]
+    # non-empty ranges are contiguous, in tile order, from 0 to n
+    ne = rg[lens > 0]
+    assert ne[0, 0] == 0 and ne[-1, 1] == n
+    np.testing.assert_array_equal(ne[1:, 0], ne[:-1, 1])
+    # every list in (depth, index) order: the depth bits as the float sort key
+    pl = st["point_list"].astype(np.int64)
+    depth_bits = st["depths"].view(np.uint32).astype(np.int64)[pl]
+    key = (depth_bits << 32) | pl
+    same_tile = np.ones(n - 1, bool)
+    starts = ne[1:, 0]
+    same_tile[starts - 1] = False  # pairs that straddle a tile boundary
+    assert (np.diff(key)[same_tile] > 0).all()
+    # every listed Gaussian is visible
+    radii = a[5].cpu().numpy()
+    assert (radii[pl] > 0).all()
+    # n_contrib never points past its tile's list
+    gx = (W + 15) // 16
+    pix = np.arange(W * Hh)
+    tile = (pix // W // 16) * gx + (pix % W) // 16
+    assert (st["n_contrib"].astype(np.int64) <= lens[tile]).all()
+
+
+def test_config4_coverage_identity():
+    inp = H.scene(**C5)
+    inp["colors"] = torch.ones_like(inp["colors"])
+    inp["semantic_feature"] = torch.ones_like(inp["semantic_feature"])
+    out = H.gpu_forward(inp, "fixed")
+    color, feat, alpha = out[1], out[2], out[4]
+    a = alpha[0]
+    assert float(a.min()) >= 0.0 and float(a.max()) <= 1.0
+    assert float(a.mean()) > 0.05  # the scene covers the image
+    assert float((color - a).abs().max()) <= 5e-5
+    assert float((feat - a).abs().max()) <= 5e-5
+
+
+def test_config4_backward_linear():
+    inp = H.scene(**C5)
+    Hh, W, F = C5["H"], C5["W"], C5["F"]
+    fwd = H.gpu_forward(inp)
+    g1 = H.upstream_grads(Hh, W, F, seed=1)
+    g2 = H.upstream_grads(Hh, W, F, seed=2)
+    g3 = tuple(x + 0.5 * y for x, y in zip(g1, g2))
+    b1 = H.gpu_backward(inp, fwd, g1, "reference")
+    b2 = H.gpu_backward(inp, fwd, g2, "reference")
+    b3 = H.gpu_backward(inp, fwd, g3, "reference")
+    for name, x, y, z in zip(GRAD_NAMES, b1, b2, b3):
+        if z.size == 0:
+            continue
+        want = x.astype(np.float64) + 0.5 * y.astype(np.float64)
+        if not np.any(want):
+            assert not np.any(z), name
+            continue
+        assert H.rel_l2(z, want) <= 1e-4, (name, H.rel_l2(z, want))
