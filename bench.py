@@ -186,10 +186,23 @@ def valu_view(stage, avg_ms):
             "peak": f"{SIMDS} SIMDs x {CLOCK_GHZ} GHz, {VALU_ISSUE_CYC} cycles per wave64 VALU instruction"}
 
 
+def calc_psnr(img1, img2):
+    """The reference's PSNR (external.py:84-86: per-channel MSE over the
+    pixels, 20 log10(1/sqrt(mse))), averaged over the channels as its callers
+    do (train.py report / visualize)."""
+    a = np.asarray(img1, np.float64).reshape(img1.shape[0], -1)
+    b = np.asarray(img2, np.float64).reshape(img2.shape[0], -1)
+    mse = ((a - b) ** 2).mean(1)
+    with np.errstate(divide="ignore"):
+        return float(np.mean(20 * np.log10(1.0 / np.sqrt(mse))))
+
+
 def cpu_baseline(args, params, label, cam, settings, dev):
     """The CPU oracle (plain C restatement, 1 thread) on one camera of the same
     scene: forward + backward.  Also returns the PSNR of the HIP render of the
-    same camera against the oracle's."""
+    same camera against the oracle's, and both renders' PSNR against a
+    ground-truth image (the oracle's render of the scene with its means
+    jittered by N(0, 0.002), seeded: a stand-in for a training target)."""
     from oracle import oracle as O
     with torch.no_grad():
         rv = params2rendervar(params, label)
@@ -222,11 +235,22 @@ def cpu_baseline(args, params, label, cam, settings, dev):
     img = out[0].float().cpu().numpy()
     mse = float(np.mean((img.astype(np.float64) - color.astype(np.float64)) ** 2))
     psnr = float("inf") if mse == 0 else 10 * np.log10(1.0 / mse)
+    g = torch.Generator().manual_seed(7)
+    jitter = host["means3D"] + 0.002 * torch.randn(host["means3D"].shape, generator=g)
+    gt = O.rasterize_gaussians(
+        np.zeros(3, np.float32), jitter.contiguous(), host["colors_precomp"], host.get("semantic_feature"),
+        host["opacities"], host["scales"], host["rotations"], 1.0, None, cam.viewmatrix, cam.projmatrix,
+        cam.c_x, cam.c_y, cam.tanfovx, cam.tanfovy, cam.H, cam.W, None, 0, cam.campos,
+        compat=args.compat)[1]
+    p_hip, p_ref = calc_psnr(img, gt), calc_psnr(color, gt)
+    psnr_gt = {"hip": round(p_hip, 4), "oracle": round(p_ref, 4), "delta_db": round(p_hip - p_ref, 6),
+               "gt": "oracle render of the scene with means jittered by N(0, 0.002)",
+               "formula": "external.py:84-86 calc_psnr, channel mean"}
     mpix = cam.W * cam.H / 1e6
     return {"value": round(mpix / (t2 - t0), 4), "unit": "Mpix/s", "cores": 1, "kind": "port",
             "sample": f"1 of {args.cams} cameras ({cam.W}x{cam.H}, {args.gaussians} Gaussians, "
                       f"F={args.features}), fwd {t1 - t0:.2f}s + bwd {t2 - t1:.2f}s, "
-                      "oracle/gs_oracle.c single thread"}, psnr
+                      "oracle/gs_oracle.c single thread"}, psnr, psnr_gt
 
 
 def main():
@@ -409,9 +433,10 @@ def main():
         result["host_step_ms"] = [round((b - a) * 1e3, 3) for a, b in zip([t0] + host_marks, host_marks)]
         result["tail_ms"] = round((t0 + elapsed - host_marks[-1]) * 1e3, 3) if world == 1 else None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cb, psnr = cpu_baseline(args, params0, label, my_cams[0], settings[0], dev)
+        cb, psnr, psnr_gt = cpu_baseline(args, params0, label, my_cams[0], settings[0], dev)
         result["cpu_baseline"] = cb
         result["psnr_vs_oracle_db"] = round(psnr, 2) if np.isfinite(psnr) else "inf"
+        result["psnr_vs_gt_db"] = psnr_gt
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
