@@ -320,7 +320,9 @@ def main():
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(device=dev) for _ in range(n_streams - 1)]
 
     def step():
-        opt.zero_grad(set_to_none=False)
+        # grads set to None: the activation backward hands every parameter a
+        # fresh gradient (no zero fills, no in-place accumulation launches)
+        opt.zero_grad(set_to_none=os.environ.get("GS_BENCH_GRAD_NONE", "1") != "0")
         if sink is not None:
             sink.reset()
         rv = params2rendervar(params, label)

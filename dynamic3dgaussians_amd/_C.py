@@ -238,11 +238,29 @@ def _buffer_shapes(P, F, M):
                 dcov3D=(P, 6), dsh=(P, M, 3), dscales=(P, 3), drot=(P, 4))
 
 
-def backward_buffers(P, F, M, device) -> dict:
+def backward_buffers(P, F, M, device, flat=False):
     """Uninitialised gradient outputs of rasterize_gaussians_backward (F = the
-    compiled feature width, M = SH coefficients per Gaussian)."""
-    return {k: torch.empty(*shape, dtype=torch.float32, device=device)
-            for k, shape in _buffer_shapes(P, F, M).items()}
+    compiled feature width, M = SH coefficients per Gaussian).  With
+    `flat=True` they are contiguous views into one buffer (each starting on a
+    256-byte boundary) and (views, buffer, offsets) is returned, so that sums
+    of whole gradient sets take one elementwise launch."""
+    shapes = _buffer_shapes(P, F, M)
+    if not flat:
+        return {k: torch.empty(*shape, dtype=torch.float32, device=device) for k, shape in shapes.items()}
+    offs, o = {}, 0
+    for k, shape in shapes.items():
+        n = 1
+        for d in shape:
+            n *= d
+        offs[k] = (o, n, shape)
+        o += (n + 63) // 64 * 64
+    buf = torch.empty(max(o, 1), dtype=torch.float32, device=device)
+    return carve_buffers(buf, offs), buf, offs
+
+
+def carve_buffers(buf, offs) -> dict:
+    """The per-gradient views of a flat backward buffer (see backward_buffers)."""
+    return {k: buf[o:o + n].view(*shape) for k, (o, n, shape) in offs.items()}
 
 
 def rasterize_gaussians_backward(background, means3D, radii, colors, semantic_feature, scales,

@@ -25,7 +25,7 @@ from typing import NamedTuple, Optional
 import torch
 import torch.nn as nn
 
-from . import _C
+from . import _C, _lib
 from ._C import get_default_compat as _default_compat
 
 
@@ -241,7 +241,8 @@ class GradientSink:
         key = (device, torch.cuda.current_stream(device).cuda_stream)
         slot = self._slots.get(key)
         if slot is None or slot["shape"] != (P, F, M):
-            slot = {"bufs": _C.backward_buffers(P, F, M, device), "shape": (P, F, M), "fresh": True}
+            bufs, flat, offs = _C.backward_buffers(P, F, M, device, flat=True)
+            slot = {"bufs": bufs, "flat": flat, "offs": offs, "shape": (P, F, M), "fresh": True}
             self._slots[key] = slot
         accumulate = not slot["fresh"]
         slot["fresh"] = False
@@ -257,12 +258,17 @@ class GradientSink:
         live = [s for s in self._slots.values() if not s["fresh"]]
         if not live:
             return {}
-        out = {}
-        for k, name in self.NAMES.items():
-            t = live[0]["bufs"][k]
-            for slot in live[1:]:
-                t = t + slot["bufs"][k]
-            out[name] = t
+        if any(s["shape"] != live[0]["shape"] for s in live[1:]):
+            raise _lib.GsplatError("GradientSink: the streams' gradient sets have different shapes")
+        # one elementwise add per extra stream over the whole gradient set
+        if len(live) == 1:
+            bufs = live[0]["bufs"]
+        else:
+            flat = live[0]["flat"] + live[1]["flat"]
+            for slot in live[2:]:
+                flat.add_(slot["flat"])
+            bufs = _C.carve_buffers(flat, live[0]["offs"])
+        out = {name: bufs[k] for k, name in self.NAMES.items()}
         P, F, M = live[0]["shape"]
         if M == 0:
             del out["shs"]
