@@ -169,3 +169,31 @@ def test_drop_in_import_name():
     import diff_gaussian_rasterization as d
     from diff_gaussian_rasterization import _C as c2
     assert d.GaussianRasterizer is R.GaussianRasterizer and c2 is _C
+
+
+@pytest.mark.parametrize("P,F,M", [(1000, 32, 0), (777, 8, 16), (5, 0, 1)])
+def test_flat_backward_buffers_carving(P, F, M):
+    """GradientSink's per-stream slot: one flat buffer whose per-gradient views
+    have the binding's shapes, are contiguous, start on 256-byte boundaries
+    and do not overlap, so a whole gradient set sums with one add."""
+    plain = _C.backward_buffers(P, F, M, "cpu")
+    views, buf, offs = _C.backward_buffers(P, F, M, "cpu", flat=True)
+    assert set(views) == set(plain)
+    spans = []
+    for k, v in views.items():
+        assert v.shape == plain[k].shape, k
+        assert v.is_contiguous(), k
+        assert v.untyped_storage().data_ptr() == buf.untyped_storage().data_ptr(), k
+        o, n, _ = offs[k]
+        assert o % 64 == 0, k  # 64 floats = 256 B
+        assert v.numel() == n
+        spans.append((o, o + n))
+    spans.sort()
+    assert all(a[1] <= b[0] for a, b in zip(spans, spans[1:]))
+    # a sum of two flat slots carves back to the per-gradient sums
+    buf.normal_()
+    other = torch.randn_like(buf)
+    summed = _C.carve_buffers(buf + other, offs)
+    ov = _C.carve_buffers(other, offs)
+    for k in views:
+        torch.testing.assert_close(summed[k], views[k] + ov[k], rtol=0, atol=0)
