@@ -1,3 +1,4 @@
+# (historical: the companion-stream code this A/B switched was measured slower and removed)
 # plan chain on a high-priority companion stream: tests, then bench A/B (long windows, repeated)
 set -o pipefail
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out; rm -f gpurun_out/ab_prio.txt
