@@ -8,9 +8,9 @@
   <= 0.1 % of pixels with a different last contributor) and gradients
   relative L2 <= 1e-4 over the Gaussians whose footprint has no flipped
   decision (over all Gaussians too in fixed mode).
-* configs[4] (1M Gaussians, 1920x1080, F = 32) is beyond what the
-  single-threaded oracle finishes in a test's time, so it is checked through
-  properties that do not depend on an oracle run:
+* configs[4] (1M Gaussians, 1920x1080, F = 32): the same oracle comparison
+  (one camera, ~30 s of single-threaded oracle time), plus properties that do
+  not depend on an oracle run:
     - the forward is deterministic (two runs bit-identical);
     - every tile list is in the reference's (depth, index) order, the ranges
       tile the instance array contiguously, n_contrib never exceeds its tile's
@@ -151,3 +151,9 @@ def test_config4_backward_linear():
             assert not np.any(z), name
             continue
         assert H.rel_l2(z, want) <= 1e-4, (name, H.rel_l2(z, want))
+
+
+def test_config4_fwd_bwd_vs_oracle():
+    """configs[4] (1M Gaussians, 1920x1080, F = 32) against the oracle: one
+    camera, forward and backward, the criteria of configs[0-2]."""
+    _fwd_bwd_vs_oracle(H.scene(**C5), "reference", 32)
