@@ -19,6 +19,7 @@ from __future__ import annotations
 import ctypes
 import importlib.util
 import os
+import warnings
 
 import torch
 
@@ -46,6 +47,13 @@ def _native_mod():
     if not os.path.exists(path):
         return None
     _lib.load()
+    if _lib._build.native_is_stale():
+        # older than its source, a public header or libgsplat_hip.so: its
+        # argument handling may not match the library -- serve the calls
+        # through the ctypes binding instead (same kernels, more host time)
+        warnings.warn("lib/_gs_native.so is stale (rebuild with `python -m dynamic3dgaussians_amd.build`); "
+                      "using the ctypes binding", RuntimeWarning)
+        return None
     spec = importlib.util.spec_from_file_location("_gs_native", path)
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
@@ -150,7 +158,8 @@ class _Inputs:
                            colors_precomp=_ptr(self.colors), semantic_feature=_ptr(self.sem),
                            opacities=_ptr(self.opacity), scales=_ptr(self.scales),
                            rotations=_ptr(self.rotations), cov3D_precomp=_ptr(self.cov3D),
-                           scale_modifier=self.scale_modifier, flags=0, grad_mask=None)
+                           scale_modifier=self.scale_modifier, flags=0, grad_mask=None,
+                           densify_accum=None, densify_denom=None, max_radius=None)
 
 
 def _camera(dev, background, viewmatrix, projmatrix, campos, c_x, c_y, tan_fovx, tan_fovy, W, H):
@@ -268,7 +277,7 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, semantic_fe
                                  c_x, c_y, tan_fovx, tan_fovy, dL_dout_color, dL_dout_feature,
                                  dL_dout_depth, dL_dout_alpha, sh, degree, campos, geomBuffer, R,
                                  binningBuffer, imageBuffer, alphas, debug, *, compat=None,
-                                 grad_mask=None, out=None, accumulate=False):
+                                 grad_mask=None, out=None, accumulate=False, densify=None):
     """RasterizeGaussiansBackwardCUDA (DGR/rasterize_points.cu:128-225).
 
     Camera scalars are consumed in this positional order, exactly as the
@@ -286,6 +295,11 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, semantic_fe
     place, and with `accumulate=True` ADDED to (GS_FLAG_ACCUMULATE) -- the
     multi-camera gradient sink (rasterizer.GradientSink).  Accumulating calls
     into the same buffers must be ordered on one stream.
+
+    `densify` (keyword-only, no reference analogue): optional (accum, denom,
+    max_radius) fp32 [P] tensors that receive this view's densification
+    statistics (external.py:136-140, train.py:288-290; gsplat_hip.h
+    gs_gaussians.densify_accum), written or, with `accumulate`, added.
     """
     L_ = _lib.load()
     cm = _compat_code(compat)
@@ -301,7 +315,7 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, semantic_fe
                                 _opt(dL_dout_depth), _opt(dL_dout_alpha), _opt(sh), int(degree), campos,
                                 geomBuffer, int(R), _opt(binningBuffer), imageBuffer, alphas, bool(debug), cm,
                                 _opt(grad_mask), None if out is None else [out[k] for k in _BUFFER_ORDER],
-                                bool(accumulate),
+                                bool(accumulate), None if densify is None else list(densify),
                                 torch.cuda.current_stream(means3D.device).cuda_stream)
         except RuntimeError as ex:
             raise _lib.GsplatError(str(ex)) from None
@@ -347,6 +361,11 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, semantic_fe
                 raise RuntimeError(f"gradient buffer {k} must be a contiguous fp32 {shape} tensor on {dev}")
         if accumulate:
             g.flags = _lib.GS_FLAG_ACCUMULATE
+    if densify is not None:
+        for t in densify:
+            if tuple(t.shape) != (P,) or t.dtype != torch.float32 or t.device != dev or not t.is_contiguous():
+                raise RuntimeError(f"densify statistics must be contiguous fp32 ({P},) tensors on {dev}")
+        g.densify_accum, g.densify_denom, g.max_radius = (t.data_ptr() for t in densify)
     scratch = torch.empty(L_.gs_backward_scratch_bytes(P, inp.F), dtype=torch.uint8, device=dev)
     stream = _stream(dev)
     p = lambda t: t.data_ptr() if (t is not None and t.numel()) else None  # noqa: E731

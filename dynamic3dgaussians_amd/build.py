@@ -35,7 +35,8 @@ VARIANT_FLAGS = {"": [], "stats": ["-DGS_STATS"],
                  "exp_nofeat": ["-DGS_EXP_NO_FEAT_ATOMIC"], "exp_noacc": ["-DGS_EXP_NO_ACC_ATOMIC"],
                  "exp_noatomic": ["-DGS_EXP_NO_FEAT_ATOMIC", "-DGS_EXP_NO_ACC_ATOMIC"],
                  "exp_occ5": ["-DGS_EXP_FWD_LDS_PAD=18000"], "exp_occ3": ["-DGS_EXP_FWD_LDS_PAD=40000"],
-                 "exp_wg1": ["-DGS_WPB_FWD=1"], "exp_tilegroup": ["-DGS_XCD_TILE_GROUP"], "exp_strip16x4": ["-DGS_STRIP_16X4"], "exp_tb512": ["-DGS_TB_THREADS=512"], "exp_fwd_nopair": ["-DGS_FWD_NO_PAIR"], "exp_acc10": ["-DGS_ACC_STRIDE=10"], "exp_wg4": ["-DGS_WPB_BWD=4"], "exp_bwd_wpe3": ["-DGS_BWD_WPE=3"],  "exp_fwd_wpe5": ["-DGS_FWD_WPE=5"], "exp_fwd_wpe6": ["-DGS_FWD_WPE=6"]}
+                 "exp_wg1": ["-DGS_WPB_FWD=1"], "exp_tilegroup": ["-DGS_XCD_TILE_GROUP"], "exp_strip16x4": ["-DGS_STRIP_16X4"], "exp_tb512": ["-DGS_TB_THREADS=512"], "exp_fwd_nopair": ["-DGS_FWD_NO_PAIR"], "exp_acc10": ["-DGS_ACC_STRIDE=10"], "exp_wg4": ["-DGS_WPB_BWD=4"], "exp_bwd_wpe3": ["-DGS_BWD_WPE=3"],  "exp_fwd_wpe5": ["-DGS_FWD_WPE=5"], "exp_fwd_wpe6": ["-DGS_FWD_WPE=6"],
+                 "exp_noorder": ["-DGS_NO_TILE_ORDER"]}
 ARCH = os.environ.get("GSPLAT_OFFLOAD_ARCH", "gfx950")
 
 # Per-file flags.  The preprocess kernels are compiled without FMA
@@ -61,9 +62,15 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found: the HIP toolchain (ROCm) is required to build libgsplat_hip.so")
 
 
+def _headers() -> list[str]:
+    """Every public header: the C ABI and the structs the ctypes mirrors
+    follow (gs_optim.h, gs_neighbor.h, gs_knn.h)."""
+    return [os.path.join(INCLUDE, f) for f in sorted(os.listdir(INCLUDE)) if f.endswith(".h")]
+
+
 def _deps() -> list[str]:
-    files = [os.path.join(CSRC, f) for f in os.listdir(CSRC)]
-    files.append(os.path.join(INCLUDE, "gsplat_hip.h"))
+    files = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f != "gs_torch_binding.cpp"]
+    files += _headers()
     files.append(os.path.abspath(__file__))
     return files
 
@@ -115,7 +122,7 @@ def native_is_stale() -> bool:
     if not os.path.exists(NATIVE):
         return True
     t = os.path.getmtime(NATIVE)
-    return any(os.path.getmtime(f) > t for f in (NATIVE_SRC, os.path.join(INCLUDE, "gsplat_hip.h"), LIB))
+    return any(os.path.getmtime(f) > t for f in (NATIVE_SRC, *_headers(), LIB))
 
 
 def build_native(force: bool = False, verbose: bool = False) -> str:

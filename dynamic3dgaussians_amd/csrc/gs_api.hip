@@ -149,6 +149,7 @@ TileArgs tile_args(int P, int W, int H, void* geom, void* image) {
   t.bsum = at<uint32_t>(image, il.bsum);
   t.meta = at<uint32_t>(image, il.meta);
   t.ranges = at<uint2>(image, il.ranges);
+  t.order = at<uint32_t>(image, il.order);
   return t;
 }
 }  // namespace
@@ -280,6 +281,7 @@ int gs_forward_render(const gs_gaussians* g, const gs_camera* cam, int debug, in
   ta.plist = L > 0 ? at<uint32_t>(binning, bl.plist) : nullptr;
   const uint2* ranges = ta.ranges;
   const uint32_t* point_list = ta.plist;
+  launch_tile_order(ta, s);
   if (L > 0) {
     {
       StageTimer t(s, GS_STAGE_DUPLICATE);
@@ -295,6 +297,7 @@ int gs_forward_render(const gs_gaussians* g, const gs_camera* cam, int debug, in
   }
   RenderArgs ra{};
   ra.W = W; ra.H = H; ra.grid_x = gx; ra.num_tiles = gx * gy; ra.F = g->F; ra.compat = compat;
+  ra.order = ta.order;
   ra.ranges = ranges; ra.point_list = point_list; ra.rec = rec; ra.feats = g->semantic_feature;
   ra.bg = cam->background;
   ra.out_color = out_color; ra.out_feature = out_feature; ra.out_depth = out_depth; ra.out_alpha = out_alpha;
@@ -338,6 +341,7 @@ int gs_backward(const gs_gaussians* g, const gs_camera* cam, const int32_t* radi
   if (g->F > 0 && !accumulate) (void)hipMemsetAsync(dL_dsemantic, 0, sizeof(float) * (size_t)g->F * P, s);
   RenderBwdArgs ra{};
   ra.W = W; ra.H = H; ra.grid_x = gx; ra.num_tiles = gx * gy; ra.F = g->F; ra.compat = compat;
+  ra.order = at<uint32_t>(image, il.order);
   ra.ranges = at<uint2>(image, il.ranges);
   ra.point_list = binning ? at<uint32_t>(binning, bl.plist) : nullptr;
   ra.rec = at<float>(geom, gl.rec);
@@ -366,6 +370,7 @@ int gs_backward(const gs_gaussians* g, const gs_camera* cam, const int32_t* radi
   b.acc = acc;
   b.rec = at<float>(geom, gl.rec);
   b.grad_mask = g->grad_mask;
+  b.st_accum = g->densify_accum; b.st_denom = g->densify_denom; b.st_maxrad = g->max_radius;
   b.dmeans2D = dL_dmeans2D; b.dcolors = dL_dcolors; b.dsemantic = dL_dsemantic; b.dopacity = dL_dopacity;
   b.dmeans3D = dL_dmeans3D; b.dcov3D = dL_dcov3D; b.dsh = dL_dsh; b.dscales = dL_dscales;
   b.drot = dL_drotations;

@@ -138,7 +138,7 @@ struct SortLayout {
 // reference's num_rendered (bounding-rect instances), longest tile, status
 enum ImgMeta { M_L = 0, M_MAXN = 1, M_LREF = 2, M_STATUS = 3 };
 struct ImgLayout {
-  size_t ranges, n_contrib, thist, ttotal, bsum, meta, total;
+  size_t ranges, n_contrib, thist, ttotal, bsum, meta, order, total;
   int64_t tiles;
   __host__ __device__ ImgLayout(int W, int H) {
     tiles = (int64_t)((W + TILE - 1) / TILE) * ((H + TILE - 1) / TILE);
@@ -150,6 +150,7 @@ struct ImgLayout {
     ttotal = o;    o = align_up(o + sizeof(uint32_t) * t, 256);
     bsum = o;      o = align_up(o + sizeof(uint32_t) * TB_BLOCKS, 256);  // per-block rect instances
     meta = o;      o = align_up(o + sizeof(uint32_t) * 4, 256);
+    order = o;     o = align_up(o + sizeof(uint32_t) * t, 256);   // tiles, longest list first
     total = o;
   }
 };

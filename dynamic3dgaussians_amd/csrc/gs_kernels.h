@@ -47,6 +47,9 @@ struct PreprocessBwdArgs {
   const float* rec;  // P x REC render records (conic)
   const float* acc;  // P x 10 blend gradient sums (AccField)
   const float* grad_mask;  // P or null (Q12 label)
+  float* st_accum;   // P or null: densification statistics of this view (gs_gaussians.densify_accum)
+  float* st_denom;   // P or null
+  float* st_maxrad;  // P or null
   float* dmeans2D;
   float* dcolors;
   float* dsemantic;
@@ -60,6 +63,7 @@ struct PreprocessBwdArgs {
 
 struct RenderArgs {
   int W, H, grid_x, num_tiles, F, compat;
+  const uint32_t* order;  // num_tiles: dispatch order of the tiles (longest list first)
   const uint2* ranges;
   const uint32_t* point_list;
   const float* rec;
@@ -74,6 +78,7 @@ struct RenderArgs {
 
 struct RenderBwdArgs {
   int W, H, grid_x, num_tiles, F, compat;
+  const uint32_t* order;  // num_tiles: dispatch order of the tiles (longest list first)
   const uint2* ranges;
   const uint32_t* point_list;
   const float* rec;
@@ -110,6 +115,7 @@ struct TileArgs {
   uint32_t* bsum;        // TB_BLOCKS: bounding-rect instances per block (the reference's count)
   uint32_t* meta;        // 4
   uint2* ranges;         // num_tiles
+  uint32_t* order;       // num_tiles: tiles by descending list length (dispatch order)
   uint64_t* keys;        // L
   uint64_t* keys2;       // L (sort twin for long tiles)
   uint32_t* plist;       // L
@@ -119,6 +125,8 @@ void launch_tile_plan(const TileArgs& a, int prefiltered, hipStream_t s);
 // render: bucket the instances by tile, then sort every tile by (depth, id).
 // max_len = the plan header's longest tile (host copy), or -1 if unknown.
 void launch_tile_bucket(const TileArgs& a, hipStream_t s);
+// dispatch order of the blend / sort kernels (tiles by descending list length)
+void launch_tile_order(const TileArgs& a, hipStream_t s);
 void launch_tile_sort(const TileArgs& a, int64_t max_len, int64_t L, hipStream_t s);
 
 bool launch_render_fwd(const RenderArgs& a, hipStream_t s);

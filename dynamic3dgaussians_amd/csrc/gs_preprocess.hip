@@ -400,6 +400,15 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdArgs a
   const int ac = a.accumulate;
   gput(a.dmeans2D + 3 * g, am0, ac); gput(a.dmeans2D + 3 * g + 1, am1, ac);
   if (!ac) a.dmeans2D[3 * g + 2] = 0.f;
+  // densification statistics of this view (external.py:136-140: the norm of
+  // the view's own means2D gradient, as gs_optim.hip's statistics do;
+  // train.py:288-290: the max screen radius); unseen Gaussians add nothing
+  if (a.st_accum) gput(a.st_accum + g, vis ? sqrtf(am0 * am0 + am1 * am1) : 0.f, ac);
+  if (a.st_denom) gput(a.st_denom + g, vis ? 1.f : 0.f, ac);
+  if (a.st_maxrad) {
+    const float r = vis ? (float)a.radii[g] : 0.f;
+    a.st_maxrad[g] = ac ? fmaxf(a.st_maxrad[g], r) : r;
+  }
   const float dcol[3] = {acc[A_R], acc[A_G], acc[A_B]};
   // Q12 label mask (DGR/__init__.py:159-173), applied at store time exactly as
   // the reference's elementwise `grad * label` (the chain rule uses unmasked dcol).

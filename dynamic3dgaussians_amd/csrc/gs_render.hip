@@ -47,6 +47,18 @@ typedef float float4_t __attribute__((ext_vector_type(4)));
 
 __device__ inline bool wave_any(bool p) { return __ballot(p) != 0ull; }
 
+// Tile of dispatch slot `i`: the plan's order puts the longest tile lists
+// first (tile_offsets_kernel), so the long-running workgroups start early and
+// short ones fill the end of the launch instead of a few long ones trailing.
+__device__ inline int tile_of(const uint32_t* __restrict__ order, int i) {
+#ifdef GS_NO_TILE_ORDER
+  (void)order;
+  return i;
+#else
+  return (int)order[i];
+#endif
+}
+
 // Work counters for kernel tuning (tools/render_stats.py); compiled only into
 // the "stats" build variant (-DGS_STATS), never into the product library.
 #ifdef GS_STATS
@@ -180,7 +192,7 @@ constexpr int fwd_waves_per_simd() {
 }
 template <int F, int COMPAT>
 __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu(fwd_waves_per_simd<F>(), 8))) void render_fwd_kernel(
-    int W, int H, int grid_x, int num_tiles, const uint2* __restrict__ ranges,
+    int W, int H, int grid_x, int num_tiles, const uint32_t* __restrict__ order, const uint2* __restrict__ ranges,
     const uint32_t* __restrict__ point_list, const float* __restrict__ rec,
     const float* __restrict__ feats, const float* __restrict__ bg, float* __restrict__ out_color,
     float* __restrict__ out_feature, float* __restrict__ out_depth, float* __restrict__ out_alpha,
@@ -204,7 +216,7 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
   // strip item = tile * 4 + wave (dispatch order, see strip_item)
   const int lane = threadIdx.x & 63, lw = threadIdx.x >> 6;  // lw: LDS slot of the wave
   const int item = strip_item(blockIdx.x, num_tiles, GS_WPB_FWD) + lw;
-  const int tile = item >> 2, wave = item & 3;
+  const int tile = tile_of(order, item >> 2), wave = item & 3;
   const int tx = tile % grid_x, ty = tile / grid_x;
   const int qx0 = strip_x0(tx, wave), qy0 = strip_y0(ty, wave);  // lane = strip pixel (lane % STRIP_W, lane / STRIP_W)
   const int px = qx0 + lane % STRIP_W, py = qy0 + lane / STRIP_W;
@@ -503,7 +515,7 @@ constexpr int bwd_waves_per_simd() {
 }
 template <int F, int COMPAT>
 __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu(bwd_waves_per_simd<F, COMPAT>(), 8))) void render_bwd_kernel(
-    int W, int H, int grid_x, int num_tiles, const uint2* __restrict__ ranges,
+    int W, int H, int grid_x, int num_tiles, const uint32_t* __restrict__ order, const uint2* __restrict__ ranges,
     const uint32_t* __restrict__ point_list, const float* __restrict__ rec,
     const float* __restrict__ feats, const float* __restrict__ bg, const float* __restrict__ alphas,
     const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dpix,
@@ -524,7 +536,7 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
   // strip item = tile * 4 + wave (dispatch order, see strip_item)
   const int lane = threadIdx.x & 63, lw = threadIdx.x >> 6;  // lw: LDS slot of the wave
   const int item = strip_item(blockIdx.x, num_tiles, GS_WPB_BWD) + lw;
-  const int tile = item >> 2, wave = item & 3;
+  const int tile = tile_of(order, item >> 2), wave = item & 3;
   const int tx = tile % grid_x, ty = tile / grid_x;
   const int qx0 = strip_x0(tx, wave), qy0 = strip_y0(ty, wave);  // lane = strip pixel (lane % STRIP_W, lane / STRIP_W)
   const int px = qx0 + lane % STRIP_W, py = qy0 + lane / STRIP_W;
@@ -832,11 +844,11 @@ static void fwd_f(const RenderArgs& a, hipStream_t s) {
 #endif
   if (a.compat == COMPAT_REFERENCE)
     hipLaunchKernelGGL((render_fwd_kernel<F, COMPAT_REFERENCE>), grid, block, pad, s, a.W, a.H, a.grid_x,
-                       a.num_tiles, a.ranges, a.point_list, a.rec, a.feats, a.bg, a.out_color,
+                       a.num_tiles, a.order, a.ranges, a.point_list, a.rec, a.feats, a.bg, a.out_color,
                        a.out_feature, a.out_depth, a.out_alpha, a.n_contrib);
   else
     hipLaunchKernelGGL((render_fwd_kernel<F, COMPAT_FIXED>), grid, block, 0, s, a.W, a.H, a.grid_x,
-                       a.num_tiles, a.ranges, a.point_list, a.rec, a.feats, a.bg, a.out_color,
+                       a.num_tiles, a.order, a.ranges, a.point_list, a.rec, a.feats, a.bg, a.out_color,
                        a.out_feature, a.out_depth, a.out_alpha, a.n_contrib);
 }
 
@@ -845,11 +857,11 @@ static void bwd_f(const RenderBwdArgs& a, hipStream_t s) {
   dim3 grid(a.num_tiles * (4 / GS_WPB_BWD)), block(64 * GS_WPB_BWD);
   if (a.compat == COMPAT_REFERENCE)
     hipLaunchKernelGGL((render_bwd_kernel<F, COMPAT_REFERENCE>), grid, block, 0, s, a.W, a.H, a.grid_x,
-                       a.num_tiles, a.ranges, a.point_list, a.rec, a.feats, a.bg, a.alphas, a.n_contrib,
+                       a.num_tiles, a.order, a.ranges, a.point_list, a.rec, a.feats, a.bg, a.alphas, a.n_contrib,
                        a.dL_dpix, a.dL_dfeat, a.dL_ddepth, a.dL_dalpha, a.acc, a.dsem);
   else
     hipLaunchKernelGGL((render_bwd_kernel<F, COMPAT_FIXED>), grid, block, 0, s, a.W, a.H, a.grid_x,
-                       a.num_tiles, a.ranges, a.point_list, a.rec, a.feats, a.bg, a.alphas, a.n_contrib,
+                       a.num_tiles, a.order, a.ranges, a.point_list, a.rec, a.feats, a.bg, a.alphas, a.n_contrib,
                        a.dL_dpix, a.dL_dfeat, a.dL_ddepth, a.dL_dalpha, a.acc, a.dsem);
 }
 

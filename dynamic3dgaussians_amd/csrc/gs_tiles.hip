@@ -208,6 +208,45 @@ __global__ __launch_bounds__(OFF_T) void tile_offsets_kernel(const uint32_t* __r
   }
 }
 
+// Dispatch order of the blend (and sort) kernels: the tiles by descending
+// list length (a counting sort on the top 10 bits of the length), so the
+// longest tiles start first and the short ones fill the end of the launch --
+// the longest-processing-time-first rule for a greedy workgroup dispatcher
+// (bench camera: render_fwd 143 -> 135 us, render_bwd 263 -> 250 us).  The
+// order inside a bucket is arbitrary: every tile's result is independent of
+// when it runs.  One workgroup; launched with the render phase, off the
+// plan -> header-read path the host waits for.
+__global__ __launch_bounds__(OFF_T) void tile_order_kernel(const uint32_t* __restrict__ ttotal, int T,
+                                                           const uint32_t* __restrict__ meta,
+                                                           uint32_t* __restrict__ order) {
+  __shared__ uint32_t s_obin[OFF_T];
+  __shared__ uint32_t s_owsum[OFF_T / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int per = (T + OFF_T - 1) / OFF_T;
+  const int a0 = min(T, tid * per), a1 = min(T, a0 + per);
+  s_obin[tid] = 0;
+  __syncthreads();
+  const uint32_t mxl = meta[M_MAXN];
+  const int sh = mxl >= OFF_T ? (32 - __builtin_clz(mxl)) - 10 : 0;
+  for (int t = a0; t < a1; ++t) atomicAdd(&s_obin[OFF_T - 1 - min(ttotal[t] >> sh, (uint32_t)(OFF_T - 1))], 1u);
+  __syncthreads();
+  const uint32_t c = s_obin[tid];
+  uint32_t ci = c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(ci, o, 64);
+    if (lane >= o) ci += y;
+  }
+  if (lane == 63) s_owsum[wave] = ci;
+  __syncthreads();
+  uint32_t base = ci - c;
+  for (int w = 0; w < wave; ++w) base += s_owsum[w];
+  s_obin[tid] = base;
+  __syncthreads();
+  for (int t = a0; t < a1; ++t)
+    order[atomicAdd(&s_obin[OFF_T - 1 - min(ttotal[t] >> sh, (uint32_t)(OFF_T - 1))], 1u)] = (uint32_t)t;
+}
+
 // One tile per workgroup: LSD radix sort of its (depth bits << 32 | id) keys
 // on the depth bits relative to the tile's minimum, 8 bits a pass, only as
 // many passes as the tile's depth-bit span needs (and passes whose digit is
@@ -354,11 +393,12 @@ __device__ __attribute__((always_inline)) KP tile_radix_sort(KP A, KP B, int n, 
 // in global memory beyond.
 template <int NT>
 __global__ __launch_bounds__(NT) void tile_sort_kernel(const uint2* __restrict__ ranges,
+                                                       const uint32_t* __restrict__ order,
                                                        uint64_t* __restrict__ keys, uint64_t* __restrict__ keys2,
                                                        uint32_t* __restrict__ plist, int cap, int lo, int hi) {
   extern __shared__ uint64_t s_key[];  // 2 x cap keys
   __shared__ RadixSmem<NT> sm;
-  const uint2 r = ranges[blockIdx.x];
+  const uint2 r = ranges[order[blockIdx.x]];  // longest tiles first
   const int n = (int)(r.y - r.x);
   if (n == 0 || n <= lo || n > hi) return;
   if (n == 1) {
@@ -390,6 +430,10 @@ void launch_tile_plan(const TileArgs& a, int prefiltered, hipStream_t s) {
                      prefiltered);
 }
 
+void launch_tile_order(const TileArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(OFF_T), 0, s, a.ttotal, a.num_tiles, a.meta, a.order);
+}
+
 void launch_tile_bucket(const TileArgs& a, hipStream_t s) {
   const int T = a.num_tiles;
   for (int t0 = 0; t0 < T; t0 += TB_BINS) {
@@ -406,18 +450,18 @@ static void tile_sort_launches(const TileArgs& a, int64_t max_len, hipStream_t s
   // LDS sized to the longest tile when the plan's header is known on the host
   if (max_len >= 0 && max_len <= TS_CAP) {
     const int cap = max_len > 0 ? (int)max_len : 1;
-    hipLaunchKernelGGL(tile_sort_kernel<NT>, grid, block, 2 * sizeof(uint64_t) * cap, s, a.ranges, a.keys,
-                       a.keys2, a.plist, cap, 0, big);
+    hipLaunchKernelGGL(tile_sort_kernel<NT>, grid, block, 2 * sizeof(uint64_t) * cap, s, a.ranges, a.order,
+                       a.keys, a.keys2, a.plist, cap, 0, big);
     return;
   }
   // Long tiles (large scenes): the common tiles keep TS_CAP-sized LDS and
   // several workgroups per CU; the long ones follow in a second launch with
   // up to the whole 160 KiB per workgroup (global memory beyond TS_CAP_LONG).
-  hipLaunchKernelGGL(tile_sort_kernel<NT>, grid, block, 2 * sizeof(uint64_t) * TS_CAP, s, a.ranges, a.keys,
-                     a.keys2, a.plist, TS_CAP, 0, TS_CAP);
+  hipLaunchKernelGGL(tile_sort_kernel<NT>, grid, block, 2 * sizeof(uint64_t) * TS_CAP, s, a.ranges, a.order,
+                     a.keys, a.keys2, a.plist, TS_CAP, 0, TS_CAP);
   const int cap2 = (max_len >= 0 && max_len < TS_CAP_LONG) ? (int)max_len : TS_CAP_LONG;
-  hipLaunchKernelGGL(tile_sort_kernel<NT>, grid, block, 2 * sizeof(uint64_t) * cap2, s, a.ranges, a.keys,
-                     a.keys2, a.plist, cap2, TS_CAP, big);
+  hipLaunchKernelGGL(tile_sort_kernel<NT>, grid, block, 2 * sizeof(uint64_t) * cap2, s, a.ranges, a.order,
+                     a.keys, a.keys2, a.plist, cap2, TS_CAP, big);
 }
 
 void launch_tile_sort(const TileArgs& a, int64_t max_len, int64_t L, hipStream_t s) {

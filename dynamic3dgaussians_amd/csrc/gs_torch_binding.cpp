@@ -94,6 +94,7 @@ struct Inputs {
     g.scale_modifier = scale_modifier;
     g.flags = 0;
     g.grad_mask = nullptr;
+    g.densify_accum = g.densify_denom = g.max_radius = nullptr;
   }
 };
 
@@ -158,7 +159,8 @@ std::tuple<int64_t, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tens
 // RasterizeGaussiansBackwardCUDA (DGR/rasterize_points.cu:128-225), positional
 // order of _C.rasterize_gaussians_backward + compat code, optional label mask,
 // optional caller-owned buffers (9, in the output order) with the accumulate
-// flag, and the stream handle.
+// flag, optional densification statistics (accum, denom, max_radius), and the
+// stream handle.
 std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> backward(
     const Tensor& bg, const Tensor& means3D, const Tensor& radii, const OptT& colors, const OptT& sem,
     const OptT& scales, const OptT& rotations, double scale_modifier, const OptT& cov3D, const Tensor& view,
@@ -166,7 +168,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tenso
     const OptT& dL_feature, const OptT& dL_depth, const OptT& dL_alpha, const OptT& sh, int64_t degree,
     const Tensor& campos, const Tensor& geom, int64_t R, const OptT& binning, const Tensor& img,
     const Tensor& alphas, bool debug, int64_t compat, const OptT& grad_mask, c10::optional<std::vector<Tensor>> out,
-    bool accumulate, int64_t stream) {
+    bool accumulate, c10::optional<std::vector<Tensor>> densify, int64_t stream) {
   Inputs in(means3D, colors, sem, c10::nullopt, scales, rotations, scale_modifier, cov3D, sh, degree);
   const Tensor& img_ref = present(dL_color) ? *dL_color : alphas;
   const int64_t H = img_ref.size(-2), W = img_ref.size(-1);
@@ -203,6 +205,16 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tenso
   } else {
     if (accumulate) throw std::runtime_error("accumulate needs the caller's gradient buffers");
     for (int i = 0; i < 9; ++i) o.push_back(at::empty(shapes[i], f32));
+  }
+  if (densify.has_value()) {
+    const auto& d = *densify;
+    if (d.size() != 3) throw std::runtime_error("densify must hold (accum, denom, max_radius)");
+    for (const auto& t : d)
+      if (t.dim() != 1 || t.size(0) != P || t.scalar_type() != at::kFloat || t.device() != in.dev || !t.is_contiguous())
+        throw std::runtime_error("densify statistics must be contiguous fp32 (P,) tensors on the device");
+    in.g.densify_accum = d[0].data_ptr<float>();
+    in.g.densify_denom = d[1].data_ptr<float>();
+    in.g.max_radius = d[2].data_ptr<float>();
   }
   Tensor scratch = at::empty({(int64_t)gs_backward_scratch_bytes(P, (int32_t)in.F)},
                              f32.dtype(at::kByte));

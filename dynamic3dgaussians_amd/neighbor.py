@@ -87,13 +87,17 @@ class _Graph:
         self.dist = _need(variables["neighbor_dist"], "neighbor_dist", torch.float32, (N, K))
         self.prev_offset = _need(variables["prev_offset"], "prev_offset", torch.float32, (N, K, 3))
         self.prev_inv_rot = _need(variables["prev_inv_rot_fg"], "prev_inv_rot_fg", torch.float32, (N, 4))
-        key = (self.nbr.data_ptr(), N, K, self.nbr._version)
+        # The reverse CSR is cached with the caller's neighbour tensor itself
+        # (kept alive by the cache) and its version counter: a reassigned
+        # variables['neighbor_indices'] is a different object even when the
+        # caching allocator hands it the address of an earlier graph, and an
+        # in-place edit bumps _version.
         cached = variables.get(_REV_KEY)
-        if cached is None or cached[0] != key:
+        if cached is None or cached[0] is not nbr or cached[1] != nbr._version:
             rev_ptr, _, rev_pos = reverse_csr(self.nbr)
-            cached = (key, rev_ptr, rev_pos)
+            cached = (nbr, nbr._version, rev_ptr, rev_pos)
             variables[_REV_KEY] = cached
-        self.rev_ptr, self.rev_pos = cached[1], cached[2]
+        self.rev_ptr, self.rev_pos = cached[2], cached[3]
 
     def struct(self) -> _lib.GsNeighborGraph:
         return _lib.GsNeighborGraph(N=self.N, K=self.K, _pad=0, nbr=_ptr(self.nbr), weight=_ptr(self.weight),

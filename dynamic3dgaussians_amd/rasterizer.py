@@ -138,13 +138,20 @@ class _RasterizeGaussians(torch.autograd.Function):
         kw = dict(compat=ctx.compat, grad_mask=label if fuse else None)
         sink = getattr(rs, "grad_sink", None)
         if sink is not None and (label is None or fuse):
+            if ctx.needs_input_grad[1] and not sink._warned_means2D:
+                # means2D.grad stays None on this path (see GradientSink)
+                import warnings
+                warnings.warn("GradientSink: means2D.grad is not populated; use sink.densify_stats() / "
+                              "sink.update_densify_stats(variables) for the densification statistics "
+                              "and sink.gradients()['means2D'] for the summed gradient", RuntimeWarning)
+                sink._warned_means2D = True
             # multi-camera step: the kernels add this camera's gradients into
             # the sink's buffers of the current stream; autograd gets None
             P = means3D.size(0)
             F = _C._feature_width(semantic_feature.numel() // max(P, 1)) if (
                 semantic_feature is not None and semantic_feature.numel()) else 0
             M = sh.size(1) if sh.numel() else 0
-            kw["out"], kw["accumulate"] = sink._claim(means3D.device, P, F, M, ctx.sem_shape)
+            kw["out"], kw["accumulate"], kw["densify"] = sink._claim(means3D.device, P, F, M, ctx.sem_shape)
             _C.rasterize_gaussians_backward(*args, **kw)
             return (None,) * len(ctx.needs_input_grad)
         if rs.debug:
@@ -222,6 +229,17 @@ class GradientSink:
     Per-stream slots: autograd runs a camera's backward on its forward's
     stream, and the accumulation is a non-atomic read-modify-write, so each
     stream sums into its own buffers.
+
+    Densification statistics.  The sink hands autograd None, so means2D.grad
+    is not populated; the reference's per-camera bookkeeping
+    (accumulate_mean2d_gradient, external.py:136-140: the NORM of each
+    camera's own means2D gradient, and the max screen radius,
+    train.py:288-290) is kept by the backward kernel instead, per camera
+    (gs_gaussians.densify_accum): `densify_stats()` returns this step's
+    increments and `update_densify_stats(variables)` adds them to the
+    reference's `variables` dict.  (The norm of the summed means2D gradient,
+    sink.gradients()['means2D'], would be a different criterion.)  Equal to
+    the reference's per-camera updates up to fp32 reordering of the sum.
     """
     # backward buffer -> GaussianRasterizer argument name
     NAMES = {"dmeans3D": "means3D", "dmeans2D": "means2D", "dsh": "shs", "dcolors": "colors_precomp",
@@ -231,6 +249,7 @@ class GradientSink:
     def __init__(self):
         self._slots = {}
         self._sem_shape = None
+        self._warned_means2D = False
 
     def reset(self) -> None:
         """Start a new sum (the next backward on each stream overwrites)."""
@@ -242,12 +261,41 @@ class GradientSink:
         slot = self._slots.get(key)
         if slot is None or slot["shape"] != (P, F, M):
             bufs, flat, offs = _C.backward_buffers(P, F, M, device, flat=True)
-            slot = {"bufs": bufs, "flat": flat, "offs": offs, "shape": (P, F, M), "fresh": True}
+            stats = torch.empty(3, P, dtype=torch.float32, device=device)  # accum, denom, max radius
+            slot = {"bufs": bufs, "flat": flat, "offs": offs, "shape": (P, F, M), "fresh": True,
+                    "stats": stats}
             self._slots[key] = slot
         accumulate = not slot["fresh"]
         slot["fresh"] = False
         self._sem_shape = sem_shape
-        return slot["bufs"], accumulate
+        return slot["bufs"], accumulate, tuple(slot["stats"].unbind(0))
+
+    def densify_stats(self) -> dict:
+        """This step's densification statistics, summed over its cameras:
+        {'means2D_gradient_accum': sum of the per-camera |dL/dmeans2D[:, :2]|
+        of the cameras that saw each Gaussian, 'denom': how many saw it,
+        'max_2D_radius': the largest screen radius} -- [P] fp32 each, zero
+        for Gaussians no camera saw.  Call like gradients()."""
+        live = [s for s in self._slots.values() if not s["fresh"]]
+        if not live:
+            return {}
+        st = live[0]["stats"].clone()
+        for slot in live[1:]:
+            st[:2] += slot["stats"][:2]
+            torch.maximum(st[2], slot["stats"][2], out=st[2])
+        return {"means2D_gradient_accum": st[0], "denom": st[1], "max_2D_radius": st[2]}
+
+    def update_densify_stats(self, variables: dict) -> None:
+        """The reference's per-camera statistics updates for every camera of
+        the step (external.py:136-140, train.py:288-290) on its `variables`
+        dict: accum += sum of norms, denom += count, max_2D_radius =
+        max(max_2D_radius, radius) -- unseen Gaussians are unchanged."""
+        st = self.densify_stats()
+        if not st:
+            return
+        variables["means2D_gradient_accum"] += st["means2D_gradient_accum"]
+        variables["denom"] += st["denom"]
+        torch.maximum(variables["max_2D_radius"], st["max_2D_radius"], out=variables["max_2D_radius"])
 
     def gradients(self) -> dict:
         """Summed gradients by GaussianRasterizer argument name (means3D,

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 5
+#define GS_ABI_VERSION 6
 
 /* compat modes: numerics of the as-shipped reference vs corrected ones */
 #define GS_COMPAT_REFERENCE 0
@@ -77,6 +77,19 @@ typedef struct gs_gaussians {
    * (DGR/diff_gaussian_rasterization/__init__.py:159-173).  dL/dmeans2D and
    * dL/dsemantic are not masked (Q12). */
   const float *grad_mask;
+  /* Optional densification statistics of this view (gs_backward only; P
+   * floats each or NULL), the reference's per-camera bookkeeping after the
+   * backward (external.py:136-140 accumulate_mean2d_gradient, train.py:288-290):
+   * for seen = radii > 0,
+   *   densify_accum[seen] += |dL/dmeans2D[seen, :2]|   (this view's gradient)
+   *   densify_denom[seen] += 1
+   *   max_radius[seen]     = max(max_radius[seen], radii[seen])
+   * With GS_FLAG_ACCUMULATE clear they are written instead (unseen -> 0), so
+   * a multi-camera step can sum per-view norms while dL_dmeans2D itself
+   * holds the sum of the views' gradients. */
+  float *densify_accum;
+  float *densify_denom;
+  float *max_radius;
 } gs_gaussians;
 
 /* Camera / raster settings (GaussianRasterizationSettings,

@@ -21,6 +21,12 @@ def _free_port():
     return p
 
 
+def _cam_norms(c, P):
+    """Stand-in for one camera's |dL/dmeans2D| contributions (deterministic
+    in the camera id)."""
+    return torch.rand(P, generator=torch.Generator().manual_seed(500 + c))
+
+
 def _worker(rank, world, port, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -38,12 +44,21 @@ def _worker(rank, world, port, q):
             g = torch.Generator().manual_seed(100 + c)
             for p in params:
                 p.grad += torch.randn(p.shape, generator=g)
-        accum = torch.full((P,), float(rank + 1))
-        bucket = GradBucket(params, extras={"means2D_gradient_accum": accum})
+        # densification statistics: running totals, identical on every rank
+        # at the start of the step; each rank adds its own cameras
+        accum = torch.full((P,), 0.5)
+        denom = torch.full((P,), 2.0)
+        bucket = GradBucket(params, extras={"means2D_gradient_accum": accum, "denom": denom})
+        for c in cams:
+            accum += _cam_norms(c, P)
+            denom += (_cam_norms(c, P) > 0.5).float()
         bucket.all_reduce()
         radius = torch.arange(P, dtype=torch.float32) * (rank + 1)
         all_reduce_max_(radius)
-        q.put((rank, [p.grad.clone() for p in params], accum.clone(), radius.clone(), cams))
+        # numpy copies: tensors would travel as shared-memory handles that die
+        # with this process
+        q.put((rank, [p.grad.numpy().copy() for p in params], (accum.numpy().copy(), denom.numpy().copy()),
+               radius.numpy().copy(), cams))
     finally:
         dist.destroy_process_group()
 
@@ -72,9 +87,15 @@ def test_bucket_all_reduce_equals_sum_of_camera_grads(world):
     all_cams = sorted(c for r in res for c in r[4])
     assert all_cams == list(range(27))
     for rank, grads, accum, radius, _ in res:
+        grads = [torch.from_numpy(g) for g in grads]
+        accum = [torch.from_numpy(a) for a in accum]
+        radius = torch.from_numpy(radius)
         for a, b in zip(grads, ref):
             torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5)
-        assert torch.all(accum == sum(range(1, world + 1)))
+        ref_acc = torch.full((P,), 0.5) + sum(_cam_norms(c, P) for c in range(27))
+        ref_den = torch.full((P,), 2.0) + sum((_cam_norms(c, P) > 0.5).float() for c in range(27))
+        torch.testing.assert_close(accum[0], ref_acc, rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(accum[1], ref_den, rtol=0, atol=0)
         torch.testing.assert_close(radius, torch.arange(P, dtype=torch.float32) * world)
 
 
@@ -91,3 +112,69 @@ def test_bucket_noop_without_process_group():
     p.grad = torch.ones(5)
     GradBucket([p]).all_reduce()
     assert torch.all(p.grad == 1)
+
+
+def _multistep_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        P = 257
+        p = torch.zeros(P, 3, requires_grad=True)
+        accum, denom = torch.zeros(P), torch.zeros(P)
+        bucket = GradBucket([p], extras={"accum": accum, "denom": denom})
+        hist = []
+        for step in range(3):
+            cams = [step * 27 + c for c in shard_cameras(27, rank, world)]
+            p.grad = torch.zeros_like(p)
+            for c in cams:
+                p.grad += _cam_norms(c, P)[:, None]
+                accum += _cam_norms(c, P)
+                denom += 1.0
+            bucket.all_reduce()
+            if step == 1:
+                # densification reset of some accumulators, identical on every
+                # rank, between steps (external.py:237-240) -> resync
+                accum[::3] = 0.0
+                denom[::3] = 0.0
+                bucket.resync()
+            hist.append((p.grad.numpy().copy(), accum.numpy().copy(), denom.numpy().copy()))
+        q.put((rank, hist))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_bucket_statistics_over_steps_match_single_process(world):
+    """Running densification statistics over several steps (with a reset in
+    between) equal the single-process accumulation over all cameras: the
+    bucket must sum per-step increments, not the totals."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_multistep_worker, args=(r, world, port, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    P = 257
+    accum, denom = torch.zeros(P), torch.zeros(P)
+    ref = []
+    for step in range(3):
+        g = torch.zeros(P, 3)
+        for c in range(step * 27, step * 27 + 27):
+            g += _cam_norms(c, P)[:, None]
+            accum += _cam_norms(c, P)
+            denom += 1.0
+        if step == 1:
+            accum[::3] = 0.0
+            denom[::3] = 0.0
+        ref.append((g, accum.clone(), denom.clone()))
+    for _, hist in res:
+        for (g, a, d), (rg, ra, rd) in zip(hist, ref):
+            g, a, d = torch.from_numpy(g), torch.from_numpy(a), torch.from_numpy(d)
+            torch.testing.assert_close(g, rg, rtol=1e-5, atol=1e-5)
+            torch.testing.assert_close(a, ra, rtol=1e-5, atol=1e-5)
+            torch.testing.assert_close(d, rd, rtol=0, atol=0)

@@ -107,3 +107,69 @@ def test_gradient_sink_matches_autograd_sum(n_streams, use_sh):
         assert a[k].shape == b[k].shape, k
         rel = ((a[k] - b[k]).norm() / a[k].norm().clamp_min(1e-30)).item()
         assert rel < 1e-5, (k, rel)
+
+
+@pytest.mark.parametrize("n_streams", [1, 3])
+def test_gradient_sink_densify_stats_match_reference_bookkeeping(n_streams, P=12000, W=144, H=112, cams=5):
+    """With a sink, means2D.grad is not populated; the per-camera statistics
+    the reference derives from it (accumulate_mean2d_gradient,
+    external.py:136-140, and max_2D_radius, train.py:288-290) come out of the
+    backward kernel: equal to the reference's per-camera updates (norm of each
+    camera's own means2D gradient) up to fp32 summation order."""
+    from dynamic3dgaussians_amd.rasterizer import GradientSink
+    dev = torch.device("cuda", 0)
+    g = make_gaussians(P, F=0, seed=5, device=dev)
+    gen = torch.Generator(device=dev).manual_seed(4)
+    up = [torch.randn(3, H, W, device=dev, generator=gen), torch.randn(1, H, W, device=dev, generator=gen)]
+    rig = camera_rig(cams, W, H)
+    names = ["means3D", "opacities", "scales", "rotations", "colors_precomp"]
+    src = dict(means3D=g["means3D"], opacities=g["opacities"], scales=g["scales"], rotations=g["rotations"],
+               colors_precomp=g["colors"])
+
+    def settings(c, sink=None):
+        return GaussianRasterizationSettings(
+            image_height=H, image_width=W, tanfovx=c.tanfovx, tanfovy=c.tanfovy, c_x=c.c_x, c_y=c.c_y,
+            bg=torch.zeros(3, device=dev), viewmatrix=torch.from_numpy(c.viewmatrix.copy()).to(dev),
+            projmatrix=torch.from_numpy(c.projmatrix.copy()).to(dev), sh_degree=0,
+            campos=torch.from_numpy(c.campos.copy()).to(dev), compat="reference", grad_sink=sink)
+
+    # the reference: one camera at a time, statistics from means2D.grad
+    variables = {"means2D_gradient_accum": torch.zeros(P, device=dev), "denom": torch.zeros(P, device=dev),
+                 "max_2D_radius": torch.zeros(P, device=dev)}
+    for c in rig:
+        leaves = {k: src[k].clone().requires_grad_(True) for k in names}
+        m2 = torch.zeros_like(leaves["means3D"], requires_grad=True)
+        im, radius, depth, _ = GaussianRasterizer(settings(c))(means2D=m2, label=torch.ones(P, device=dev),
+                                                               **leaves)
+        torch.autograd.backward([im, depth], up)
+        seen = radius > 0
+        variables["max_2D_radius"][seen] = torch.max(radius[seen], variables["max_2D_radius"][seen])
+        variables["means2D_gradient_accum"][seen] += torch.norm(m2.grad[seen, :2], dim=-1)
+        variables["denom"][seen] += 1
+    # the sink, cameras over n_streams streams
+    sink = GradientSink()
+    mine = {k: torch.zeros(P, device=dev) for k in variables}
+    mine["means2D_gradient_accum"] += 0.25  # running totals from earlier steps are kept
+    main = torch.cuda.current_stream(dev)
+    streams = [main] + [torch.cuda.Stream(device=dev) for _ in range(n_streams - 1)]
+    for st in streams:
+        st.wait_stream(main)
+    sink.reset()
+    leaves = {k: src[k].clone().requires_grad_(True) for k in names}
+    m2 = torch.zeros_like(leaves["means3D"], requires_grad=True)
+    with pytest.warns(RuntimeWarning, match="means2D.grad is not populated"):
+        for i, c in enumerate(rig):
+            with torch.cuda.stream(streams[i % n_streams]):
+                im, radius, depth, _ = GaussianRasterizer(settings(c, sink))(
+                    means2D=m2, label=torch.ones(P, device=dev), **leaves)
+                torch.autograd.backward([im, depth], up)
+    for st in streams:
+        main.wait_stream(st)
+    assert m2.grad is None
+    sink.update_densify_stats(mine)
+    torch.cuda.synchronize()
+    assert int((variables["denom"] > 0).sum()) > P // 4  # the scene is seen
+    torch.testing.assert_close(mine["denom"], variables["denom"], rtol=0, atol=0)
+    torch.testing.assert_close(mine["max_2D_radius"], variables["max_2D_radius"], rtol=0, atol=0)
+    torch.testing.assert_close(mine["means2D_gradient_accum"] - 0.25, variables["means2D_gradient_accum"],
+                               rtol=1e-5, atol=1e-6)

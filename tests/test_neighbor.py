@@ -174,3 +174,30 @@ def test_neighbor_edge_cases():
     # CPU tensors raise (no CPU path)
     with pytest.raises(_lib.GsplatError):
         neighbor_losses(pts.cpu(), rot.cpu(), {k: t.cpu() for k, t in v.items()})
+
+
+@gpu
+def test_reverse_csr_cache_follows_reassigned_graph():
+    """The reference reassigns variables['neighbor_indices'] with a fresh
+    tensor (train.py:316-326); a same-shape graph that reuses the freed
+    address of the previous one must not pick up the cached reverse CSR."""
+    from dynamic3dgaussians_amd.neighbor import neighbor_losses
+    N, K = 1000, 7
+    pts, rot, v = make_state(N=N, K=K, seed=3, device="cuda")
+    p, r = pts.clone().requires_grad_(True), rot.clone().requires_grad_(True)
+    sum(neighbor_losses(p, r, v)).backward()
+    # a different graph of the same shape, stored where the old one lived
+    perm = torch.randperm(N, generator=torch.Generator().manual_seed(9)).cuda()
+    new_nbr = v["neighbor_indices"][perm].clone()
+    old_ptr = v["neighbor_indices"].data_ptr()
+    v["neighbor_indices"].copy_(new_nbr)  # in place: same address, bumped _version
+    assert v["neighbor_indices"].data_ptr() == old_ptr
+    for graph in ("in_place", "reassigned"):
+        if graph == "reassigned":
+            v["neighbor_indices"] = v["neighbor_indices"].clone()  # a new object
+        p1, r1 = pts.clone().requires_grad_(True), rot.clone().requires_grad_(True)
+        p2, r2 = pts.clone().requires_grad_(True), rot.clone().requires_grad_(True)
+        sum(neighbor_losses(p1, r1, v)).backward()
+        sum(ON.torch_reference(p2, r2, v)).backward()
+        assert _rel(p1.grad, p2.grad) <= 1e-4, graph
+        assert _rel(r1.grad, r2.grad) <= 1e-4, graph
