@@ -42,7 +42,7 @@ from dynamic3dgaussians_amd.camera import camera_rig  # noqa: E402
 from dynamic3dgaussians_amd.distributed import GradBucket  # noqa: E402
 from dynamic3dgaussians_amd.optim import FusedAdam  # noqa: E402
 from dynamic3dgaussians_amd.rasterizer import (GaussianRasterizationSettings,  # noqa: E402
-                                               GaussianRasterizer, GradientSink)
+                                               GaussianRasterizer, GaussianRasterizerBatch, GradientSink)
 from dynamic3dgaussians_amd.scene import make_gaussians  # noqa: E402
 
 METRIC = "rendered Mpix/s fwd+bwd (1/8 GPU) at 300k Gaussians; PSNR vs ref"
@@ -64,6 +64,9 @@ def parse():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--step-times", action="store_true",
                     help="also report host timestamps of the timed steps (diagnostic)")
+    ap.add_argument("--mode", default=os.environ.get("GS_BENCH_MODE", "batch"), choices=["batch", "percam"],
+                    help="batch: the rank's cameras through GaussianRasterizerBatch (one launch per stage "
+                         "for all of them); percam: one GaussianRasterizer call per camera (the drop-in)")
     return ap.parse_args()
 
 
@@ -265,7 +268,7 @@ def main():
     # kernels (GradientSink: GS_FLAG_ACCUMULATE into per-stream buffers)
     # instead of autograd adding 7 gradient tensors per camera into the
     # leaves; GS_BENCH_SINK=0 restores autograd's accumulation.
-    use_sink = os.environ.get("GS_BENCH_SINK", "1") != "0"
+    use_sink = os.environ.get("GS_BENCH_SINK", "1") != "0" and args.mode == "percam"
     sink = GradientSink() if use_sink else None
     settings = make_settings(my_cams, dev, args.compat, sink)
     params, label = make_params(args, dev)
@@ -318,8 +321,31 @@ def main():
         # the leaves' accumulation crosses the camera streams by design
         torch.autograd.graph.set_warn_on_accumulate_grad_stream_mismatch(False)
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(device=dev) for _ in range(n_streams - 1)]
+    if args.mode == "batch":
+        n_streams = 1
+        # one upstream gradient per camera, materialized once (the batch's
+        # backward reads [C, ...] images like C per-camera backwards do)
+        C_ = len(settings)
+        up_color_b = up_color.expand(C_, -1, -1, -1).contiguous()
+        up_depth_b = up_depth.expand(C_, -1, -1, -1).contiguous()
+        up_feat_b = up_feat.expand(C_, -1, -1, -1).contiguous() if up_feat is not None else None
+        batch_ras = GaussianRasterizerBatch(settings)
+
+    def step_batch():
+        opt.zero_grad(set_to_none=True)
+        rv = params2rendervar(params, label)
+        if up_feat_b is not None:  # G3 call (label + semantic_feature)
+            im, radius, feat, depth, _ = batch_ras(**rv)
+            torch.autograd.backward([im, depth, feat], [up_color_b, up_depth_b, up_feat_b])
+        else:                      # G2 call (label only)
+            im, radius, depth, _ = batch_ras(**rv)
+            torch.autograd.backward([im, depth], [up_color_b, up_depth_b])
+        bucket.all_reduce()
+        opt.step()
 
     def step():
+        if args.mode == "batch":
+            return step_batch()
         # grads set to None: the activation backward hands every parameter a
         # fresh gradient (no zero fills, no in-place accumulation launches)
         opt.zero_grad(set_to_none=os.environ.get("GS_BENCH_GRAD_NONE", "1") != "0")
@@ -420,9 +446,12 @@ def main():
         "data": "synthetic",
         "config": {"workload": f"{args.gaussians // 1000}k Gaussians x {args.cams} cams/rank x "
                                f"{W_}x{H_}, F={args.features} semantic channels, colors_precomp; "
-                               "fwd+bwd per camera + grad all-reduce + Adam",
+                               "fwd+bwd of every camera + grad all-reduce + Adam",
+                   "mode": ("camera batch (GaussianRasterizerBatch: one launch per stage for the rank's "
+                            "cameras)" if args.mode == "batch" else "per camera (GaussianRasterizer drop-in)"),
                    "optimizer": optim_kind, "streams": n_streams,
-                   "grad_sum": "in-kernel (GradientSink)" if use_sink else "autograd",
+                   "grad_sum": ("in-kernel (camera sum in preprocess_bwd)" if args.mode == "batch" else
+                                "in-kernel (GradientSink)" if use_sink else "autograd"),
                    "gaussians": args.gaussians, "cams_per_rank": args.cams, "width": W_,
                    "height": H_, "feature_channels": args.features, "compat": args.compat,
                    "parallelism": f"camera-sharded dp{world}"},

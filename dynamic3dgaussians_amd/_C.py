@@ -411,3 +411,149 @@ def mark_visible(means3D, viewmatrix, projmatrix):
         check(L_.gs_mark_visible(P, m.data_ptr(), v.data_ptr(), pr.data_ptr(), present.data_ptr(),
                                  _stream(dev)), "mark_visible")
     return present
+
+
+# ---------------------------------------------------------------------------
+# Camera batches (include/gsplat_hip.h gs_*_batch; no reference analogue): the
+# C cameras of one multi-camera step rendered with one launch per stage.
+
+def _camera_batch(dev, background, viewmatrices, projmatrices, campos, c_x, c_y, tan_fovx, tan_fovy, W, H):
+    C = len(c_x)
+    if not (1 <= C <= 64):
+        raise _lib.GsplatError(f"camera batch size {C} outside 1..64")
+    if not (len(c_y) == len(tan_fovx) == len(tan_fovy) == C):
+        raise RuntimeError("per-camera scalars must all have C entries")
+    view = _dev(viewmatrices, dev, "viewmatrices").reshape(C, 16).contiguous()
+    proj = _dev(projmatrices, dev, "projmatrices").reshape(C, 16).contiguous()
+    cpos = _dev(campos, dev, "campos").reshape(C, 3).contiguous()
+    bg = _dev(background, dev, "bg").reshape(-1)
+    cams = (GsCamera * C)()
+    for c in range(C):
+        cams[c] = GsCamera(viewmatrix=view.data_ptr() + 64 * c, projmatrix=proj.data_ptr() + 64 * c,
+                           campos=cpos.data_ptr() + 12 * c, background=bg.data_ptr(), c_x=float(c_x[c]),
+                           c_y=float(c_y[c]), tan_fovx=float(tan_fovx[c]), tan_fovy=float(tan_fovy[c]),
+                           image_width=int(W), image_height=int(H))
+    return cams, C, [view, proj, cpos, bg]
+
+
+def rasterize_gaussians_batch(background, means3D, colors, semantic_feature, opacity, scales, rotations,
+                              scale_modifier, cov3D_precomp, viewmatrices, projmatrices, c_x, c_y, tan_fovx,
+                              tan_fovy, image_height, image_width, sh, degree, campos, prefiltered, debug,
+                              *, compat=None):
+    """The forward of C cameras at once (gs_forward_plan_batch +
+    gs_forward_render_batch): the arguments of rasterize_gaussians with
+    per-camera matrices stacked ([C,4,4] or [C,16], campos [C,3]) and the
+    camera scalars as length-C sequences.  Returns (num_rendered[C],
+    color[C,3,H,W], feature_map[C,F,H,W], depth[C,1,H,W], alpha[C,1,H,W],
+    radii[C,P] int32, geomBuffer, binningBuffer, imgBuffer, num_instances[C]);
+    camera c's outputs equal rasterize_gaussians' for that camera."""
+    L_ = _lib.load()
+    cm = _compat_code(compat)
+    inp = _Inputs(means3D, colors, semantic_feature, opacity, scales, rotations, scale_modifier,
+                  cov3D_precomp, sh, degree)
+    dev, P = inp.device, inp.P
+    H, W = int(image_height), int(image_width)
+    cams, C, keep = _camera_batch(dev, background, viewmatrices, projmatrices, campos, c_x, c_y, tan_fovx,
+                                  tan_fovy, W, H)
+    f32 = dict(dtype=torch.float32, device=dev)
+    u8 = dict(dtype=torch.uint8, device=dev)
+    if P == 0:
+        return ([0] * C, torch.zeros(C, 3, H, W, **f32), torch.zeros(C, inp.F_user, H, W, **f32),
+                torch.zeros(C, 1, H, W, **f32), torch.zeros(C, 1, H, W, **f32),
+                torch.zeros(C, 0, dtype=torch.int32, device=dev), torch.empty(0, **u8), torch.empty(0, **u8),
+                torch.empty(0, **u8), [0] * C)
+    g = inp.struct()
+    out_color = torch.empty(C, 3, H, W, **f32)
+    out_feature = torch.empty(C, inp.F, H, W, **f32)
+    out_depth = torch.empty(C, 1, H, W, **f32)
+    out_alpha = torch.empty(C, 1, H, W, **f32)
+    radii = torch.empty(C, P, dtype=torch.int32, device=dev)
+    geom = torch.empty(L_.gs_batch_geom_buffer_bytes(P, C), **u8)
+    img = torch.empty(L_.gs_batch_image_buffer_bytes(W, H, C), **u8)
+    stream = _stream(dev)
+    NR = (ctypes.c_int64 * C)()
+    NI = (ctypes.c_int64 * C)()
+    check(L_.gs_forward_plan_batch(ctypes.byref(g), cams, C, int(bool(prefiltered)), int(bool(debug)), cm,
+                                   geom.data_ptr(), img.data_ptr(), radii.data_ptr(), NR, NI, stream),
+          "rasterize_gaussians_batch (preprocess)")
+    binning = torch.empty(max(1, L_.gs_batch_binning_buffer_bytes(C, NI)), **u8)
+    check(L_.gs_forward_render_batch(ctypes.byref(g), cams, C, int(bool(debug)), cm, geom.data_ptr(),
+                                     binning.data_ptr(), img.data_ptr(), NI, radii.data_ptr(),
+                                     out_color.data_ptr(), out_feature.data_ptr() if inp.F else None,
+                                     out_depth.data_ptr(), out_alpha.data_ptr(), stream),
+          "rasterize_gaussians_batch (render)")
+    del keep
+    feature_map = out_feature[:, :inp.F_user] if inp.F_user != inp.F else out_feature
+    return (list(NR), out_color, feature_map, out_depth, out_alpha, radii, geom, binning, img, list(NI))
+
+
+def rasterize_gaussians_batch_backward(background, means3D, radii, colors, semantic_feature, scales,
+                                       rotations, scale_modifier, cov3D_precomp, viewmatrices, projmatrices,
+                                       c_x, c_y, tan_fovx, tan_fovy, dL_dout_color, dL_dout_feature,
+                                       dL_dout_depth, dL_dout_alpha, sh, degree, campos, geomBuffer,
+                                       num_instances, binningBuffer, imageBuffer, alphas, debug, *,
+                                       compat=None, grad_mask=None, densify=None):
+    """The backward of a camera batch (gs_backward_batch): the arguments of
+    rasterize_gaussians_backward with stacked per-camera matrices, scalars
+    and upstream gradients ([C, ...]), in the binding's positional camera
+    semantics.  Returns the rasterize_gaussians_backward tuple with every
+    per-Gaussian gradient SUMMED over the cameras.  `densify` as in
+    rasterize_gaussians_backward (per-camera statistics, summed)."""
+    L_ = _lib.load()
+    cm = _compat_code(compat)
+    inp = _Inputs(means3D, colors, semantic_feature, None, scales, rotations, scale_modifier,
+                  cov3D_precomp, sh, degree)
+    dev, P = inp.device, inp.P
+    C = len(c_x)
+    img_ref = dL_dout_color if _present(dL_dout_color) else alphas
+    H, W = img_ref.size(-2), img_ref.size(-1)
+    f32 = dict(dtype=torch.float32, device=dev)
+    if P == 0:
+        z = lambda *s: torch.zeros(*s, **f32)  # noqa: E731
+        return (z(0, 3), z(0, 3), z(0, inp.F_user), z(0, 1), z(0, 3), z(0, 6), z(0, inp.M, 3),
+                z(0, 3), z(0, 4))
+    cams, C, keep = _camera_batch(dev, background, viewmatrices, projmatrices, campos, c_x, c_y, tan_fovx,
+                                  tan_fovy, W, H)
+    g = inp.struct()
+    if grad_mask is not None:
+        gm = grad_mask.to(device=dev, dtype=torch.float32).reshape(-1).contiguous()
+        if gm.numel() != P:
+            raise RuntimeError(f"grad_mask must have {P} elements, got {gm.numel()}")
+        g.grad_mask = gm.data_ptr()
+
+    def img(t, ch, name):
+        if not _present(t):
+            return None
+        t = _dev(t, dev, name).reshape(C, -1, H, W)
+        if t.size(1) < ch:
+            t = torch.cat([t, torch.zeros(C, ch - t.size(1), H, W, **f32)], 1)
+        return t.contiguous()
+    dLc = img(dL_dout_color, 3, "dL_dout_color")
+    dLd = img(dL_dout_depth, 1, "dL_dout_depth")
+    dLa = img(dL_dout_alpha, 1, "dL_dout_alpha")
+    dLf = img(dL_dout_feature, inp.F, "dL_dout_feature") if inp.F else None
+    alphas_c = _dev(alphas, dev, "alpha")
+    radii_c = radii.to(device=dev, dtype=torch.int32).contiguous()
+    if tuple(radii_c.shape) != (C, P):
+        raise RuntimeError(f"radii must be [C={C}, P={P}]")
+    out = backward_buffers(P, inp.F, inp.M, dev)
+    if densify is not None:
+        for t in densify:
+            if tuple(t.shape) != (P,) or t.dtype != torch.float32 or t.device != dev or not t.is_contiguous():
+                raise RuntimeError(f"densify statistics must be contiguous fp32 ({P},) tensors on {dev}")
+        g.densify_accum, g.densify_denom, g.max_radius = (t.data_ptr() for t in densify)
+    NI = (ctypes.c_int64 * C)(*[int(x) for x in num_instances])
+    scratch = torch.empty(L_.gs_batch_backward_scratch_bytes(P, inp.F, C), dtype=torch.uint8, device=dev)
+    stream = _stream(dev)
+    p = lambda t: t.data_ptr() if (t is not None and t.numel()) else None  # noqa: E731
+    check(L_.gs_backward_batch(ctypes.byref(g), cams, C, radii_c.data_ptr(), int(bool(debug)), cm,
+                               geomBuffer.data_ptr(), p(binningBuffer), imageBuffer.data_ptr(), NI,
+                               alphas_c.data_ptr(), p(dLc), p(dLf), p(dLd), p(dLa), scratch.data_ptr(),
+                               out["dmeans2D"].data_ptr(), out["dcolors"].data_ptr(), p(out["dsem"]),
+                               out["dopacity"].data_ptr(), out["dmeans3D"].data_ptr(), out["dcov3D"].data_ptr(),
+                               p(out["dsh"]), out["dscales"].data_ptr(), out["drot"].data_ptr(), stream),
+          "rasterize_gaussians_batch_backward")
+    del keep
+    dsem = out["dsem"][:, :inp.F_user] if inp.F_user != inp.F else out["dsem"]
+    return (out["dmeans2D"], out["dcolors"], dsem, out["dopacity"], out["dmeans3D"],
+            out["dcov3D"], out["dsh"], out["dscales"], out["drot"])

@@ -16,7 +16,7 @@ _lock = threading.Lock()
 _lib = None
 
 c_void_p = ctypes.c_void_p
-ABI_VERSION = 6  # include/gsplat_hip.h GS_ABI_VERSION
+ABI_VERSION = 7  # include/gsplat_hip.h GS_ABI_VERSION
 GS_FLAG_ACCUMULATE = 1  # include/gsplat_hip.h
 c_int32, c_int64, c_float, c_size_t = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_size_t
 
@@ -88,6 +88,20 @@ PROTOTYPES = {
                                    c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "gs_batch_geom_buffer_bytes": (c_size_t, [c_int64, c_int32]),
+    "gs_batch_image_buffer_bytes": (c_size_t, [c_int32, c_int32, c_int32]),
+    "gs_batch_binning_buffer_bytes": (c_size_t, [c_int32, ctypes.POINTER(c_int64)]),
+    "gs_batch_backward_scratch_bytes": (c_size_t, [c_int64, c_int32, c_int32]),
+    "gs_forward_plan_batch": (ctypes.c_int, [P_G, P_C, c_int32, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                             c_void_p, c_void_p, c_void_p, ctypes.POINTER(c_int64),
+                                             ctypes.POINTER(c_int64), c_void_p]),
+    "gs_forward_render_batch": (ctypes.c_int, [P_G, P_C, c_int32, ctypes.c_int, ctypes.c_int, c_void_p,
+                                               c_void_p, c_void_p, ctypes.POINTER(c_int64), c_void_p, c_void_p,
+                                               c_void_p, c_void_p, c_void_p, c_void_p]),
+    "gs_backward_batch": (ctypes.c_int, [P_G, P_C, c_int32, c_void_p, ctypes.c_int, ctypes.c_int, c_void_p,
+                                         c_void_p, c_void_p, ctypes.POINTER(c_int64), c_void_p, c_void_p,
+                                         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "gs_mark_visible": (ctypes.c_int, [c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "gs_debug_export": (ctypes.c_int, [c_int64, c_int32, c_int32, c_void_p, c_void_p, c_void_p,
                                        c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

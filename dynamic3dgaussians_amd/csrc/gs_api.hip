@@ -129,8 +129,9 @@ struct StageTimer {
 // that gs_forward_render can size its sort launch without another readback.
 struct PlanInfo {
   const void* image = nullptr;
-  int64_t L = -1;
-  int64_t max_len = -1;
+  int C = 0;
+  int64_t L = -1;        // the batch's total list instances
+  int64_t max_len = -1;  // its longest tile
 };
 thread_local PlanInfo g_plan;
 
@@ -191,25 +192,68 @@ const char* gs_last_error(void) { return g_err.c_str(); }
 size_t gs_geom_buffer_bytes(int64_t P) { return GeomLayout(P > 0 ? P : 0).total; }
 size_t gs_binning_buffer_bytes(int64_t L) { return BinLayout(L > 0 ? L : 0).total; }
 size_t gs_image_buffer_bytes(int32_t W, int32_t H) { return ImgLayout(W, H).total; }
-size_t gs_backward_scratch_bytes(int64_t P, int32_t F) {
-  (void)F;
-  return align_up(sizeof(float) * (size_t)ACC_STRIDE * (size_t)(P > 0 ? P : 0), 256) + 256;
+size_t gs_backward_scratch_bytes(int64_t P, int32_t F) { return gs_batch_backward_scratch_bytes(P, F, 1); }
+
+// ---- forward / backward: camera batches (C = 1: the reference's entry points)
+
+// The batch's CamBatch from C gs_camera blocks: matrices contiguous per
+// camera (camera c's at camera 0's + 16 c / + 3 c), one shared background.
+static int make_batch(const gs_camera* cams, int C, int P, int W, int H, CamBatch& cb) {
+  if (C < 1 || C > GS_MAX_CAMS) return fail(-1, "camera batch size %d outside 1..%d", C, GS_MAX_CAMS);
+  cb = CamBatch{};
+  cb.C = C;
+  cb.geom_stride = (int64_t)GeomLayout(P).total;
+  cb.img_stride = (int64_t)ImgLayout(W, H).total;
+  cb.view = cams[0].viewmatrix;
+  cb.proj = cams[0].projmatrix;
+  cb.campos = cams[0].campos;
+  for (int c = 0; c < C; ++c) {
+    const gs_camera& k = cams[c];
+    if (k.image_width != W || k.image_height != H)
+      return fail(-1, "camera %d: every camera of a batch has the image size of camera 0", c);
+    if (k.viewmatrix != cb.view + 16 * c || k.projmatrix != cb.proj + 16 * c || k.campos != cb.campos + 3 * c)
+      return fail(-1, "camera %d: batch camera matrices must be contiguous ([C,16], [C,16], [C,3])", c);
+    if (k.background != cams[0].background)
+      return fail(-1, "camera %d: the cameras of a batch share one background", c);
+    cb.c_x[c] = k.c_x;
+    cb.c_y[c] = k.c_y;
+    cb.tanx[c] = k.tan_fovx;
+    cb.tany[c] = k.tan_fovy;
+  }
+  return 0;
 }
 
-int gs_forward_plan(const gs_gaussians* g, const gs_camera* cam, int prefiltered, int debug, int compat,
-                    void* geom, void* image, int32_t* radii, int64_t* num_rendered, int64_t* num_instances,
-                    gs_stream_t stream) {
-  if (int e = check_gaussians(g, cam, true)) return e;
+// Binning buffer offsets of the cameras (each a BinLayout of its own length).
+static int64_t batch_bin_offsets(int C, const int64_t* L, CamBatch* cb) {
+  int64_t o = 0;
+  for (int c = 0; c < C; ++c) {
+    const int64_t l = L ? (L[c] > 0 ? L[c] : 0) : 0;
+    if (cb) {
+      cb->bin_off[c] = o;
+      cb->bin_L[c] = l;
+    }
+    o += (int64_t)BinLayout(l).total;
+  }
+  return o;
+}
+
+static int plan_impl(const gs_gaussians* g, const gs_camera* cams, int C, int prefiltered, int debug, int compat,
+                     void* geom, void* image, int32_t* radii, int64_t* num_rendered, int64_t* num_instances,
+                     hipStream_t s) {
+  if (int e = check_gaussians(g, cams, true)) return e;
   if (!num_rendered) return fail(-1, "num_rendered is null");
-  *num_rendered = 0;
-  if (num_instances) *num_instances = 0;
+  for (int c = 0; c < C; ++c) {
+    num_rendered[c] = 0;
+    if (num_instances) num_instances[c] = 0;
+  }
   g_plan = PlanInfo{};
   const int P = g->P;
   if (P == 0) return 0;
   if (!geom || !image || !radii) return fail(-1, "geom buffer, image buffer and radii are required");
-  hipStream_t s = (hipStream_t)stream;
+  const int W = cams[0].image_width, H = cams[0].image_height;
+  CamBatch cb;
+  if (int e = make_batch(cams, C, P, W, H, cb)) return e;
   const GeomLayout gl(P);
-  const int W = cam->image_width, H = cam->image_height;
   const TileArgs ta = tile_args(P, W, H, geom, image);
   PreprocessArgs a{};
   a.P = P; a.D = g->D; a.M = g->M; a.W = W; a.H = H;
@@ -217,11 +261,7 @@ int gs_forward_plan(const gs_gaussians* g, const gs_camera* cam, int prefiltered
   a.prefiltered = prefiltered;
   a.means3D = g->means3D; a.scales = g->scales; a.rotations = g->rotations; a.opacities = g->opacities;
   a.shs = g->shs; a.cov3D_precomp = g->cov3D_precomp; a.colors_precomp = g->colors_precomp;
-  a.view = cam->viewmatrix; a.proj = cam->projmatrix; a.campos = cam->campos;
   a.scale_modifier = g->scale_modifier;
-  a.c_x = cam->c_x; a.c_y = cam->c_y; a.tan_fovx = cam->tan_fovx; a.tan_fovy = cam->tan_fovy;
-  a.focal_y = (float)H / (2.0f * cam->tan_fovy);  // CR/rasterizer_impl.cu:227-228
-  a.focal_x = (float)W / (2.0f * cam->tan_fovx);
   a.radii = radii;
   a.rec = at<float>(geom, gl.rec);
   a.cov3D = at<float>(geom, gl.cov3D);
@@ -229,131 +269,138 @@ int gs_forward_plan(const gs_gaussians* g, const gs_camera* cam, int prefiltered
   a.tiles = at<uint32_t>(geom, gl.tiles);
   a.rect = at<uint16_t>(geom, gl.rect);
   a.status = reinterpret_cast<int*>(ta.meta + M_STATUS);
-  if (prefiltered) (void)hipMemsetAsync(a.status, 0, 4, s);  // culled-but-prefiltered flag
+  if (prefiltered)  // culled-but-prefiltered flags
+    for (int c = 0; c < C; ++c) (void)hipMemsetAsync(shift_bytes(a.status, c * cb.img_stride), 0, 4, s);
   {
     StageTimer t(s, GS_STAGE_PREPROCESS);
-    launch_preprocess_fwd(a, s);
+    launch_preprocess_fwd(a, cb, s);
   }
   if (int e = check("preprocess", debug, s)) return e;
   {
     StageTimer t(s, GS_STAGE_SCAN);
-    launch_tile_plan(ta, prefiltered, s);
+    launch_tile_plan(ta, cb, prefiltered, s);
   }
   if (int e = check("tile plan", debug, s)) return e;
-  // The one host read of the forward (CR/rasterizer_impl.cu:287): the list
-  // instance count sizes the binning buffer; the reference's count and the
-  // rest of the header ride along.
-  uint32_t host[4] = {0, 0, 0, 0};
-  hipError_t he = hipMemcpyAsync(host, ta.meta, sizeof(host), hipMemcpyDeviceToHost, s);
+  // The one host read of the forward (CR/rasterizer_impl.cu:287), one for
+  // the whole batch: the list instance counts size the binning buffer; the
+  // reference's counts and the rest of the headers ride along.
+  uint32_t host[GS_MAX_CAMS][4];
+  hipError_t he = hipMemcpy2DAsync(host, sizeof(host[0]), ta.meta, (size_t)cb.img_stride, sizeof(host[0]), C,
+                                   hipMemcpyDeviceToHost, s);
   if (he == hipSuccess) he = hipStreamSynchronize(s);
   if (he != hipSuccess) return fail((int)he, "num_rendered readback: %s", hipGetErrorString(he));
-  if (prefiltered && (host[M_STATUS] & 1u))
-    return fail(-2, "Point is filtered although prefiltered is set. This shouldn't happen!");
-  if (host[M_STATUS] & 2u) return fail(-1, "more than 2^32 tile instances");
-  *num_rendered = host[M_LREF];
-  if (num_instances) *num_instances = host[M_L];
+  int64_t max_len = 0, total = 0;
+  for (int c = 0; c < C; ++c) {
+    if (prefiltered && (host[c][M_STATUS] & 1u))
+      return fail(-2, "Point is filtered although prefiltered is set. This shouldn't happen!");
+    if (host[c][M_STATUS] & 2u) return fail(-1, "more than 2^32 tile instances");
+    num_rendered[c] = host[c][M_LREF];
+    if (num_instances) num_instances[c] = host[c][M_L];
+    max_len = host[c][M_MAXN] > max_len ? host[c][M_MAXN] : max_len;
+    total += host[c][M_L];
+  }
   g_plan.image = image;
-  g_plan.L = host[M_L];
-  g_plan.max_len = host[M_MAXN];
+  g_plan.C = C;
+  g_plan.L = total;
+  g_plan.max_len = max_len;
   (void)compat;
   return 0;
 }
 
-int gs_forward_render(const gs_gaussians* g, const gs_camera* cam, int debug, int compat, void* geom,
-                      void* binning, void* image, int64_t L, const int32_t* radii, float* out_color,
-                      float* out_feature, float* out_depth, float* out_alpha, gs_stream_t stream) {
-  if (int e = check_gaussians(g, cam, true)) return e;
+static int render_impl(const gs_gaussians* g, const gs_camera* cams, int C, int debug, int compat, void* geom,
+                       void* binning, void* image, const int64_t* L, const int32_t* radii, float* out_color,
+                       float* out_feature, float* out_depth, float* out_alpha, hipStream_t s) {
+  if (int e = check_gaussians(g, cams, true)) return e;
   const int P = g->P;
   if (P == 0) return 0;  // the reference leaves the zero-filled outputs untouched
-  if (!geom || !image || (L > 0 && !binning) || !radii) return fail(-1, "state buffers are required");
+  int64_t total = 0;
+  for (int c = 0; c < C; ++c) total += L[c] > 0 ? L[c] : 0;
+  if (!geom || !image || (total > 0 && !binning) || !radii) return fail(-1, "state buffers are required");
   if (!out_color || !out_depth || (g->F > 0 && !out_feature) || (compat != COMPAT_REFERENCE && !out_alpha))
     return fail(-1, "output image pointers are required");
-  hipStream_t s = (hipStream_t)stream;
-  const int W = cam->image_width, H = cam->image_height;
+  const int W = cams[0].image_width, H = cams[0].image_height;
+  CamBatch cb;
+  if (int e = make_batch(cams, C, P, W, H, cb)) return e;
+  batch_bin_offsets(C, L, &cb);
   const int gx = (W + TILE - 1) / TILE, gy = (H + TILE - 1) / TILE;
   const GeomLayout gl(P);
-  const BinLayout bl(L);
   const ImgLayout il(W, H);
   const float* rec = at<float>(geom, gl.rec);
   TileArgs ta = tile_args(P, W, H, geom, image);
-  ta.keys = L > 0 ? at<uint64_t>(binning, bl.keys) : nullptr;
-  ta.keys2 = L > 0 ? at<uint64_t>(binning, bl.keys2) : nullptr;
-  ta.plist = L > 0 ? at<uint32_t>(binning, bl.plist) : nullptr;
-  const uint2* ranges = ta.ranges;
-  const uint32_t* point_list = ta.plist;
-  launch_tile_order(ta, s);
-  if (L > 0) {
+  ta.binning = total > 0 ? binning : nullptr;
+  launch_tile_order(ta, cb, s);
+  if (total > 0) {
     {
       StageTimer t(s, GS_STAGE_DUPLICATE);
-      launch_tile_bucket(ta, s);
+      launch_tile_bucket(ta, cb, s);
     }
     if (int e = check("duplicateWithKeys", debug, s)) return e;
-    const bool known = g_plan.image == image && g_plan.L == L;
+    const bool known = g_plan.image == image && g_plan.C == C && g_plan.L == total;
     {
       StageTimer t(s, GS_STAGE_SORT);
-      launch_tile_sort(ta, known ? g_plan.max_len : -1, L, s);
+      launch_tile_sort(ta, cb, known ? g_plan.max_len : -1, total, s);
     }
     if (int e = check("tile sort", debug, s)) return e;
   }
   RenderArgs ra{};
   ra.W = W; ra.H = H; ra.grid_x = gx; ra.num_tiles = gx * gy; ra.F = g->F; ra.compat = compat;
   ra.order = ta.order;
-  ra.ranges = ranges; ra.point_list = point_list; ra.rec = rec; ra.feats = g->semantic_feature;
-  ra.bg = cam->background;
+  ra.ranges = ta.ranges; ra.point_list = total > 0 ? static_cast<const uint32_t*>(binning) : nullptr;
+  ra.rec = rec; ra.feats = g->semantic_feature;
+  ra.bg = cams[0].background;
   ra.out_color = out_color; ra.out_feature = out_feature; ra.out_depth = out_depth; ra.out_alpha = out_alpha;
   ra.n_contrib = at<uint32_t>(image, il.n_contrib);
   {
     StageTimer t(s, GS_STAGE_RENDER_FWD);
-    if (!launch_render_fwd(ra, s)) return fail(-1, "unsupported feature width %d", g->F);
+    if (!launch_render_fwd(ra, cb, s)) return fail(-1, "unsupported feature width %d", g->F);
   }
   return check("render", debug, s);
 }
 
-int gs_backward(const gs_gaussians* g, const gs_camera* cam, const int32_t* radii, int debug, int compat,
-                const void* geom, const void* binning, const void* image, int64_t L, const float* alphas,
-                const float* dL_dout_color, const float* dL_dout_feature, const float* dL_dout_depth,
-                const float* dL_dout_alpha, void* scratch, float* dL_dmeans2D, float* dL_dcolors,
-                float* dL_dsemantic, float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh,
-                float* dL_dscales, float* dL_drotations, gs_stream_t stream) {
-  if (int e = check_gaussians(g, cam, false)) return e;
+static int backward_impl(const gs_gaussians* g, const gs_camera* cams, int C, const int32_t* radii, int debug,
+                         int compat, const void* geom, const void* binning, const void* image, const int64_t* L,
+                         const float* alphas, const float* dL_dout_color, const float* dL_dout_feature,
+                         const float* dL_dout_depth, const float* dL_dout_alpha, void* scratch, float* dL_dmeans2D,
+                         float* dL_dcolors, float* dL_dsemantic, float* dL_dopacity, float* dL_dmeans3D,
+                         float* dL_dcov3D, float* dL_dsh, float* dL_dscales, float* dL_drotations, hipStream_t s) {
+  if (int e = check_gaussians(g, cams, false)) return e;
   const int P = g->P;
   if (P == 0) return 0;
-  // L (num_rendered) is not needed: the tile lists sit at the start of the
-  // binning buffer and the ranges say how long they are (an empty binning
-  // buffer means every list is empty)
-  (void)L;
   if (!geom || !image || !scratch || !radii) return fail(-1, "state buffers are required");
   if (!alphas) return fail(-1, "the forward's alpha image is required");
   if (!dL_dmeans2D || !dL_dcolors || !dL_dopacity || !dL_dmeans3D || !dL_dcov3D || !dL_dscales ||
       !dL_drotations || (g->F > 0 && !dL_dsemantic) || (g->M > 0 && !dL_dsh))
     return fail(-1, "gradient outputs are required");
-  hipStream_t s = (hipStream_t)stream;
-  const int W = cam->image_width, H = cam->image_height;
+  const int W = cams[0].image_width, H = cams[0].image_height;
+  CamBatch cb;
+  if (int e = make_batch(cams, C, P, W, H, cb)) return e;
+  // the tile lists sit at the start of each camera's binning buffer and the
+  // ranges say how long they are (an empty binning buffer: every list empty)
+  batch_bin_offsets(C, L, &cb);
   const int gx = (W + TILE - 1) / TILE, gy = (H + TILE - 1) / TILE;
   const GeomLayout gl(P);
-  const BinLayout bl(L);
   const ImgLayout il(W, H);
   float* acc = static_cast<float*>(scratch);
-  (void)hipMemsetAsync(acc, 0, sizeof(float) * (size_t)ACC_STRIDE * P, s);
+  (void)hipMemsetAsync(acc, 0, sizeof(float) * (size_t)ACC_STRIDE * P * C, s);
   const bool accumulate = (g->flags & GS_FLAG_ACCUMULATE) != 0;
   // the blend kernel adds the feature gradients atomically: zero first unless
   // the output already holds the sums to add to
   if (g->F > 0 && !accumulate) (void)hipMemsetAsync(dL_dsemantic, 0, sizeof(float) * (size_t)g->F * P, s);
   RenderBwdArgs ra{};
-  ra.W = W; ra.H = H; ra.grid_x = gx; ra.num_tiles = gx * gy; ra.F = g->F; ra.compat = compat;
+  ra.W = W; ra.H = H; ra.grid_x = gx; ra.num_tiles = gx * gy; ra.F = g->F; ra.compat = compat; ra.P = P;
   ra.order = at<uint32_t>(image, il.order);
   ra.ranges = at<uint2>(image, il.ranges);
-  ra.point_list = binning ? at<uint32_t>(binning, bl.plist) : nullptr;
+  ra.point_list = static_cast<const uint32_t*>(binning);
   ra.rec = at<float>(geom, gl.rec);
   ra.feats = g->semantic_feature;
-  ra.bg = cam->background;
+  ra.bg = cams[0].background;
   ra.alphas = alphas;
   ra.n_contrib = at<uint32_t>(image, il.n_contrib);
   ra.dL_dpix = dL_dout_color; ra.dL_dfeat = dL_dout_feature; ra.dL_ddepth = dL_dout_depth;
   ra.dL_dalpha = dL_dout_alpha; ra.acc = acc; ra.dsem = dL_dsemantic;
   {
     StageTimer t(s, GS_STAGE_RENDER_BWD);
-    if (!launch_render_bwd(ra, s)) return fail(-1, "unsupported feature width %d", g->F);
+    if (!launch_render_bwd(ra, cb, s)) return fail(-1, "unsupported feature width %d", g->F);
   }
   if (int e = check("render backward", debug, s)) return e;
   PreprocessBwdArgs b{};
@@ -361,12 +408,9 @@ int gs_backward(const gs_gaussians* g, const gs_camera* cam, const int32_t* radi
   b.accumulate = accumulate ? 1 : 0;
   b.means3D = g->means3D; b.radii = radii; b.shs = g->shs; b.clamped = at<uint8_t>(geom, gl.clamped);
   b.scales = g->scales; b.rotations = g->rotations;
-  b.cov3D = g->cov3D_precomp ? g->cov3D_precomp : at<float>(geom, gl.cov3D);
-  b.view = cam->viewmatrix; b.proj = cam->projmatrix; b.campos = cam->campos;
+  b.cov3D = at<float>(geom, gl.cov3D);
+  b.cov3D_precomp = g->cov3D_precomp;
   b.scale_modifier = g->scale_modifier;
-  b.c_x = cam->c_x; b.c_y = cam->c_y; b.tan_fovx = cam->tan_fovx; b.tan_fovy = cam->tan_fovy;
-  b.focal_y = (float)H / (2.0f * cam->tan_fovy);  // CR/rasterizer_impl.cu:398-399
-  b.focal_x = (float)W / (2.0f * cam->tan_fovx);
   b.acc = acc;
   b.rec = at<float>(geom, gl.rec);
   b.grad_mask = g->grad_mask;
@@ -376,9 +420,86 @@ int gs_backward(const gs_gaussians* g, const gs_camera* cam, const int32_t* radi
   b.drot = dL_drotations;
   {
     StageTimer t(s, GS_STAGE_PREPROCESS_BWD);
-    launch_preprocess_bwd(b, s);
+    launch_preprocess_bwd(b, cb, s);
   }
   return check("preprocess backward", debug, s);
+}
+
+int gs_forward_plan(const gs_gaussians* g, const gs_camera* cam, int prefiltered, int debug, int compat,
+                    void* geom, void* image, int32_t* radii, int64_t* num_rendered, int64_t* num_instances,
+                    gs_stream_t stream) {
+  if (!cam) return fail(-1, "null argument block");
+  return plan_impl(g, cam, 1, prefiltered, debug, compat, geom, image, radii, num_rendered, num_instances,
+                   (hipStream_t)stream);
+}
+
+int gs_forward_render(const gs_gaussians* g, const gs_camera* cam, int debug, int compat, void* geom,
+                      void* binning, void* image, int64_t L, const int32_t* radii, float* out_color,
+                      float* out_feature, float* out_depth, float* out_alpha, gs_stream_t stream) {
+  if (!cam) return fail(-1, "null argument block");
+  return render_impl(g, cam, 1, debug, compat, geom, binning, image, &L, radii, out_color, out_feature, out_depth,
+                     out_alpha, (hipStream_t)stream);
+}
+
+int gs_backward(const gs_gaussians* g, const gs_camera* cam, const int32_t* radii, int debug, int compat,
+                const void* geom, const void* binning, const void* image, int64_t L, const float* alphas,
+                const float* dL_dout_color, const float* dL_dout_feature, const float* dL_dout_depth,
+                const float* dL_dout_alpha, void* scratch, float* dL_dmeans2D, float* dL_dcolors,
+                float* dL_dsemantic, float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh,
+                float* dL_dscales, float* dL_drotations, gs_stream_t stream) {
+  if (!cam) return fail(-1, "null argument block");
+  // L (num_rendered) is not needed: one camera's tile lists start the binning buffer
+  (void)L;
+  const int64_t L0 = 0;
+  return backward_impl(g, cam, 1, radii, debug, compat, geom, binning, image, &L0, alphas, dL_dout_color,
+                       dL_dout_feature, dL_dout_depth, dL_dout_alpha, scratch, dL_dmeans2D, dL_dcolors,
+                       dL_dsemantic, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations,
+                       (hipStream_t)stream);
+}
+
+size_t gs_batch_geom_buffer_bytes(int64_t P, int32_t C) { return GeomLayout(P > 0 ? P : 0).total * (C > 0 ? C : 0); }
+size_t gs_batch_image_buffer_bytes(int32_t W, int32_t H, int32_t C) { return ImgLayout(W, H).total * (C > 0 ? C : 0); }
+size_t gs_batch_binning_buffer_bytes(int32_t C, const int64_t* num_instances) {
+  if (C < 1 || C > GS_MAX_CAMS || !num_instances) return 0;
+  return (size_t)batch_bin_offsets(C, num_instances, nullptr);
+}
+size_t gs_batch_backward_scratch_bytes(int64_t P, int32_t F, int32_t C) {
+  (void)F;
+  return align_up(sizeof(float) * (size_t)ACC_STRIDE * (size_t)(P > 0 ? P : 0) * (C > 0 ? C : 0), 256) + 256;
+}
+
+int gs_forward_plan_batch(const gs_gaussians* g, const gs_camera* cams, int32_t C, int prefiltered, int debug,
+                          int compat, void* geom, void* image, int32_t* radii, int64_t* num_rendered,
+                          int64_t* num_instances, gs_stream_t stream) {
+  if (!cams) return fail(-1, "null argument block");
+  if (C < 1 || C > GS_MAX_CAMS) return fail(-1, "camera batch size %d outside 1..%d", C, GS_MAX_CAMS);
+  return plan_impl(g, cams, C, prefiltered, debug, compat, geom, image, radii, num_rendered, num_instances,
+                   (hipStream_t)stream);
+}
+
+int gs_forward_render_batch(const gs_gaussians* g, const gs_camera* cams, int32_t C, int debug, int compat,
+                            void* geom, void* binning, void* image, const int64_t* num_instances,
+                            const int32_t* radii, float* out_color, float* out_feature, float* out_depth,
+                            float* out_alpha, gs_stream_t stream) {
+  if (!cams || !num_instances) return fail(-1, "null argument block");
+  if (C < 1 || C > GS_MAX_CAMS) return fail(-1, "camera batch size %d outside 1..%d", C, GS_MAX_CAMS);
+  return render_impl(g, cams, C, debug, compat, geom, binning, image, num_instances, radii, out_color,
+                     out_feature, out_depth, out_alpha, (hipStream_t)stream);
+}
+
+int gs_backward_batch(const gs_gaussians* g, const gs_camera* cams, int32_t C, const int32_t* radii, int debug,
+                      int compat, const void* geom, const void* binning, const void* image,
+                      const int64_t* num_instances, const float* alphas, const float* dL_dout_color,
+                      const float* dL_dout_feature, const float* dL_dout_depth, const float* dL_dout_alpha,
+                      void* scratch, float* dL_dmeans2D, float* dL_dcolors, float* dL_dsemantic,
+                      float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscales,
+                      float* dL_drotations, gs_stream_t stream) {
+  if (!cams || !num_instances) return fail(-1, "null argument block");
+  if (C < 1 || C > GS_MAX_CAMS) return fail(-1, "camera batch size %d outside 1..%d", C, GS_MAX_CAMS);
+  return backward_impl(g, cams, C, radii, debug, compat, geom, binning, image, num_instances, alphas,
+                       dL_dout_color, dL_dout_feature, dL_dout_depth, dL_dout_alpha, scratch, dL_dmeans2D,
+                       dL_dcolors, dL_dsemantic, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales,
+                       dL_drotations, (hipStream_t)stream);
 }
 
 int gs_mark_visible(int64_t P, const float* means3D, const float* viewmatrix, const float* projmatrix,

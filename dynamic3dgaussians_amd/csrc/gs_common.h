@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace gs {
 
 // Binning tile = 16x16 pixels, identical to the reference (CR/config.h:18-19)
@@ -154,6 +156,32 @@ struct ImgLayout {
     total = o;
   }
 };
+
+// ---------------------------------------------------------------- camera batches
+// A multi-camera batch: C cameras of one image size over one Gaussian set
+// (the per-timestep multi-camera step).  Every per-camera buffer is the
+// single-camera layout repeated: geometry and image buffers at a fixed
+// stride, binning buffers at host-computed offsets (their lengths differ),
+// images and radii [C, ...].  Kernels take the camera from blockIdx.y (or
+// the minor index of a flattened grid); the single-camera entry points are
+// the C = 1 case.  Camera parameters ride in the kernel arguments.
+constexpr int GS_MAX_CAMS = 64;
+struct CamBatch {
+  int C;
+  int64_t geom_stride;   // bytes between the cameras' geometry buffers
+  int64_t img_stride;    // bytes between the cameras' image buffers
+  const float* view;     // C x 16 column-major 4x4 (device)
+  const float* proj;     // C x 16
+  const float* campos;   // C x 3
+  float c_x[GS_MAX_CAMS], c_y[GS_MAX_CAMS], tanx[GS_MAX_CAMS], tany[GS_MAX_CAMS];
+  int64_t bin_off[GS_MAX_CAMS];  // byte offset of camera c's binning buffer
+  int64_t bin_L[GS_MAX_CAMS];    // camera c's tile-list length (instances)
+};
+template <class T>
+__host__ __device__ inline T* shift_bytes(T* p, int64_t bytes) {
+  return p ? reinterpret_cast<T*>(reinterpret_cast<char*>(const_cast<typename std::remove_const<T>::type*>(p)) + bytes)
+           : p;
+}
 
 // ---------------------------------------------------------------- device math
 

@@ -6,6 +6,8 @@
 #include "../../include/gs_optim.h"
 #include <stdint.h>
 
+#include "gs_common.h"
+
 namespace gs {
 
 struct PreprocessArgs {
@@ -39,7 +41,8 @@ struct PreprocessBwdArgs {
   const uint8_t* clamped;
   const float* scales;
   const float* rotations;
-  const float* cov3D;  // precomputed or the forward's
+  const float* cov3D;          // the forward's (geometry buffer of camera 0; per camera at geom_stride)
+  const float* cov3D_precomp;  // the caller's, or null
   const float* view;
   const float* proj;
   const float* campos;
@@ -77,7 +80,7 @@ struct RenderArgs {
 };
 
 struct RenderBwdArgs {
-  int W, H, grid_x, num_tiles, F, compat;
+  int W, H, grid_x, num_tiles, F, compat, P;
   const uint32_t* order;  // num_tiles: dispatch order of the tiles (longest list first)
   const uint2* ranges;
   const uint32_t* point_list;
@@ -94,8 +97,8 @@ struct RenderBwdArgs {
   float* dsem;  // P x F semantic-feature gradients (the output), zeroed (or holding earlier sums) by the caller
 };
 
-void launch_preprocess_fwd(const PreprocessArgs& a, hipStream_t s);
-void launch_preprocess_bwd(const PreprocessBwdArgs& a, hipStream_t s);
+void launch_preprocess_fwd(const PreprocessArgs& a, const CamBatch& cb, hipStream_t s);
+void launch_preprocess_bwd(const PreprocessBwdArgs& a, const CamBatch& cb, hipStream_t s);
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t s);
 
 // Stable LSD radix sort on bits [0, end_bit) (the standalone gs_sort_pairs
@@ -119,18 +122,74 @@ struct TileArgs {
   uint64_t* keys;        // L
   uint64_t* keys2;       // L (sort twin for long tiles)
   uint32_t* plist;       // L
+  void* binning;         // binning buffer base (batch: camera c at CamBatch::bin_off[c]), or null
 };
+// TileArgs of camera c of a batch (pointers of camera 0 -> camera c).
+__host__ __device__ inline TileArgs cam_tile_args(const TileArgs& a0, const CamBatch& cb, int c) {
+  TileArgs a = a0;
+  const int64_t go = c * cb.geom_stride, io = c * cb.img_stride;
+  a.rect = shift_bytes(a0.rect, go);
+  a.tiles = shift_bytes(a0.tiles, go);
+  a.rec = shift_bytes(a0.rec, go);
+  a.thist = shift_bytes(a0.thist, io);
+  a.ttotal = shift_bytes(a0.ttotal, io);
+  a.bsum = shift_bytes(a0.bsum, io);
+  a.meta = shift_bytes(a0.meta, io);
+  a.ranges = shift_bytes(a0.ranges, io);
+  a.order = shift_bytes(a0.order, io);
+  if (a0.binning) {
+    char* b = static_cast<char*>(a0.binning) + cb.bin_off[c];
+    const BinLayout bl(cb.bin_L[c]);
+    a.plist = reinterpret_cast<uint32_t*>(b + bl.plist);
+    a.keys = reinterpret_cast<uint64_t*>(b + bl.keys);
+    a.keys2 = reinterpret_cast<uint64_t*>(b + bl.keys2);
+  }
+  return a;
+}
 // plan: per-block tile histograms, tile totals and offsets, ranges, header
-void launch_tile_plan(const TileArgs& a, int prefiltered, hipStream_t s);
+void launch_tile_plan(const TileArgs& a, const CamBatch& cb, int prefiltered, hipStream_t s);
 // render: bucket the instances by tile, then sort every tile by (depth, id).
 // max_len = the plan header's longest tile (host copy), or -1 if unknown.
-void launch_tile_bucket(const TileArgs& a, hipStream_t s);
+void launch_tile_bucket(const TileArgs& a, const CamBatch& cb, hipStream_t s);
 // dispatch order of the blend / sort kernels (tiles by descending list length)
-void launch_tile_order(const TileArgs& a, hipStream_t s);
-void launch_tile_sort(const TileArgs& a, int64_t max_len, int64_t L, hipStream_t s);
+void launch_tile_order(const TileArgs& a, const CamBatch& cb, hipStream_t s);
+// max_len: the longest tile over the batch (-1: unknown); L: the batch's total instances
+void launch_tile_sort(const TileArgs& a, const CamBatch& cb, int64_t max_len, int64_t L, hipStream_t s);
 
-bool launch_render_fwd(const RenderArgs& a, hipStream_t s);
-bool launch_render_bwd(const RenderBwdArgs& a, hipStream_t s);
+// Camera c of a batch: image-buffer, geometry, binning and image pointers of
+// camera 0 -> camera c (point_list = the batch's binning base).
+__host__ __device__ inline RenderArgs cam_render_args(const RenderArgs& a0, const CamBatch& cb, int c) {
+  RenderArgs a = a0;
+  const int64_t go = c * cb.geom_stride, io = c * cb.img_stride, hw = (int64_t)a0.W * a0.H;
+  a.order = shift_bytes(a0.order, io);
+  a.ranges = shift_bytes(a0.ranges, io);
+  a.n_contrib = shift_bytes(a0.n_contrib, io);
+  a.rec = shift_bytes(a0.rec, go);
+  a.point_list = shift_bytes(a0.point_list, cb.bin_off[c]);
+  a.out_color = a0.out_color ? a0.out_color + c * 3 * hw : nullptr;
+  a.out_feature = a0.out_feature ? a0.out_feature + c * a0.F * hw : nullptr;
+  a.out_depth = a0.out_depth ? a0.out_depth + c * hw : nullptr;
+  a.out_alpha = a0.out_alpha ? a0.out_alpha + c * hw : nullptr;
+  return a;
+}
+__host__ __device__ inline RenderBwdArgs cam_render_bwd_args(const RenderBwdArgs& a0, const CamBatch& cb, int c) {
+  RenderBwdArgs a = a0;
+  const int64_t go = c * cb.geom_stride, io = c * cb.img_stride, hw = (int64_t)a0.W * a0.H;
+  a.order = shift_bytes(a0.order, io);
+  a.ranges = shift_bytes(a0.ranges, io);
+  a.n_contrib = shift_bytes(a0.n_contrib, io);
+  a.rec = shift_bytes(a0.rec, go);
+  a.point_list = shift_bytes(a0.point_list, cb.bin_off[c]);
+  a.alphas = a0.alphas ? a0.alphas + c * hw : nullptr;
+  a.dL_dpix = a0.dL_dpix ? a0.dL_dpix + c * 3 * hw : nullptr;
+  a.dL_dfeat = a0.dL_dfeat ? a0.dL_dfeat + c * a0.F * hw : nullptr;
+  a.dL_ddepth = a0.dL_ddepth ? a0.dL_ddepth + c * hw : nullptr;
+  a.dL_dalpha = a0.dL_dalpha ? a0.dL_dalpha + c * hw : nullptr;
+  a.acc = a0.acc + (size_t)c * a0.P * ACC_STRIDE;
+  return a;
+}
+bool launch_render_fwd(const RenderArgs& a, const CamBatch& cb, hipStream_t s);
+bool launch_render_bwd(const RenderBwdArgs& a, const CamBatch& cb, hipStream_t s);
 
 void launch_test_wave_reduce(int n, const float* in, float* out, hipStream_t s);
 

@@ -167,9 +167,33 @@ __device__ inline void sh_fwd(int deg, int M, V3 p, V3 cp, const float* __restri
 
 // ------------------------------------------------------------------ forward
 
-__global__ __launch_bounds__(256) void preprocess_fwd_kernel(PreprocessArgs a) {
+// Camera c (blockIdx.y) of a batch: its parameters and per-camera outputs.
+__device__ inline PreprocessArgs cam_args(const PreprocessArgs& a0, const CamBatch& cb, int c) {
+  PreprocessArgs a = a0;
+  a.view = cb.view + 16 * c;
+  a.proj = cb.proj + 16 * c;
+  a.campos = cb.campos + 3 * c;
+  a.c_x = cb.c_x[c];
+  a.c_y = cb.c_y[c];
+  a.tan_fovx = cb.tanx[c];
+  a.tan_fovy = cb.tany[c];
+  a.focal_y = (float)a.H / (2.0f * a.tan_fovy);  // CR/rasterizer_impl.cu:227-228
+  a.focal_x = (float)a.W / (2.0f * a.tan_fovx);
+  const int64_t go = c * cb.geom_stride;
+  a.radii = a0.radii + (size_t)c * a0.P;
+  a.rec = shift_bytes(a0.rec, go);
+  a.cov3D = shift_bytes(a0.cov3D, go);
+  a.clamped = shift_bytes(a0.clamped, go);
+  a.tiles = shift_bytes(a0.tiles, go);
+  a.rect = shift_bytes(a0.rect, go);
+  a.status = shift_bytes(a0.status, c * cb.img_stride);
+  return a;
+}
+
+__global__ __launch_bounds__(256) void preprocess_fwd_kernel(PreprocessArgs a0, CamBatch batch) {
   const int g = blockIdx.x * 256 + threadIdx.x;
-  if (g >= a.P) return;
+  if (g >= a0.P) return;
+  const PreprocessArgs a = cam_args(a0, batch, blockIdx.y);
   a.radii[g] = 0;
   a.tiles[g] = 0;
   reinterpret_cast<ushort4*>(a.rect)[g] = make_ushort4(0, 0, 0, 0);
@@ -252,9 +276,9 @@ __global__ __launch_bounds__(256) void preprocess_fwd_kernel(PreprocessArgs a) {
       make_ushort4((uint16_t)bx0, (uint16_t)by0, (uint16_t)bx1, (uint16_t)by1);
 }
 
-void launch_preprocess_fwd(const PreprocessArgs& a, hipStream_t s) {
+void launch_preprocess_fwd(const PreprocessArgs& a, const CamBatch& cb, hipStream_t s) {
   if (a.P <= 0) return;
-  hipLaunchKernelGGL(preprocess_fwd_kernel, dim3((a.P + 255) / 256), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(preprocess_fwd_kernel, dim3((a.P + 255) / 256, cb.C), dim3(256), 0, s, a, cb);
 }
 
 __global__ __launch_bounds__(256) void mark_visible_kernel(int P, const float* __restrict__ means3D,
@@ -377,59 +401,74 @@ __device__ inline void cov3d_bwd(V3 scale, float mod, float4 rot, const float d[
 }
 
 // Fused computeCov2DCUDA + preprocessCUDA backward + scatter of the blend
-// gradients (the per-Gaussian accumulation record) into the output tensors.
-// Every output element is written, so outputs need no zero-fill.
-__global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdArgs a) {
+// gradients (the per-Gaussian accumulation record) into the output tensors,
+// for every camera of the batch: one thread per Gaussian walks the cameras in
+// order and sums their contributions in registers (deterministic, one write
+// per output), so a batch costs one pass over the Gaussian state instead of
+// C read-modify-write passes.  Every output element is written, so outputs
+// need no zero-fill.
+__global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdArgs a, CamBatch cb) {
   const int g = blockIdx.x * 256 + threadIdx.x;
   if (g >= a.P) return;
-  const float* acc = a.acc + (size_t)ACC_STRIDE * g;
-  const bool vis = a.radii[g] > 0;
-  // blend gradients -> output tensors (zero for culled Gaussians: never touched)
-  // dL/dmean2D = sum over pixels of dL/dG * dG/d(offset) * ndc scale
-  // (CR/backward.cu:616-621): from the blend kernel's basis sums (AccField),
-  // the conic and ddelx_dx = 0.5 W, ddely_dy = 0.5 H (:520-521).
-  float am0 = 0.f, am1 = 0.f;
-  float4 con = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (vis) {
-    con = reinterpret_cast<const float4*>(a.rec + (size_t)REC * g)[0];  // x, y, a, b
-    const float cc = a.rec[(size_t)REC * g + R_CC];
-    const float sex = acc[A_MX], sey = acc[A_MY];
-    am0 = (-con.z * sex - con.w * sey) * (0.5f * (float)a.W);
-    am1 = (-cc * sey - con.w * sex) * (0.5f * (float)a.H);
-  }
   const int ac = a.accumulate;
-  gput(a.dmeans2D + 3 * g, am0, ac); gput(a.dmeans2D + 3 * g + 1, am1, ac);
-  if (!ac) a.dmeans2D[3 * g + 2] = 0.f;
-  // densification statistics of this view (external.py:136-140: the norm of
-  // the view's own means2D gradient, as gs_optim.hip's statistics do;
-  // train.py:288-290: the max screen radius); unseen Gaussians add nothing
-  if (a.st_accum) gput(a.st_accum + g, vis ? sqrtf(am0 * am0 + am1 * am1) : 0.f, ac);
-  if (a.st_denom) gput(a.st_denom + g, vis ? 1.f : 0.f, ac);
-  if (a.st_maxrad) {
-    const float r = vis ? (float)a.radii[g] : 0.f;
-    a.st_maxrad[g] = ac ? fmaxf(a.st_maxrad[g], r) : r;
-  }
-  const float dcol[3] = {acc[A_R], acc[A_G], acc[A_B]};
-  // Q12 label mask (DGR/__init__.py:159-173), applied at store time exactly as
-  // the reference's elementwise `grad * label` (the chain rule uses unmasked dcol).
   const bool masked = a.grad_mask != nullptr;
   const float mk = masked ? a.grad_mask[g] : 1.f;
-  gput(a.dcolors + 3 * g, dcol[0] * mk, ac); gput(a.dcolors + 3 * g + 1, dcol[1] * mk, ac);
-  gput(a.dcolors + 3 * g + 2, dcol[2] * mk, ac);
-  gput(a.dopacity + g, acc[A_OP] * mk, ac);
+  const V3 mean = ld3(a.means3D + 3 * g);
+  // camera sums (the first camera assigns, so C = 1 is the single-view value)
+  float am[2] = {0.f, 0.f}, dcol[3] = {0.f, 0.f, 0.f}, dop = 0.f;
   float dm[3] = {0.f, 0.f, 0.f};
   float dcov[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  float dscale[3] = {0.f, 0.f, 0.f}, drot[4] = {0.f, 0.f, 0.f, 0.f};
-  if (vis) {
-    const V3 mean = ld3(a.means3D + 3 * g);
-    const float* c3 = a.cov3D + 6 * g;
+  float st_acc = 0.f, st_den = 0.f, st_rad = 0.f;
+  bool any_vis = false, sh_written = ac != 0;
+  for (int c = 0; c < cb.C; ++c) {
+    const bool first = c == 0;
+    auto add = [&](float& sum, float v) { sum = first ? v : sum + v; };
+    const float* acc = a.acc + ((size_t)c * a.P + g) * ACC_STRIDE;
+    const int rad = a.radii[(size_t)c * a.P + g];
+    const bool vis = rad > 0;
+    const float* rec = shift_bytes(a.rec, c * cb.geom_stride) + (size_t)REC * g;
+    // blend gradients -> output tensors (zero for culled Gaussians: never touched)
+    // dL/dmean2D = sum over pixels of dL/dG * dG/d(offset) * ndc scale
+    // (CR/backward.cu:616-621): from the blend kernel's basis sums (AccField),
+    // the conic and ddelx_dx = 0.5 W, ddely_dy = 0.5 H (:520-521).
+    float am0 = 0.f, am1 = 0.f;
+    if (vis) {
+      const float4 con = reinterpret_cast<const float4*>(rec)[0];  // x, y, a, b
+      const float cc = rec[R_CC];
+      const float sex = acc[A_MX], sey = acc[A_MY];
+      am0 = (-con.z * sex - con.w * sey) * (0.5f * (float)a.W);
+      am1 = (-cc * sey - con.w * sex) * (0.5f * (float)a.H);
+    }
+    add(am[0], am0);
+    add(am[1], am1);
+    // densification statistics of this view (external.py:136-140: the norm of
+    // the view's own means2D gradient, as gs_optim.hip's statistics do;
+    // train.py:288-290: the max screen radius); unseen Gaussians add nothing
+    add(st_acc, vis ? sqrtf(am0 * am0 + am1 * am1) : 0.f);
+    add(st_den, vis ? 1.f : 0.f);
+    st_rad = fmaxf(st_rad, vis ? (float)rad : 0.f);
+    const float dcol_c[3] = {acc[A_R], acc[A_G], acc[A_B]};
+    add(dcol[0], dcol_c[0]);
+    add(dcol[1], dcol_c[1]);
+    add(dcol[2], dcol_c[2]);
+    add(dop, acc[A_OP]);
+    if (!vis) continue;
+    const float* view = cb.view + 16 * c;
+    const float* pr = cb.proj + 16 * c;
+    // the camera scalars exactly as the binding passed them (Q2 in reference
+    // mode: the Python wrapper's swapped order, DGR/__init__.py:130-133)
+    const float c_x = cb.c_x[c], c_y = cb.c_y[c], tan_fovx = cb.tanx[c], tan_fovy = cb.tany[c];
+    const float focal_y = (float)a.H / (2.0f * tan_fovy);  // CR/rasterizer_impl.cu:398-399
+    const float focal_x = (float)a.W / (2.0f * tan_fovx);
+    const float* c3 = a.cov3D_precomp ? a.cov3D_precomp + 6 * g
+                                      : shift_bytes(a.cov3D, c * cb.geom_stride) + 6 * g;
     float c3v[6];
 #pragma unroll
     for (int i = 0; i < 6; ++i) c3v[i] = c3[i];
     // dL/dconic = -1/2 sum e (dx^2, dx dy, dy^2) (CR/backward.cu:622-624)
     const float dcx = -0.5f * acc[A_CA], dcy = -0.5f * acc[A_CB], dcz = -0.5f * acc[A_CC];
     Ewa e;
-    ewa_setup(mean, a.view, a.W, a.H, a.c_x, a.c_y, a.focal_x, a.focal_y, a.tan_fovx, a.tan_fovy, e);
+    ewa_setup(mean, view, a.W, a.H, c_x, c_y, focal_x, focal_y, tan_fovx, tan_fovy, e);
     float xg, yg;
     if (a.compat == COMPAT_REFERENCE) {  // Q3
       xg = (e.txtz < e.lxn || e.txtz > e.lxp) ? 0.f : 1.f;
@@ -440,21 +479,22 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdArgs a
     }
     float cov[3];
     ewa_cov2d(e, c3v, cov);
-    const float ca = cov[0], cb = cov[1], cc = cov[2];
-    const float denom = ca * cc - cb * cb;
+    const float ca = cov[0], cb2 = cov[1], cc = cov[2];
+    const float denom = ca * cc - cb2 * cb2;
     float da = 0, db = 0, dc = 0;
+    float dcv[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     const float d2inv = 1.0f / ((denom * denom) + 0.0000001f);
     const float(&A)[2][3] = e.a;
     if (d2inv != 0) {
-      da = d2inv * (-cc * cc * dcx + 2 * cb * cc * dcy + (denom - ca * cc) * dcz);
-      dc = d2inv * (-ca * ca * dcz + 2 * ca * cb * dcy + (denom - ca * cc) * dcx);
-      db = d2inv * 2 * (cb * cc * dcx - (denom + 2 * cb * cb) * dcy + ca * cb * dcz);
-      dcov[0] = (A[0][0] * A[0][0] * da + A[0][0] * A[1][0] * db + A[1][0] * A[1][0] * dc);
-      dcov[3] = (A[0][1] * A[0][1] * da + A[0][1] * A[1][1] * db + A[1][1] * A[1][1] * dc);
-      dcov[5] = (A[0][2] * A[0][2] * da + A[0][2] * A[1][2] * db + A[1][2] * A[1][2] * dc);
-      dcov[1] = 2 * A[0][0] * A[0][1] * da + (A[0][0] * A[1][1] + A[0][1] * A[1][0]) * db + 2 * A[1][0] * A[1][1] * dc;
-      dcov[2] = 2 * A[0][0] * A[0][2] * da + (A[0][0] * A[1][2] + A[0][2] * A[1][0]) * db + 2 * A[1][0] * A[1][2] * dc;
-      dcov[4] = 2 * A[0][2] * A[0][1] * da + (A[0][1] * A[1][2] + A[0][2] * A[1][1]) * db + 2 * A[1][1] * A[1][2] * dc;
+      da = d2inv * (-cc * cc * dcx + 2 * cb2 * cc * dcy + (denom - ca * cc) * dcz);
+      dc = d2inv * (-ca * ca * dcz + 2 * ca * cb2 * dcy + (denom - ca * cc) * dcx);
+      db = d2inv * 2 * (cb2 * cc * dcx - (denom + 2 * cb2 * cb2) * dcy + ca * cb2 * dcz);
+      dcv[0] = (A[0][0] * A[0][0] * da + A[0][0] * A[1][0] * db + A[1][0] * A[1][0] * dc);
+      dcv[3] = (A[0][1] * A[0][1] * da + A[0][1] * A[1][1] * db + A[1][1] * A[1][1] * dc);
+      dcv[5] = (A[0][2] * A[0][2] * da + A[0][2] * A[1][2] * db + A[1][2] * A[1][2] * dc);
+      dcv[1] = 2 * A[0][0] * A[0][1] * da + (A[0][0] * A[1][1] + A[0][1] * A[1][0]) * db + 2 * A[1][0] * A[1][1] * dc;
+      dcv[2] = 2 * A[0][0] * A[0][2] * da + (A[0][0] * A[1][2] + A[0][2] * A[1][0]) * db + 2 * A[1][0] * A[1][2] * dc;
+      dcv[4] = 2 * A[0][2] * A[0][1] * da + (A[0][1] * A[1][2] + A[0][2] * A[1][1]) * db + 2 * A[1][1] * A[1][2] * dc;
     }
     const float V[3][3] = {{c3v[0], c3v[1], c3v[2]}, {c3v[1], c3v[3], c3v[4]}, {c3v[2], c3v[4], c3v[5]}};
     float dT0[3], dT1[3];
@@ -465,38 +505,61 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdArgs a
       dT0[k] = 2 * r0 * da + r1 * db;
       dT1[k] = 2 * r1 * dc + r0 * db;
     }
-    const float* v = a.view;
+    const float* v = view;
     const float dJ00 = v[0] * dT0[0] + v[4] * dT0[1] + v[8] * dT0[2];
     const float dJ02 = v[2] * dT0[0] + v[6] * dT0[1] + v[10] * dT0[2];
     const float dJ11 = v[1] * dT1[0] + v[5] * dT1[1] + v[9] * dT1[2];
     const float dJ12 = v[2] * dT1[0] + v[6] * dT1[1] + v[10] * dT1[2];
     const float tz = 1.f / e.t[2], tz2 = tz * tz, tz3 = tz2 * tz;
-    const float hx = a.focal_x, hy = a.focal_y;
+    const float hx = focal_x, hy = focal_y;
     const float dtx = xg * -hx * tz2 * dJ02;
     const float dty = yg * -hy * tz2 * dJ12;
     const float dtz = -hx * tz2 * dJ00 - hy * tz2 * dJ11 + (2 * hx * e.t[0]) * tz3 * dJ02 + (2 * hy * e.t[1]) * tz3 * dJ12;
-    dm[0] = v[0] * dtx + v[1] * dty + v[2] * dtz;
-    dm[1] = v[4] * dtx + v[5] * dty + v[6] * dtz;
-    dm[2] = v[8] * dtx + v[9] * dty + v[10] * dtz;
+    float dmc[3];
+    dmc[0] = v[0] * dtx + v[1] * dty + v[2] * dtz;
+    dmc[1] = v[4] * dtx + v[5] * dty + v[6] * dtz;
+    dmc[2] = v[8] * dtx + v[9] * dty + v[10] * dtz;
     // mean2D and depth contributions (backward.cu:389-420)
-    const float* pr = a.proj;
     const float4 mh = xf44(pr, mean);
     const float mw = 1.0f / (mh.w + 0.0000001f);
     const float mul1 = (pr[0] * mean.x + pr[4] * mean.y + pr[8] * mean.z + pr[12]) * mw * mw;
     const float mul2 = (pr[1] * mean.x + pr[5] * mean.y + pr[9] * mean.z + pr[13]) * mw * mw;
-    dm[0] += (pr[0] * mw - pr[3] * mul1) * am0 + (pr[1] * mw - pr[3] * mul2) * am1;
-    dm[1] += (pr[4] * mw - pr[7] * mul1) * am0 + (pr[5] * mw - pr[7] * mul2) * am1;
-    dm[2] += (pr[8] * mw - pr[11] * mul1) * am0 + (pr[9] * mw - pr[11] * mul2) * am1;
+    dmc[0] += (pr[0] * mw - pr[3] * mul1) * am0 + (pr[1] * mw - pr[3] * mul2) * am1;
+    dmc[1] += (pr[4] * mw - pr[7] * mul1) * am0 + (pr[5] * mw - pr[7] * mul2) * am1;
+    dmc[2] += (pr[8] * mw - pr[11] * mul1) * am0 + (pr[9] * mw - pr[11] * mul2) * am1;
     const float mul3 = v[2] * mean.x + v[6] * mean.y + v[10] * mean.z + v[14];
     const float dd = acc[A_DEPTH];
-    dm[0] += (v[2] - v[3] * mul3) * dd;
-    dm[1] += (v[6] - v[7] * mul3) * dd;
-    dm[2] += (v[10] - v[11] * mul3) * dd;
-    if (a.shs) sh_bwd(a.D, a.M, mean, ld3(a.campos), a.shs, g, a.clamped[g], dcol, a.dsh, dm, mk, ac);
-    if (a.scales) cov3d_bwd(ld3(a.scales + 3 * g), a.scale_modifier,
-                            reinterpret_cast<const float4*>(a.rotations)[g], dcov, dscale, drot);
+    dmc[0] += (v[2] - v[3] * mul3) * dd;
+    dmc[1] += (v[6] - v[7] * mul3) * dd;
+    dmc[2] += (v[10] - v[11] * mul3) * dd;
+    if (a.shs) {
+      const uint8_t* clamped = shift_bytes(a.clamped, c * cb.geom_stride);
+      sh_bwd(a.D, a.M, mean, ld3(cb.campos + 3 * c), a.shs, g, clamped[g], dcol_c, a.dsh, dmc, mk,
+             sh_written ? 1 : 0);
+      sh_written = true;
+    }
+    // the first camera that sees the Gaussian assigns, the later ones add
+#pragma unroll
+    for (int i = 0; i < 3; ++i) dm[i] = any_vis ? dm[i] + dmc[i] : dmc[i];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) dcov[i] = any_vis ? dcov[i] + dcv[i] : dcv[i];
+    any_vis = true;
   }
-  if ((!vis || !a.shs) && a.M > 0 && !ac) {  // no SH gradient: zeros (masked like the rest)
+  float dscale[3] = {0.f, 0.f, 0.f}, drot[4] = {0.f, 0.f, 0.f, 0.f};
+  if (any_vis && a.scales)
+    cov3d_bwd(ld3(a.scales + 3 * g), a.scale_modifier, reinterpret_cast<const float4*>(a.rotations)[g], dcov,
+              dscale, drot);
+  gput(a.dmeans2D + 3 * g, am[0], ac); gput(a.dmeans2D + 3 * g + 1, am[1], ac);
+  if (!ac) a.dmeans2D[3 * g + 2] = 0.f;
+  if (a.st_accum) gput(a.st_accum + g, st_acc, ac);
+  if (a.st_denom) gput(a.st_denom + g, st_den, ac);
+  if (a.st_maxrad) a.st_maxrad[g] = ac ? fmaxf(a.st_maxrad[g], st_rad) : st_rad;
+  // Q12 label mask (DGR/__init__.py:159-173), applied at store time exactly as
+  // the reference's elementwise `grad * label` (the chain rule uses unmasked dcol).
+  gput(a.dcolors + 3 * g, dcol[0] * mk, ac); gput(a.dcolors + 3 * g + 1, dcol[1] * mk, ac);
+  gput(a.dcolors + 3 * g + 2, dcol[2] * mk, ac);
+  gput(a.dopacity + g, dop * mk, ac);
+  if (!sh_written && a.M > 0) {  // no SH gradient: zeros (masked like the rest)
     float* ds = a.dsh + (size_t)g * a.M * 3;
     for (int i = 0; i < 3 * a.M; ++i) ds[i] = 0.f * mk;
   }
@@ -515,9 +578,9 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdArgs a
   }
 }
 
-void launch_preprocess_bwd(const PreprocessBwdArgs& a, hipStream_t s) {
+void launch_preprocess_bwd(const PreprocessBwdArgs& a, const CamBatch& cb, hipStream_t s) {
   if (a.P <= 0) return;
-  hipLaunchKernelGGL(preprocess_bwd_kernel, dim3((a.P + 255) / 256), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(preprocess_bwd_kernel, dim3((a.P + 255) / 256), dim3(256), 0, s, a, cb);
 }
 
 }  // namespace gs

@@ -192,11 +192,23 @@ constexpr int fwd_waves_per_simd() {
 }
 template <int F, int COMPAT>
 __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu(fwd_waves_per_simd<F>(), 8))) void render_fwd_kernel(
-    int W, int H, int grid_x, int num_tiles, const uint32_t* __restrict__ order, const uint2* __restrict__ ranges,
-    const uint32_t* __restrict__ point_list, const float* __restrict__ rec,
-    const float* __restrict__ feats, const float* __restrict__ bg, float* __restrict__ out_color,
-    float* __restrict__ out_feature, float* __restrict__ out_depth, float* __restrict__ out_alpha,
-    uint32_t* __restrict__ n_contrib) {
+    RenderArgs a0, CamBatch cb) {
+  // camera c of the batch: workgroups are dealt camera-minor (block b ->
+  // camera b % C, tile slot b / C), so every camera's longest tiles start first
+  const int cam = blockIdx.x % cb.C, bslot = blockIdx.x / cb.C;
+  const RenderArgs ca = cam_render_args(a0, cb, cam);
+  const int W = ca.W, H = ca.H, grid_x = ca.grid_x, num_tiles = ca.num_tiles;
+  const uint32_t* __restrict__ order = ca.order;
+  const uint2* __restrict__ ranges = ca.ranges;
+  const uint32_t* __restrict__ point_list = ca.point_list;
+  const float* __restrict__ rec = ca.rec;
+  const float* __restrict__ feats = ca.feats;
+  const float* __restrict__ bg = ca.bg;
+  float* __restrict__ out_color = ca.out_color;
+  float* __restrict__ out_feature = ca.out_feature;
+  float* __restrict__ out_depth = ca.out_depth;
+  float* __restrict__ out_alpha = ca.out_alpha;
+  uint32_t* __restrict__ n_contrib = ca.n_contrib;
   // Features: 8 / 16 channels on the VALU (v_pk_fma_f32 with the Gaussian's
   // row in SGPRs, requested at the top of the iteration); 32 / 64 channels on
   // the matrix cores: a wave parks the weights w = alpha T of 16 blending
@@ -215,7 +227,7 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
 
   // strip item = tile * 4 + wave (dispatch order, see strip_item)
   const int lane = threadIdx.x & 63, lw = threadIdx.x >> 6;  // lw: LDS slot of the wave
-  const int item = strip_item(blockIdx.x, num_tiles, GS_WPB_FWD) + lw;
+  const int item = strip_item(bslot, num_tiles, GS_WPB_FWD) + lw;
   const int tile = tile_of(order, item >> 2), wave = item & 3;
   const int tx = tile % grid_x, ty = tile / grid_x;
   const int qx0 = strip_x0(tx, wave), qy0 = strip_y0(ty, wave);  // lane = strip pixel (lane % STRIP_W, lane / STRIP_W)
@@ -515,12 +527,25 @@ constexpr int bwd_waves_per_simd() {
 }
 template <int F, int COMPAT>
 __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu(bwd_waves_per_simd<F, COMPAT>(), 8))) void render_bwd_kernel(
-    int W, int H, int grid_x, int num_tiles, const uint32_t* __restrict__ order, const uint2* __restrict__ ranges,
-    const uint32_t* __restrict__ point_list, const float* __restrict__ rec,
-    const float* __restrict__ feats, const float* __restrict__ bg, const float* __restrict__ alphas,
-    const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dpix,
-    const float* __restrict__ dL_dfeat, const float* __restrict__ dL_ddepth,
-    const float* __restrict__ dL_dalpha, float* __restrict__ acc, float* __restrict__ dsem) {
+    RenderBwdArgs a0, CamBatch cb) {
+  // camera c of the batch: workgroups are dealt camera-minor (see the forward)
+  const int cam = blockIdx.x % cb.C, bslot = blockIdx.x / cb.C;
+  const RenderBwdArgs ca = cam_render_bwd_args(a0, cb, cam);
+  const int W = ca.W, H = ca.H, grid_x = ca.grid_x, num_tiles = ca.num_tiles;
+  const uint32_t* __restrict__ order = ca.order;
+  const uint2* __restrict__ ranges = ca.ranges;
+  const uint32_t* __restrict__ point_list = ca.point_list;
+  const float* __restrict__ rec = ca.rec;
+  const float* __restrict__ feats = ca.feats;
+  const float* __restrict__ bg = ca.bg;
+  const float* __restrict__ alphas = ca.alphas;
+  const uint32_t* __restrict__ n_contrib = ca.n_contrib;
+  const float* __restrict__ dL_dpix = ca.dL_dpix;
+  const float* __restrict__ dL_dfeat = ca.dL_dfeat;
+  const float* __restrict__ dL_ddepth = ca.dL_ddepth;
+  const float* __restrict__ dL_dalpha = ca.dL_dalpha;
+  float* __restrict__ acc = ca.acc;
+  float* __restrict__ dsem = ca.dsem;
   constexpr int WB = 16;                      // Gaussians per matrix batch
   constexpr int CB = F >= 16 ? F / 16 : 0;    // 16-channel feature blocks with their own accumulators
   constexpr int CB1 = CB > 0 ? CB : 1;
@@ -535,7 +560,7 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
 
   // strip item = tile * 4 + wave (dispatch order, see strip_item)
   const int lane = threadIdx.x & 63, lw = threadIdx.x >> 6;  // lw: LDS slot of the wave
-  const int item = strip_item(blockIdx.x, num_tiles, GS_WPB_BWD) + lw;
+  const int item = strip_item(bslot, num_tiles, GS_WPB_BWD) + lw;
   const int tile = tile_of(order, item >> 2), wave = item & 3;
   const int tx = tile % grid_x, ty = tile / grid_x;
   const int qx0 = strip_x0(tx, wave), qy0 = strip_y0(ty, wave);  // lane = strip pixel (lane % STRIP_W, lane / STRIP_W)
@@ -835,58 +860,50 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
 // ------------------------------------------------------------------ dispatch
 
 template <int F>
-static void fwd_f(const RenderArgs& a, hipStream_t s) {
-  dim3 grid(a.num_tiles * (4 / GS_WPB_FWD)), block(64 * GS_WPB_FWD);
+static void fwd_f(const RenderArgs& a, const CamBatch& cb, hipStream_t s) {
+  dim3 grid(a.num_tiles * (4 / GS_WPB_FWD) * cb.C), block(64 * GS_WPB_FWD);
 #ifdef GS_EXP_FWD_LDS_PAD
   const size_t pad = GS_EXP_FWD_LDS_PAD;  // occupancy experiment: unused dynamic LDS
 #else
   const size_t pad = 0;
 #endif
   if (a.compat == COMPAT_REFERENCE)
-    hipLaunchKernelGGL((render_fwd_kernel<F, COMPAT_REFERENCE>), grid, block, pad, s, a.W, a.H, a.grid_x,
-                       a.num_tiles, a.order, a.ranges, a.point_list, a.rec, a.feats, a.bg, a.out_color,
-                       a.out_feature, a.out_depth, a.out_alpha, a.n_contrib);
+    hipLaunchKernelGGL((render_fwd_kernel<F, COMPAT_REFERENCE>), grid, block, pad, s, a, cb);
   else
-    hipLaunchKernelGGL((render_fwd_kernel<F, COMPAT_FIXED>), grid, block, 0, s, a.W, a.H, a.grid_x,
-                       a.num_tiles, a.order, a.ranges, a.point_list, a.rec, a.feats, a.bg, a.out_color,
-                       a.out_feature, a.out_depth, a.out_alpha, a.n_contrib);
+    hipLaunchKernelGGL((render_fwd_kernel<F, COMPAT_FIXED>), grid, block, 0, s, a, cb);
 }
 
 template <int F>
-static void bwd_f(const RenderBwdArgs& a, hipStream_t s) {
-  dim3 grid(a.num_tiles * (4 / GS_WPB_BWD)), block(64 * GS_WPB_BWD);
+static void bwd_f(const RenderBwdArgs& a, const CamBatch& cb, hipStream_t s) {
+  dim3 grid(a.num_tiles * (4 / GS_WPB_BWD) * cb.C), block(64 * GS_WPB_BWD);
   if (a.compat == COMPAT_REFERENCE)
-    hipLaunchKernelGGL((render_bwd_kernel<F, COMPAT_REFERENCE>), grid, block, 0, s, a.W, a.H, a.grid_x,
-                       a.num_tiles, a.order, a.ranges, a.point_list, a.rec, a.feats, a.bg, a.alphas, a.n_contrib,
-                       a.dL_dpix, a.dL_dfeat, a.dL_ddepth, a.dL_dalpha, a.acc, a.dsem);
+    hipLaunchKernelGGL((render_bwd_kernel<F, COMPAT_REFERENCE>), grid, block, 0, s, a, cb);
   else
-    hipLaunchKernelGGL((render_bwd_kernel<F, COMPAT_FIXED>), grid, block, 0, s, a.W, a.H, a.grid_x,
-                       a.num_tiles, a.order, a.ranges, a.point_list, a.rec, a.feats, a.bg, a.alphas, a.n_contrib,
-                       a.dL_dpix, a.dL_dfeat, a.dL_ddepth, a.dL_dalpha, a.acc, a.dsem);
+    hipLaunchKernelGGL((render_bwd_kernel<F, COMPAT_FIXED>), grid, block, 0, s, a, cb);
 }
 
-bool launch_render_fwd(const RenderArgs& a, hipStream_t s) {
+bool launch_render_fwd(const RenderArgs& a, const CamBatch& cb, hipStream_t s) {
   if (a.num_tiles <= 0) return true;
   switch (a.F) {
-    case 0: fwd_f<0>(a, s); return true;
-    case 4: fwd_f<4>(a, s); return true;
-    case 8: fwd_f<8>(a, s); return true;
-    case 16: fwd_f<16>(a, s); return true;
-    case 32: fwd_f<32>(a, s); return true;
-    case 64: fwd_f<64>(a, s); return true;
+    case 0: fwd_f<0>(a, cb, s); return true;
+    case 4: fwd_f<4>(a, cb, s); return true;
+    case 8: fwd_f<8>(a, cb, s); return true;
+    case 16: fwd_f<16>(a, cb, s); return true;
+    case 32: fwd_f<32>(a, cb, s); return true;
+    case 64: fwd_f<64>(a, cb, s); return true;
     default: return false;
   }
 }
 
-bool launch_render_bwd(const RenderBwdArgs& a, hipStream_t s) {
+bool launch_render_bwd(const RenderBwdArgs& a, const CamBatch& cb, hipStream_t s) {
   if (a.num_tiles <= 0) return true;
   switch (a.F) {
-    case 0: bwd_f<0>(a, s); return true;
-    case 4: bwd_f<4>(a, s); return true;
-    case 8: bwd_f<8>(a, s); return true;
-    case 16: bwd_f<16>(a, s); return true;
-    case 32: bwd_f<32>(a, s); return true;
-    case 64: bwd_f<64>(a, s); return true;
+    case 0: bwd_f<0>(a, cb, s); return true;
+    case 4: bwd_f<4>(a, cb, s); return true;
+    case 8: bwd_f<8>(a, cb, s); return true;
+    case 16: bwd_f<16>(a, cb, s); return true;
+    case 32: bwd_f<32>(a, cb, s); return true;
+    case 64: bwd_f<64>(a, cb, s); return true;
     default: return false;
   }
 }

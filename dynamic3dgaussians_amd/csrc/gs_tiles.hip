@@ -42,7 +42,8 @@ constexpr int LANE_TILES = 16;
 // The reference's tiles_touched (its num_rendered) is summed per block
 // alongside.
 template <bool WRITE>
-__global__ __launch_bounds__(TB_THREADS) void tile_hist_kernel(TileArgs a, int t0, int nt) {
+__global__ __launch_bounds__(TB_THREADS) void tile_hist_kernel(TileArgs a0, CamBatch cb, int t0, int nt) {
+  const TileArgs a = cam_tile_args(a0, cb, blockIdx.y);
   extern __shared__ uint32_t s_bin[];  // nt counters (hist) or cursors (bucket)
   __shared__ uint32_t s_rect[TB_THREADS / 64];
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
@@ -113,8 +114,10 @@ __global__ __launch_bounds__(TB_THREADS) void tile_hist_kernel(TileArgs a, int t
 // row and load), the 16 block-group partial sums are scanned through LDS.
 static_assert(TB_BLOCKS == 256, "tile_rowscan_kernel: 16 block groups of 16 blocks");
 constexpr int RS_T = 16;
-__global__ __launch_bounds__(256) void tile_rowscan_kernel(uint32_t* __restrict__ thist,
-                                                           uint32_t* __restrict__ ttotal, int T) {
+__global__ __launch_bounds__(256) void tile_rowscan_kernel(uint32_t* __restrict__ thist0,
+                                                           uint32_t* __restrict__ ttotal0, int T, CamBatch cb) {
+  uint32_t* __restrict__ thist = shift_bytes(thist0, blockIdx.y * cb.img_stride);
+  uint32_t* __restrict__ ttotal = shift_bytes(ttotal0, blockIdx.y * cb.img_stride);
   __shared__ uint32_t s_part[16][RS_T];
   const int tid = threadIdx.x, tt = tid % RS_T, bg = tid / RS_T;
   const int t = blockIdx.x * RS_T + tt;
@@ -147,10 +150,16 @@ __global__ __launch_bounds__(256) void tile_rowscan_kernel(uint32_t* __restrict_
 
 // One workgroup: exclusive scan of the tile totals into ranges, and the header.
 constexpr int OFF_T = 1024;
-__global__ __launch_bounds__(OFF_T) void tile_offsets_kernel(const uint32_t* __restrict__ ttotal, int T,
-                                                             const uint32_t* __restrict__ bsum,
-                                                             uint2* __restrict__ ranges,
-                                                             uint32_t* __restrict__ meta, int prefiltered) {
+__global__ __launch_bounds__(OFF_T) void tile_offsets_kernel(const uint32_t* __restrict__ ttotal0, int T,
+                                                             const uint32_t* __restrict__ bsum0,
+                                                             uint2* __restrict__ ranges0,
+                                                             uint32_t* __restrict__ meta0, int prefiltered,
+                                                             CamBatch cb) {
+  const int64_t io = blockIdx.x * cb.img_stride;  // one workgroup per camera
+  const uint32_t* __restrict__ ttotal = shift_bytes(ttotal0, io);
+  const uint32_t* __restrict__ bsum = shift_bytes(bsum0, io);
+  uint2* __restrict__ ranges = shift_bytes(ranges0, io);
+  uint32_t* __restrict__ meta = shift_bytes(meta0, io);
   __shared__ unsigned long long s_sum[OFF_T / 64];
   __shared__ unsigned long long s_lref;
   __shared__ uint32_t s_max;
@@ -216,9 +225,13 @@ __global__ __launch_bounds__(OFF_T) void tile_offsets_kernel(const uint32_t* __r
 // order inside a bucket is arbitrary: every tile's result is independent of
 // when it runs.  One workgroup; launched with the render phase, off the
 // plan -> header-read path the host waits for.
-__global__ __launch_bounds__(OFF_T) void tile_order_kernel(const uint32_t* __restrict__ ttotal, int T,
-                                                           const uint32_t* __restrict__ meta,
-                                                           uint32_t* __restrict__ order) {
+__global__ __launch_bounds__(OFF_T) void tile_order_kernel(const uint32_t* __restrict__ ttotal0, int T,
+                                                           const uint32_t* __restrict__ meta0,
+                                                           uint32_t* __restrict__ order0, CamBatch cb) {
+  const int64_t io = blockIdx.x * cb.img_stride;  // one workgroup per camera
+  const uint32_t* __restrict__ ttotal = shift_bytes(ttotal0, io);
+  const uint32_t* __restrict__ meta = shift_bytes(meta0, io);
+  uint32_t* __restrict__ order = shift_bytes(order0, io);
   __shared__ uint32_t s_obin[OFF_T];
   __shared__ uint32_t s_owsum[OFF_T / 64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -392,13 +405,14 @@ __device__ __attribute__((always_inline)) KP tile_radix_sort(KP A, KP B, int n, 
 // others exit).  Keys sorted in LDS up to `cap` (the launch's dynamic LDS),
 // in global memory beyond.
 template <int NT>
-__global__ __launch_bounds__(NT) void tile_sort_kernel(const uint2* __restrict__ ranges,
-                                                       const uint32_t* __restrict__ order,
-                                                       uint64_t* __restrict__ keys, uint64_t* __restrict__ keys2,
-                                                       uint32_t* __restrict__ plist, int cap, int lo, int hi) {
+__global__ __launch_bounds__(NT) void tile_sort_kernel(TileArgs a0, CamBatch cb, int cap, int lo, int hi) {
   extern __shared__ uint64_t s_key[];  // 2 x cap keys
   __shared__ RadixSmem<NT> sm;
-  const uint2 r = ranges[order[blockIdx.x]];  // longest tiles first
+  const TileArgs ta = cam_tile_args(a0, cb, blockIdx.y);
+  uint64_t* __restrict__ keys = ta.keys;
+  uint64_t* __restrict__ keys2 = ta.keys2;
+  uint32_t* __restrict__ plist = ta.plist;
+  const uint2 r = ta.ranges[ta.order[blockIdx.x]];  // longest tiles first
   const int n = (int)(r.y - r.x);
   if (n == 0 || n <= lo || n > hi) return;
   if (n == 1) {
@@ -418,59 +432,57 @@ __global__ __launch_bounds__(NT) void tile_sort_kernel(const uint2* __restrict__
 
 // ------------------------------------------------------------------ launchers
 
-void launch_tile_plan(const TileArgs& a, int prefiltered, hipStream_t s) {
+void launch_tile_plan(const TileArgs& a, const CamBatch& cb, int prefiltered, hipStream_t s) {
   const int T = a.num_tiles;
   for (int t0 = 0; t0 < T; t0 += TB_BINS) {
     const int nt = min(TB_BINS, T - t0);
-    hipLaunchKernelGGL(tile_hist_kernel<false>, dim3(TB_BLOCKS), dim3(TB_THREADS), sizeof(uint32_t) * nt, s, a,
-                       t0, nt);
+    hipLaunchKernelGGL(tile_hist_kernel<false>, dim3(TB_BLOCKS, cb.C), dim3(TB_THREADS), sizeof(uint32_t) * nt, s,
+                       a, cb, t0, nt);
   }
-  hipLaunchKernelGGL(tile_rowscan_kernel, dim3((T + RS_T - 1) / RS_T), dim3(256), 0, s, a.thist, a.ttotal, T);
-  hipLaunchKernelGGL(tile_offsets_kernel, dim3(1), dim3(OFF_T), 0, s, a.ttotal, T, a.bsum, a.ranges, a.meta,
-                     prefiltered);
+  hipLaunchKernelGGL(tile_rowscan_kernel, dim3((T + RS_T - 1) / RS_T, cb.C), dim3(256), 0, s, a.thist, a.ttotal, T,
+                     cb);
+  hipLaunchKernelGGL(tile_offsets_kernel, dim3(cb.C), dim3(OFF_T), 0, s, a.ttotal, T, a.bsum, a.ranges, a.meta,
+                     prefiltered, cb);
 }
 
-void launch_tile_order(const TileArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(OFF_T), 0, s, a.ttotal, a.num_tiles, a.meta, a.order);
+void launch_tile_order(const TileArgs& a, const CamBatch& cb, hipStream_t s) {
+  hipLaunchKernelGGL(tile_order_kernel, dim3(cb.C), dim3(OFF_T), 0, s, a.ttotal, a.num_tiles, a.meta, a.order, cb);
 }
 
-void launch_tile_bucket(const TileArgs& a, hipStream_t s) {
+void launch_tile_bucket(const TileArgs& a, const CamBatch& cb, hipStream_t s) {
   const int T = a.num_tiles;
   for (int t0 = 0; t0 < T; t0 += TB_BINS) {
     const int nt = min(TB_BINS, T - t0);
-    hipLaunchKernelGGL(tile_hist_kernel<true>, dim3(TB_BLOCKS), dim3(TB_THREADS), sizeof(uint32_t) * nt, s, a,
-                       t0, nt);
+    hipLaunchKernelGGL(tile_hist_kernel<true>, dim3(TB_BLOCKS, cb.C), dim3(TB_THREADS), sizeof(uint32_t) * nt, s,
+                       a, cb, t0, nt);
   }
 }
 
 template <int NT>
-static void tile_sort_launches(const TileArgs& a, int64_t max_len, hipStream_t s) {
-  const dim3 grid(a.num_tiles), block(NT);
+static void tile_sort_launches(const TileArgs& a, const CamBatch& cb, int64_t max_len, hipStream_t s) {
+  const dim3 grid(a.num_tiles, cb.C), block(NT);
   const int big = 0x7FFFFFFF;
   // LDS sized to the longest tile when the plan's header is known on the host
   if (max_len >= 0 && max_len <= TS_CAP) {
     const int cap = max_len > 0 ? (int)max_len : 1;
-    hipLaunchKernelGGL(tile_sort_kernel<NT>, grid, block, 2 * sizeof(uint64_t) * cap, s, a.ranges, a.order,
-                       a.keys, a.keys2, a.plist, cap, 0, big);
+    hipLaunchKernelGGL(tile_sort_kernel<NT>, grid, block, 2 * sizeof(uint64_t) * cap, s, a, cb, cap, 0, big);
     return;
   }
   // Long tiles (large scenes): the common tiles keep TS_CAP-sized LDS and
   // several workgroups per CU; the long ones follow in a second launch with
   // up to the whole 160 KiB per workgroup (global memory beyond TS_CAP_LONG).
-  hipLaunchKernelGGL(tile_sort_kernel<NT>, grid, block, 2 * sizeof(uint64_t) * TS_CAP, s, a.ranges, a.order,
-                     a.keys, a.keys2, a.plist, TS_CAP, 0, TS_CAP);
+  hipLaunchKernelGGL(tile_sort_kernel<NT>, grid, block, 2 * sizeof(uint64_t) * TS_CAP, s, a, cb, TS_CAP, 0, TS_CAP);
   const int cap2 = (max_len >= 0 && max_len < TS_CAP_LONG) ? (int)max_len : TS_CAP_LONG;
-  hipLaunchKernelGGL(tile_sort_kernel<NT>, grid, block, 2 * sizeof(uint64_t) * cap2, s, a.ranges, a.order,
-                     a.keys, a.keys2, a.plist, cap2, TS_CAP, big);
+  hipLaunchKernelGGL(tile_sort_kernel<NT>, grid, block, 2 * sizeof(uint64_t) * cap2, s, a, cb, cap2, TS_CAP, big);
 }
 
-void launch_tile_sort(const TileArgs& a, int64_t max_len, int64_t L, hipStream_t s) {
+void launch_tile_sort(const TileArgs& a, const CamBatch& cb, int64_t max_len, int64_t L, hipStream_t s) {
   // workgroup size by the mean tile length: 256 threads keep short tiles'
   // per-pass overhead low (bench camera: ~660 keys per tile), 512 split long
   // tiles' passes over twice the waves (1080p / 1M Gaussians: ~1800)
-  const int64_t mean = a.num_tiles > 0 ? L / a.num_tiles : 0;
-  if (L >= 0 && mean >= TS_WIDE_MEAN) tile_sort_launches<512>(a, max_len, s);
-  else tile_sort_launches<256>(a, max_len, s);
+  const int64_t mean = a.num_tiles > 0 ? L / ((int64_t)a.num_tiles * cb.C) : 0;
+  if (L >= 0 && mean >= TS_WIDE_MEAN) tile_sort_launches<512>(a, cb, max_len, s);
+  else tile_sort_launches<256>(a, cb, max_len, s);
 }
 
 }  // namespace gs

@@ -373,3 +373,163 @@ class GaussianRasterizer(nn.Module):
         if has_sem:                    # G4 (feature-3DGS style)
             return color, feature_map, radii, depth
         return color, radii, depth     # G1 (upstream "w-depth" API)
+
+
+# ---------------------------------------------------------------------------
+# Camera batches (no reference analogue): the C cameras of one multi-camera
+# training step rasterized together -- one launch per stage
+# over all cameras (include/gsplat_hip.h gs_*_batch).  Camera c's outputs are
+# those of GaussianRasterizer with settings[c]; the backward returns the
+# gradients summed over the cameras, i.e. what autograd accumulates when the
+# same inputs feed C per-camera rasterizations.
+
+def _batch_settings(settings_list):
+    rs0 = settings_list[0]
+    for rs in settings_list[1:]:
+        for name in ("image_height", "image_width", "scale_modifier", "sh_degree", "prefiltered", "debug"):
+            if getattr(rs, name) != getattr(rs0, name):
+                raise ValueError(f"the cameras of a batch share {name}")
+        if _compat_of(rs) != _compat_of(rs0):
+            raise ValueError("the cameras of a batch share compat")
+        if rs.bg is not rs0.bg and not torch.equal(rs.bg, rs0.bg):
+            raise ValueError("the cameras of a batch share one background")
+    for name in ("bg", "viewmatrix", "projmatrix", "campos"):
+        if any(getattr(rs, name) is None for rs in settings_list):
+            raise TypeError(f"GaussianRasterizationSettings.{name} is required")
+    return rs0
+
+
+class _RasterizeGaussiansBatch(torch.autograd.Function):
+    """_RasterizeGaussians over a list of camera settings (one launch per
+    stage for all of them); outputs stacked [C, ...]."""
+
+    @staticmethod
+    def forward(ctx, means3D, means2D, sh, colors_precomp, semantic_feature, opacities, scales, rotations,
+                cov3Ds_precomp, settings_list, label, densify_out):
+        rs0 = _batch_settings(settings_list)
+        compat = _compat_of(rs0)
+        C = len(settings_list)
+        pp = [_principal_point(rs) for rs in settings_list]
+        views = torch.stack([rs.viewmatrix.reshape(16) for rs in settings_list])
+        projs = torch.stack([rs.projmatrix.reshape(16) for rs in settings_list])
+        cpos = torch.stack([rs.campos.reshape(3) for rs in settings_list])
+        sh = _empty_like_none(sh)
+        colors_precomp = _empty_like_none(colors_precomp)
+        scales = _empty_like_none(scales)
+        rotations = _empty_like_none(rotations)
+        cov3Ds_precomp = _empty_like_none(cov3Ds_precomp)
+        tx = [rs.tanfovx for rs in settings_list]
+        ty = [rs.tanfovy for rs in settings_list]
+        out = _C.rasterize_gaussians_batch(
+            rs0.bg, means3D, colors_precomp, semantic_feature, opacities, scales, rotations, rs0.scale_modifier,
+            cov3Ds_precomp, views, projs, [p[0] for p in pp], [p[1] for p in pp], tx, ty, rs0.image_height,
+            rs0.image_width, sh, rs0.sh_degree, cpos, rs0.prefiltered, rs0.debug, compat=compat)
+        num_rendered, color, feature_map, depth, alpha, radii, geom, binning, img, num_instances = out
+        ctx.rs0 = rs0
+        ctx.cams = (views, projs, cpos, pp, tx, ty)
+        ctx.num_rendered = num_rendered
+        ctx.num_instances = num_instances
+        ctx.compat = compat
+        ctx.C = C
+        ctx.densify_out = densify_out
+        ctx.set_materialize_grads(False)
+        ctx.sem_shape = None if semantic_feature is None else tuple(semantic_feature.shape)
+        ctx.save_for_backward(colors_precomp, semantic_feature, means3D, scales, rotations, cov3Ds_precomp,
+                              radii, sh, geom, binning, img, alpha,
+                              label if isinstance(label, torch.Tensor) else None)
+        ctx.mark_non_differentiable(radii)
+        return color, radii, feature_map, depth, alpha
+
+    @staticmethod
+    def backward(ctx, grad_color, grad_radii, grad_out_feature, grad_depth, grad_alpha):
+        rs0 = ctx.rs0
+        views, projs, cpos, pp, tx, ty = ctx.cams
+        (colors_precomp, semantic_feature, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geom,
+         binning, img, alpha, label) = ctx.saved_tensors
+        cx, cy = [p[0] for p in pp], [p[1] for p in pp]
+        # Q2 in reference mode, per camera (see _RasterizeGaussians.backward)
+        cam4 = (tx, ty, cx, cy) if ctx.compat == "reference" else (cx, cy, tx, ty)
+        fuse = (label is not None and label.dim() == 1 and label.numel() == means3D.size(0)
+                and label.dtype in _FUSABLE_LABEL_DTYPES)
+        grads = _C.rasterize_gaussians_batch_backward(
+            rs0.bg, means3D, radii, colors_precomp, semantic_feature, scales, rotations, rs0.scale_modifier,
+            cov3Ds_precomp, views, projs, *cam4, grad_color, grad_out_feature, grad_depth, grad_alpha, sh,
+            rs0.sh_degree, cpos, geom, ctx.num_instances, binning, img, alpha, rs0.debug, compat=ctx.compat,
+            grad_mask=label if fuse else None, densify=ctx.densify_out)
+        (grad_means2D, grad_colors_precomp, grad_semantic_feature, grad_opacities, grad_means3D,
+         grad_cov3Ds_precomp, grad_sh, grad_scales, grad_rotations) = grads
+        if ctx.sem_shape is not None:
+            grad_semantic_feature = grad_semantic_feature.reshape(ctx.sem_shape)
+        else:
+            grad_semantic_feature = None
+        if label is not None and not fuse:
+            lab = label.unsqueeze(1)
+            grad_means3D = grad_means3D * lab
+            grad_sh = grad_sh * lab[..., None]
+            grad_colors_precomp = grad_colors_precomp * lab
+            grad_opacities = grad_opacities * lab
+            grad_scales = grad_scales * lab
+            grad_rotations = grad_rotations * lab
+            grad_cov3Ds_precomp = grad_cov3Ds_precomp * lab
+        grads = (grad_means3D, grad_means2D, grad_sh, grad_colors_precomp, grad_semantic_feature,
+                 grad_opacities, grad_scales, grad_rotations, grad_cov3Ds_precomp, None, None, None)
+        return tuple(g if need else None for g, need in zip(grads, ctx.needs_input_grad))
+
+
+def rasterize_gaussians_batch(means3D, means2D, sh, colors_precomp, semantic_feature, opacities, scales,
+                              rotations, cov3Ds_precomp, settings_list, label=None, densify_out=None):
+    """rasterize_gaussians over a list of camera settings; outputs [C, ...]
+    (color, radii, feature_map, depth, alpha).  `densify_out`: optional
+    (accum, denom, max_radius) fp32 [P] tensors the backward fills with the
+    cameras' densification statistics (GradientSink.densify_stats)."""
+    return _RasterizeGaussiansBatch.apply(means3D, means2D, sh, colors_precomp, semantic_feature, opacities,
+                                          scales, rotations, cov3Ds_precomp, list(settings_list), label,
+                                          densify_out)
+
+
+class GaussianRasterizerBatch(nn.Module):
+    """GaussianRasterizer for a batch of cameras of one image size (the
+    cameras of one multi-camera training step): the same keyword call and
+    caller-generation arity dispatch, outputs stacked [C, ...], gradients
+    summed over the cameras.  `track_densify=True` keeps the cameras'
+    densification statistics of the last backward in `densify_stats`
+    (the reference's accumulate_mean2d_gradient / max_2D_radius inputs,
+    external.py:136-140, train.py:288-290; see GradientSink)."""
+
+    def __init__(self, settings_list, track_densify=False):
+        super().__init__()
+        self.settings_list = list(settings_list)
+        self.track_densify = track_densify
+        self.densify_stats = None
+
+    def forward(self, means3D, means2D, opacities=None, shs=None, semantic_feature=None, colors_precomp=None,
+                scales=None, rotations=None, cov3D_precomp=None, label=_UNSET):
+        if (shs is None and colors_precomp is None) or (shs is not None and colors_precomp is not None):
+            raise Exception('Please provide excatly one of either SHs or precomputed colors!')
+        if ((scales is None or rotations is None) and cov3D_precomp is None) or \
+                ((scales is not None or rotations is not None) and cov3D_precomp is not None):
+            raise Exception('Please provide exactly one of either scale/rotation pair or '
+                            'precomputed 3D covariance!')
+        shs = torch.Tensor([]) if shs is None else shs
+        colors_precomp = torch.Tensor([]) if colors_precomp is None else colors_precomp
+        scales = torch.Tensor([]) if scales is None else scales
+        rotations = torch.Tensor([]) if rotations is None else rotations
+        cov3D_precomp = torch.Tensor([]) if cov3D_precomp is None else cov3D_precomp
+        has_label = label is not _UNSET
+        lab = label if (has_label and isinstance(label, torch.Tensor)) else None
+        dens = None
+        if self.track_densify:
+            P = means3D.size(0)
+            dens = tuple(torch.zeros(P, dtype=torch.float32, device=means3D.device) for _ in range(3))
+            self.densify_stats = {"means2D_gradient_accum": dens[0], "denom": dens[1], "max_2D_radius": dens[2]}
+        color, radii, feature_map, depth, alpha = rasterize_gaussians_batch(
+            means3D, means2D, shs, colors_precomp, semantic_feature, opacities, scales, rotations,
+            cov3D_precomp, self.settings_list, lab, dens)
+        has_sem = semantic_feature is not None
+        if has_label and has_sem:      # G3
+            return color, radii, feature_map, depth, alpha
+        if has_label:                  # G2
+            return color, radii, depth, alpha
+        if has_sem:                    # G4
+            return color, feature_map, radii, depth
+        return color, radii, depth     # G1

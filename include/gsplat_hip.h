@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 6
+#define GS_ABI_VERSION 7
 
 /* compat modes: numerics of the as-shipped reference vs corrected ones */
 #define GS_COMPAT_REFERENCE 0
@@ -160,6 +160,49 @@ int gs_backward(const gs_gaussians *g, const gs_camera *cam, const int32_t *radi
                 float *dL_dsemantic, float *dL_dopacity, float *dL_dmeans3D,
                 float *dL_dcov3D, float *dL_dsh, float *dL_dscales,
                 float *dL_drotations, gs_stream_t stream);
+
+/* ---- camera batches (no reference analogue): the C cameras of one
+ * multi-camera training step (the per-timestep camera rig)
+ * rendered by ONE launch per stage instead of C per-camera call sequences --
+ * no per-camera tails in the blend kernels, one host read of the plan for
+ * the whole batch.  The per-camera semantics are exactly those of
+ * gs_forward_plan / gs_forward_render / gs_backward (which are the C = 1
+ * case), except that the backward SUMS the per-Gaussian gradients over the
+ * cameras (and the densification statistics, gs_gaussians.densify_*).
+ *
+ *  - cams[C] (host array, 1 <= C <= 64): one image size; the device
+ *    matrices of camera c are rows c of [C,16] view / [C,16] proj / [C,3]
+ *    campos arrays (cams[c].viewmatrix == cams[0].viewmatrix + 16 c, ...);
+ *    one shared background.  Camera scalars per camera, in the reference's
+ *    positional semantics as for the single-camera calls (Q2 included).
+ *  - State buffers: gs_batch_*_bytes; radii C x P; images C x (3|F|1|1) x H x W.
+ *  - num_instances[C] from the plan is passed back to the render and the
+ *    backward (each camera's binning buffer has its own length). */
+size_t gs_batch_geom_buffer_bytes(int64_t P, int32_t C);
+size_t gs_batch_image_buffer_bytes(int32_t W, int32_t H, int32_t C);
+size_t gs_batch_binning_buffer_bytes(int32_t C, const int64_t *num_instances);
+size_t gs_batch_backward_scratch_bytes(int64_t P, int32_t F, int32_t C);
+
+int gs_forward_plan_batch(const gs_gaussians *g, const gs_camera *cams, int32_t C,
+                          int prefiltered, int debug, int compat, void *geom_buffer,
+                          void *image_buffer, int32_t *radii, int64_t *num_rendered,
+                          int64_t *num_instances, gs_stream_t stream);
+
+int gs_forward_render_batch(const gs_gaussians *g, const gs_camera *cams, int32_t C,
+                            int debug, int compat, void *geom_buffer, void *binning_buffer,
+                            void *image_buffer, const int64_t *num_instances,
+                            const int32_t *radii, float *out_color, float *out_feature,
+                            float *out_depth, float *out_alpha, gs_stream_t stream);
+
+int gs_backward_batch(const gs_gaussians *g, const gs_camera *cams, int32_t C,
+                      const int32_t *radii, int debug, int compat, const void *geom_buffer,
+                      const void *binning_buffer, const void *image_buffer,
+                      const int64_t *num_instances, const float *alphas,
+                      const float *dL_dout_color, const float *dL_dout_feature,
+                      const float *dL_dout_depth, const float *dL_dout_alpha, void *scratch,
+                      float *dL_dmeans2D, float *dL_dcolors, float *dL_dsemantic,
+                      float *dL_dopacity, float *dL_dmeans3D, float *dL_dcov3D, float *dL_dsh,
+                      float *dL_dscales, float *dL_drotations, gs_stream_t stream);
 
 /* markVisible -- replaces DGR/rasterize_points.cu:227-246 and
  * CR/rasterizer_impl.cu:141-153 (checkFrustum).  present[P] is 0/1 bytes. */

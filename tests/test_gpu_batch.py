@@ -1,0 +1,166 @@
+"""Camera batches (gs_*_batch, GaussianRasterizerBatch): one launch per stage
+for the C cameras of a multi-camera step.  Camera c's forward outputs must be
+bit-identical to the per-camera drop-in rasterizer's, and the backward must
+equal the sum of the per-camera gradients (autograd's accumulation) up to
+fp32 summation order."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+from dynamic3dgaussians_amd.camera import camera_rig
+from dynamic3dgaussians_amd.rasterizer import (GaussianRasterizationSettings, GaussianRasterizer,
+                                               GaussianRasterizerBatch)
+from dynamic3dgaussians_amd.scene import make_gaussians
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+def _settings(cams, W, H, compat, sh_degree=0, bg=None):
+    bg = torch.zeros(3, device=DEV) if bg is None else bg
+    return [GaussianRasterizationSettings(
+        image_height=H, image_width=W, tanfovx=c.tanfovx, tanfovy=c.tanfovy, c_x=c.c_x, c_y=c.c_y, bg=bg,
+        viewmatrix=torch.from_numpy(c.viewmatrix.copy()).to(DEV),
+        projmatrix=torch.from_numpy(c.projmatrix.copy()).to(DEV), sh_degree=sh_degree,
+        campos=torch.from_numpy(c.campos.copy()).to(DEV), compat=compat) for c in cams]
+
+
+def _scene(P, F, use_sh, seed=0):
+    g = make_gaussians(P, F=F, seed=seed, device=DEV)
+    gen = torch.Generator(device=DEV).manual_seed(seed + 11)
+    src = dict(means3D=g["means3D"], opacities=g["opacities"], scales=g["scales"], rotations=g["rotations"])
+    if F:
+        src["semantic_feature"] = g["semantic_feature"]
+    if use_sh:
+        src["shs"] = torch.randn(P, 16, 3, device=DEV, generator=gen) * 0.2
+    else:
+        src["colors_precomp"] = g["colors"]
+    return src
+
+
+def _rel(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+@pytest.mark.parametrize("F,use_sh,compat", [(0, False, "reference"), (32, False, "reference"),
+                                             (8, True, "fixed"), (32, False, "fixed"), (16, True, "reference")])
+def test_batch_matches_per_camera(F, use_sh, compat, P=15000, W=176, H=144, C=5):
+    src = _scene(P, F, use_sh, seed=F + (7 if use_sh else 0))
+    rig = camera_rig(C, W, H)
+    sets = _settings(rig, W, H, compat, sh_degree=3 if use_sh else 0)
+    gen = torch.Generator(device=DEV).manual_seed(3)
+    label = (torch.rand(P, device=DEV, generator=gen) > 0.25).float()
+    up_c = torch.randn(C, 3, H, W, device=DEV, generator=gen)
+    up_d = torch.randn(C, 1, H, W, device=DEV, generator=gen)
+    up_f = torch.randn(C, F, H, W, device=DEV, generator=gen) if F else None
+    up_a = torch.randn(C, 1, H, W, device=DEV, generator=gen)
+    names = list(src)
+
+    # per camera (the drop-in), autograd sums over the cameras
+    leaves = {k: v.clone().requires_grad_(True) for k, v in src.items()}
+    m2 = torch.zeros(P, 3, device=DEV, requires_grad=True)
+    ref = []
+    for c in range(C):
+        out = GaussianRasterizer(sets[c])(means2D=m2, label=label, **leaves)
+        if F:
+            im, radius, feat, depth, alpha = out
+        else:
+            im, radius, depth, alpha = out
+            feat = None
+        ref.append((im.detach(), radius, None if feat is None else feat.detach(), depth.detach(), alpha.detach()))
+        outs, gr = [im, depth, alpha], [up_c[c], up_d[c], up_a[c]]
+        if F:
+            outs.append(feat)
+            gr.append(up_f[c])
+        torch.autograd.backward(outs, gr)
+    ref_grads = {k: leaves[k].grad.clone() for k in names}
+    ref_grads["means2D"] = m2.grad.clone()
+
+    # the batch
+    leaves_b = {k: v.clone().requires_grad_(True) for k, v in src.items()}
+    m2b = torch.zeros(P, 3, device=DEV, requires_grad=True)
+    out = GaussianRasterizerBatch(sets)(means2D=m2b, label=label, **leaves_b)
+    if F:
+        im, radius, feat, depth, alpha = out
+    else:
+        im, radius, depth, alpha = out
+        feat = None
+    assert im.shape == (C, 3, H, W) and radius.shape == (C, P) and depth.shape == (C, 1, H, W)
+    for c in range(C):
+        r_im, r_rad, r_feat, r_depth, r_alpha = ref[c]
+        assert torch.equal(im[c], r_im), c
+        assert torch.equal(radius[c], r_rad), c
+        assert torch.equal(depth[c], r_depth), c
+        assert torch.equal(alpha[c], r_alpha), c
+        if F:
+            assert torch.equal(feat[c], r_feat), c
+    outs, gr = [im, depth, alpha], [up_c, up_d, up_a]
+    if F:
+        outs.append(feat)
+        gr.append(up_f)
+    torch.autograd.backward(outs, gr)
+    for k in names:
+        assert leaves_b[k].grad is not None, k
+        assert _rel(leaves_b[k].grad, ref_grads[k]) < 1e-5, (k, _rel(leaves_b[k].grad, ref_grads[k]))
+    assert _rel(m2b.grad, ref_grads["means2D"]) < 1e-5
+    # label masking: masked Gaussians get exactly zero (Q12)
+    off = label == 0
+    assert torch.all(leaves_b["means3D"].grad[off] == 0)
+
+
+def test_batch_of_one_is_the_single_camera_call(P=12000, W=128, H=96):
+    src = _scene(P, 32, False, seed=2)
+    rig = camera_rig(3, W, H)
+    sets = _settings(rig[1:2], W, H, "reference")
+    a = GaussianRasterizer(sets[0])(means2D=torch.zeros(P, 3, device=DEV), label=torch.ones(P, device=DEV), **src)
+    b = GaussianRasterizerBatch(sets)(means2D=torch.zeros(P, 3, device=DEV), label=torch.ones(P, device=DEV), **src)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y[0])
+
+
+def test_batch_with_empty_and_partial_views(P=8000, W=160, H=112):
+    """A camera that sees nothing (every list empty) next to ones that do."""
+    src = _scene(P, 8, False, seed=4)
+    rig = camera_rig(3, W, H)
+    sets = _settings(rig, W, H, "reference")
+    # camera 1 looks away from the scene: view matrix of camera 0 turned around
+    v = sets[0].viewmatrix.clone()
+    v[:, 2] = -v[:, 2]
+    v[:, 0] = -v[:, 0]
+    sets[1] = sets[1]._replace(viewmatrix=v, projmatrix=sets[1].projmatrix)
+    leaves = {k: t.clone().requires_grad_(True) for k, t in src.items()}
+    m2 = torch.zeros(P, 3, device=DEV, requires_grad=True)
+    im, radius, feat, depth, alpha = GaussianRasterizerBatch(sets)(means2D=m2, label=torch.ones(P, device=DEV),
+                                                                    **leaves)
+    ref = GaussianRasterizer(sets[1])(means2D=torch.zeros(P, 3, device=DEV), label=torch.ones(P, device=DEV), **src)
+    assert torch.equal(im[1], ref[0]) and torch.equal(radius[1], ref[1])
+    (im.sum() + feat.sum() + depth.sum()).backward()
+    assert all(torch.isfinite(t.grad).all() for t in leaves.values())
+
+
+def test_batch_densify_stats_match_reference_bookkeeping(P=12000, W=144, H=112, C=4):
+    src = _scene(P, 0, False, seed=6)
+    rig = camera_rig(C, W, H)
+    sets = _settings(rig, W, H, "reference")
+    gen = torch.Generator(device=DEV).manual_seed(5)
+    up = torch.randn(C, 3, H, W, device=DEV, generator=gen)
+    acc, den, mx = torch.zeros(P, device=DEV), torch.zeros(P, device=DEV), torch.zeros(P, device=DEV)
+    for c in range(C):
+        m2 = torch.zeros(P, 3, device=DEV, requires_grad=True)
+        im, radius, depth = GaussianRasterizer(sets[c])(means2D=m2, **src)
+        im.backward(up[c])
+        seen = radius > 0
+        mx[seen] = torch.max(radius[seen].float(), mx[seen])
+        acc[seen] += torch.norm(m2.grad[seen, :2], dim=-1)
+        den[seen] += 1
+    ras = GaussianRasterizerBatch(sets, track_densify=True)
+    m2 = torch.zeros(P, 3, device=DEV, requires_grad=True)
+    im, radius, depth = ras(means2D=m2, **src)
+    im.backward(up)
+    st = ras.densify_stats
+    torch.testing.assert_close(st["denom"], den, rtol=0, atol=0)
+    torch.testing.assert_close(st["max_2D_radius"], mx, rtol=0, atol=0)
+    torch.testing.assert_close(st["means2D_gradient_accum"], acc, rtol=1e-5, atol=1e-6)
