@@ -383,7 +383,11 @@ class GaussianRasterizer(nn.Module):
 # gradients summed over the cameras, i.e. what autograd accumulates when the
 # same inputs feed C per-camera rasterizations.
 
-def _batch_settings(settings_list):
+def _batch_settings(settings_list, check_values=True):
+    """Validate a camera batch: one image size, scale modifier, SH degree,
+    numerics and background.  The background comparison reads device values
+    (a host synchronisation per camera), so GaussianRasterizerBatch does it
+    once at construction (check_values=False afterwards)."""
     rs0 = settings_list[0]
     for rs in settings_list[1:]:
         for name in ("image_height", "image_width", "scale_modifier", "sh_degree", "prefiltered", "debug"):
@@ -391,12 +395,27 @@ def _batch_settings(settings_list):
                 raise ValueError(f"the cameras of a batch share {name}")
         if _compat_of(rs) != _compat_of(rs0):
             raise ValueError("the cameras of a batch share compat")
-        if rs.bg is not rs0.bg and not torch.equal(rs.bg, rs0.bg):
+        if check_values and rs.bg is not rs0.bg and not torch.equal(rs.bg, rs0.bg):
             raise ValueError("the cameras of a batch share one background")
     for name in ("bg", "viewmatrix", "projmatrix", "campos"):
         if any(getattr(rs, name) is None for rs in settings_list):
             raise TypeError(f"GaussianRasterizationSettings.{name} is required")
     return rs0
+
+
+class _BatchCameras:
+    """The stacked per-camera device tensors and scalars of a validated
+    camera batch (built once per GaussianRasterizerBatch)."""
+
+    def __init__(self, settings_list, check_values=True):
+        self.rs0 = _batch_settings(settings_list, check_values)
+        self.C = len(settings_list)
+        self.pp = [_principal_point(rs) for rs in settings_list]
+        self.views = torch.stack([rs.viewmatrix.reshape(16) for rs in settings_list]).float().contiguous()
+        self.projs = torch.stack([rs.projmatrix.reshape(16) for rs in settings_list]).float().contiguous()
+        self.cpos = torch.stack([rs.campos.reshape(3) for rs in settings_list]).float().contiguous()
+        self.tx = [rs.tanfovx for rs in settings_list]
+        self.ty = [rs.tanfovy for rs in settings_list]
 
 
 class _RasterizeGaussiansBatch(torch.autograd.Function):
@@ -405,21 +424,19 @@ class _RasterizeGaussiansBatch(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, means3D, means2D, sh, colors_precomp, semantic_feature, opacities, scales, rotations,
-                cov3Ds_precomp, settings_list, label, densify_out):
-        rs0 = _batch_settings(settings_list)
+                cov3Ds_precomp, cams, label, densify_out):
+        if not isinstance(cams, _BatchCameras):
+            cams = _BatchCameras(cams)
+        rs0 = cams.rs0
         compat = _compat_of(rs0)
-        C = len(settings_list)
-        pp = [_principal_point(rs) for rs in settings_list]
-        views = torch.stack([rs.viewmatrix.reshape(16) for rs in settings_list])
-        projs = torch.stack([rs.projmatrix.reshape(16) for rs in settings_list])
-        cpos = torch.stack([rs.campos.reshape(3) for rs in settings_list])
+        C = cams.C
+        pp, views, projs, cpos = cams.pp, cams.views, cams.projs, cams.cpos
         sh = _empty_like_none(sh)
         colors_precomp = _empty_like_none(colors_precomp)
         scales = _empty_like_none(scales)
         rotations = _empty_like_none(rotations)
         cov3Ds_precomp = _empty_like_none(cov3Ds_precomp)
-        tx = [rs.tanfovx for rs in settings_list]
-        ty = [rs.tanfovy for rs in settings_list]
+        tx, ty = cams.tx, cams.ty
         out = _C.rasterize_gaussians_batch(
             rs0.bg, means3D, colors_precomp, semantic_feature, opacities, scales, rotations, rs0.scale_modifier,
             cov3Ds_precomp, views, projs, [p[0] for p in pp], [p[1] for p in pp], tx, ty, rs0.image_height,
@@ -482,9 +499,9 @@ def rasterize_gaussians_batch(means3D, means2D, sh, colors_precomp, semantic_fea
     (color, radii, feature_map, depth, alpha).  `densify_out`: optional
     (accum, denom, max_radius) fp32 [P] tensors the backward fills with the
     cameras' densification statistics (GradientSink.densify_stats)."""
+    cams = settings_list if isinstance(settings_list, _BatchCameras) else _BatchCameras(list(settings_list))
     return _RasterizeGaussiansBatch.apply(means3D, means2D, sh, colors_precomp, semantic_feature, opacities,
-                                          scales, rotations, cov3Ds_precomp, list(settings_list), label,
-                                          densify_out)
+                                          scales, rotations, cov3Ds_precomp, cams, label, densify_out)
 
 
 class GaussianRasterizerBatch(nn.Module):
@@ -494,11 +511,14 @@ class GaussianRasterizerBatch(nn.Module):
     summed over the cameras.  `track_densify=True` keeps the cameras'
     densification statistics of the last backward in `densify_stats`
     (the reference's accumulate_mean2d_gradient / max_2D_radius inputs,
-    external.py:136-140, train.py:288-290; see GradientSink)."""
+    external.py:136-140, train.py:288-290; see GradientSink).  The cameras'
+    matrices are stacked once at construction: build a new rasterizer when
+    they change (as the reference builds its settings per camera)."""
 
     def __init__(self, settings_list, track_densify=False):
         super().__init__()
         self.settings_list = list(settings_list)
+        self._cams = _BatchCameras(self.settings_list)
         self.track_densify = track_densify
         self.densify_stats = None
 
@@ -524,7 +544,7 @@ class GaussianRasterizerBatch(nn.Module):
             self.densify_stats = {"means2D_gradient_accum": dens[0], "denom": dens[1], "max_2D_radius": dens[2]}
         color, radii, feature_map, depth, alpha = rasterize_gaussians_batch(
             means3D, means2D, shs, colors_precomp, semantic_feature, opacities, scales, rotations,
-            cov3D_precomp, self.settings_list, lab, dens)
+            cov3D_precomp, self._cams, lab, dens)
         has_sem = semantic_feature is not None
         if has_label and has_sem:      # G3
             return color, radii, feature_map, depth, alpha
