@@ -458,22 +458,32 @@ void launch_tile_bucket(const TileArgs& a, const CamBatch& cb, hipStream_t s) {
   }
 }
 
+// Tile-length classes of the sort launches.  The LDS of a launch is sized to
+// its longest tile, and the occupancy with it: the short tiles (most of them:
+// ~660 keys on the bench camera) get their own launch with small LDS and many
+// workgroups per CU, the long ones follow with LDS for their length (and
+// global memory beyond TS_CAP_LONG).  Bench batch (27 cameras): sort 0.94 ->
+// 0.80 ms per step with the small class at 1024 keys.
+#ifndef GS_SORT_SMALL
+#define GS_SORT_SMALL 1024
+#endif
 template <int NT>
 static void tile_sort_launches(const TileArgs& a, const CamBatch& cb, int64_t max_len, hipStream_t s) {
   const dim3 grid(a.num_tiles, cb.C), block(NT);
   const int big = 0x7FFFFFFF;
-  // LDS sized to the longest tile when the plan's header is known on the host
-  if (max_len >= 0 && max_len <= TS_CAP) {
-    const int cap = max_len > 0 ? (int)max_len : 1;
-    hipLaunchKernelGGL(tile_sort_kernel<NT>, grid, block, 2 * sizeof(uint64_t) * cap, s, a, cb, cap, 0, big);
+  auto launch = [&](int cap, int lo, int hi) {
+    hipLaunchKernelGGL(tile_sort_kernel<NT>, grid, block, 2 * sizeof(uint64_t) * (cap > 0 ? cap : 1), s, a, cb,
+                       cap > 0 ? cap : 1, lo, hi);
+  };
+  if (max_len < 0) {  // unknown lengths: the LDS classes and the global-memory class
+    launch(TS_CAP, 0, TS_CAP);
+    launch(TS_CAP_LONG, TS_CAP, big);
     return;
   }
-  // Long tiles (large scenes): the common tiles keep TS_CAP-sized LDS and
-  // several workgroups per CU; the long ones follow in a second launch with
-  // up to the whole 160 KiB per workgroup (global memory beyond TS_CAP_LONG).
-  hipLaunchKernelGGL(tile_sort_kernel<NT>, grid, block, 2 * sizeof(uint64_t) * TS_CAP, s, a, cb, TS_CAP, 0, TS_CAP);
-  const int cap2 = (max_len >= 0 && max_len < TS_CAP_LONG) ? (int)max_len : TS_CAP_LONG;
-  hipLaunchKernelGGL(tile_sort_kernel<NT>, grid, block, 2 * sizeof(uint64_t) * cap2, s, a, cb, cap2, TS_CAP, big);
+  const int64_t small = GS_SORT_SMALL;
+  launch((int)(max_len < small ? max_len : small), 0, (int)small);
+  if (max_len > small) launch((int)(max_len < TS_CAP ? max_len : TS_CAP), (int)small, TS_CAP);
+  if (max_len > TS_CAP) launch((int)(max_len < TS_CAP_LONG ? max_len : TS_CAP_LONG), TS_CAP, big);
 }
 
 void launch_tile_sort(const TileArgs& a, const CamBatch& cb, int64_t max_len, int64_t L, hipStream_t s) {
