@@ -3,12 +3,21 @@
 
 Workload (BASELINE.json configs[2], the north-star metric's config): a
 Panoptic-sized scene of 300k Gaussians rendered from a 27-camera rig at
-800x800, through the drop-in GaussianRasterizer (G3 call pattern of
-dyn_train.py:244: precomputed colours + 32-channel semantic features + label),
-forward AND backward for every camera, then ONE flat all-reduce of the
-per-Gaussian gradients (N > 1) and an Adam step -- one step of the
-per-timestep training loop.  Data is synthetic (no network): seeded Gaussians
-and cameras (dynamic3dgaussians_amd/scene.py, camera.py).
+800x800 (G3 call pattern of dyn_train.py:244: precomputed colours +
+32-channel semantic features + label), forward AND backward for every camera,
+then ONE flat all-reduce of the per-Gaussian gradients (N > 1) and an Adam
+step -- one step of the per-timestep training loop.  Data is synthetic (no
+network): seeded Gaussians and cameras (dynamic3dgaussians_amd/scene.py,
+camera.py).
+
+Two call patterns (--mode; the headline is --mode, the other one is timed
+right after it on the same scene and reported as `other_mode`):
+  batch   the rank's cameras through GaussianRasterizerBatch: one launch per
+          stage for all of them, gradients summed over the cameras in-kernel
+          (the default: the multi-camera step as one pass);
+  percam  one drop-in GaussianRasterizer call per camera (the reference's
+          call pattern) over 4 HIP streams, gradients summed by a
+          GradientSink.
 
 Scaling is weak: every rank renders its own 27 cameras of a 27*N camera rig
 with the full Gaussian set replicated; value = all ranks' pixels / step time.
@@ -114,7 +123,9 @@ def params2rendervar(params, label):
         "rotations": torch.nn.functional.normalize(params["unnorm_rotations"]),
         "opacities": torch.sigmoid(params["logit_opacities"]),
         "scales": torch.exp(params["log_scales"]),
-        "means2D": torch.zeros_like(params["means3D"], requires_grad=True) + 0,
+        # screen-space means: the bench does no densification, so no gradient
+        # is requested for them (GradientSink / batch keep the statistics)
+        "means2D": torch.zeros_like(params["means3D"]),
         "label": label,
     }
     if "semantic_feature" in params:
@@ -153,33 +164,39 @@ def stage_bytes(L, Pv, P, W, H, F, C=3, TB=256):
     }
 
 
-def load_pmc_traffic(stage):
+def load_pmc_traffic(stage, cams_per_launch):
     """HBM bytes per launch from a committed rocprofv3 PMC summary, if any
-    (profiles/pmc_traffic.json, written by tools/pmc_traffic.py)."""
+    (profiles/pmc_traffic.json, written by tools/pmc_traffic.py: bytes per
+    camera, measured on 27-camera batch launches) x the launch's cameras."""
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        return d.get("bytes_per_launch", {}).get(stage)
+        per_cam = d.get("bytes_per_camera", {}).get(stage)
+        return None if per_cam is None else int(per_cam * cams_per_launch)
     except Exception:
         return None
 
 
 # stage -> (kernel key in profiles/pmc_valu.json, matrix-core cycles per MFMA)
-VALU_KERNEL = {"render_bwd": ("render_bwd", 32), "render_fwd": ("render_fwd", 64),
+# matrix-core cycles per MFMA on one SIMD (MI355X_MICROARCH.md constants):
+# v_mfma_f32_16x16x32_bf16 16 (backward), v_mfma_f32_32x32x16_bf16 32 (forward)
+VALU_KERNEL = {"render_bwd": ("render_bwd", 16), "render_fwd": ("render_fwd", 32),
                "sort": ("tile_sort", 0), "duplicate": ("tile_hist_kernel<true>", 0),
                "preprocess": ("preprocess_fwd", 0), "preprocess_bwd": ("preprocess_bwd", 0)}
 SIMDS, CLOCK_GHZ, VALU_ISSUE_CYC = 1024, 2.4, 4  # MI355X: 256 CUs x 4 SIMDs; wave64 VALU = 4 cycles
 
 
-def valu_view(stage, avg_ms):
+def valu_view(stage, avg_ms, cams_per_launch):
     """Issue-rate view of a kernel (the blend kernels are VALU/MFMA-issue
-    bound): committed per-launch instruction counts
-    (profiles/pmc_valu.json) over the live launch time."""
+    bound): committed per-camera instruction counts
+    (profiles/pmc_valu.json) x the launch's cameras, over the live launch time."""
     try:
-        d = json.load(open(os.path.join(REPO, "profiles", "pmc_valu.json")))["kernels"]
+        d = json.load(open(os.path.join(REPO, "profiles", "pmc_valu.json")))
+        if d.get("per") != "camera":
+            return None
         key, mfma_cyc = VALU_KERNEL[stage]
-        k = d[key]
+        k = {c: v * cams_per_launch for c, v in d["kernels"][key].items()}
     except Exception:
         return None
     cyc = k["SQ_INSTS_VALU"] * VALU_ISSUE_CYC + k.get("SQ_INSTS_MFMA", 0) * mfma_cyc
@@ -268,7 +285,7 @@ def main():
     # kernels (GradientSink: GS_FLAG_ACCUMULATE into per-stream buffers)
     # instead of autograd adding 7 gradient tensors per camera into the
     # leaves; GS_BENCH_SINK=0 restores autograd's accumulation.
-    use_sink = os.environ.get("GS_BENCH_SINK", "1") != "0" and args.mode == "percam"
+    use_sink = os.environ.get("GS_BENCH_SINK", "1") != "0"
     sink = GradientSink() if use_sink else None
     settings = make_settings(my_cams, dev, args.compat, sink)
     params, label = make_params(args, dev)
@@ -321,15 +338,13 @@ def main():
         # the leaves' accumulation crosses the camera streams by design
         torch.autograd.graph.set_warn_on_accumulate_grad_stream_mismatch(False)
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(device=dev) for _ in range(n_streams - 1)]
-    if args.mode == "batch":
-        n_streams = 1
-        # one upstream gradient per camera, materialized once (the batch's
-        # backward reads [C, ...] images like C per-camera backwards do)
-        C_ = len(settings)
-        up_color_b = up_color.expand(C_, -1, -1, -1).contiguous()
-        up_depth_b = up_depth.expand(C_, -1, -1, -1).contiguous()
-        up_feat_b = up_feat.expand(C_, -1, -1, -1).contiguous() if up_feat is not None else None
-        batch_ras = GaussianRasterizerBatch(settings)
+    # one upstream gradient per camera, materialized once (the batch's
+    # backward reads [C, ...] images like C per-camera backwards do)
+    C_ = len(settings)
+    up_color_b = up_color.expand(C_, -1, -1, -1).contiguous()
+    up_depth_b = up_depth.expand(C_, -1, -1, -1).contiguous()
+    up_feat_b = up_feat.expand(C_, -1, -1, -1).contiguous() if up_feat is not None else None
+    batch_ras = GaussianRasterizerBatch(settings)
 
     def step_batch():
         opt.zero_grad(set_to_none=True)
@@ -343,8 +358,8 @@ def main():
         bucket.all_reduce()
         opt.step()
 
-    def step():
-        if args.mode == "batch":
+    def step(mode=args.mode):
+        if mode == "batch":
             return step_batch()
         # grads set to None: the activation backward hands every parameter a
         # fresh gradient (no zero fills, no in-place accumulation launches)
@@ -421,6 +436,27 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    # the other call pattern on the same scene, timed the same way (reported
+    # beside the headline: the per-camera drop-in or the camera batch)
+    other = "percam" if args.mode == "batch" else "batch"
+    for _ in range(args.warmup):
+        step(other)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        step(other)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    other_elapsed = time.perf_counter() - t1
+    if world > 1:
+        t = torch.tensor([other_elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        other_elapsed = float(t.item())
+
     ms_per_step = elapsed / args.steps * 1e3
     mpix_total = world * args.cams * W_ * H_ / 1e6
     value = mpix_total / (ms_per_step / 1e3)
@@ -432,12 +468,13 @@ def main():
     avg_ms = stages[dom][0] / max(launches, 1)
     alg_per_launch = alg_bytes_total / max(launches, 1)
     achieved = alg_per_launch / (avg_ms / 1e3) / 1e9 if avg_ms > 0 else 0.0
-    traffic = load_pmc_traffic(dom)
+    cams_per_launch = args.cams if args.mode == "batch" else 1
+    traffic = load_pmc_traffic(dom, cams_per_launch)
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic, "kernel": dom, "avg_launch_ms": round(avg_ms, 4),
                 "alg_bytes_per_launch": int(alg_per_launch),
-                "issue": valu_view(dom, avg_ms)}
+                "issue": valu_view(dom, avg_ms, cams_per_launch), "cams_per_launch": cams_per_launch}
 
     result = {
         "metric": METRIC, "value": round(value, 3), "unit": "Mpix/s", "n_gpus": world,
@@ -449,7 +486,7 @@ def main():
                                "fwd+bwd of every camera + grad all-reduce + Adam",
                    "mode": ("camera batch (GaussianRasterizerBatch: one launch per stage for the rank's "
                             "cameras)" if args.mode == "batch" else "per camera (GaussianRasterizer drop-in)"),
-                   "optimizer": optim_kind, "streams": n_streams,
+                   "optimizer": optim_kind, "streams": n_streams if args.mode == "percam" else 1,
                    "grad_sum": ("in-kernel (camera sum in preprocess_bwd)" if args.mode == "batch" else
                                 "in-kernel (GradientSink)" if use_sink else "autograd"),
                    "gaussians": args.gaussians, "cams_per_rank": args.cams, "width": W_,
@@ -457,6 +494,9 @@ def main():
                    "parallelism": f"camera-sharded dp{world}"},
         "roofline": roofline,
         "stages_ms_per_step": {k: round(v, 4) for k, v in stage_ms.items()},
+        "other_mode": {"mode": other, "ms_per_step": round(other_elapsed / args.steps * 1e3, 3),
+                       "value": round(world * args.cams * W_ * H_ / 1e6 / (other_elapsed / args.steps), 3),
+                       "streams": n_streams if other == "percam" else 1},
         "instances_per_cam": int(np.mean([L for L, _, _ in inst])),
         "num_rendered_per_cam": int(np.mean([R for _, _, R in inst])),
     }

@@ -1,0 +1,67 @@
+#!/usr/bin/env python3
+"""Batch forward + backward of the bench scene (300k Gaussians, 27 cameras
+800x800, F = 32) through GaussianRasterizerBatch, a few times -- the program
+rocprofv3 --pmc runs to count the bench's kernels per launch (one launch = all
+27 cameras).
+
+    rocprofv3 --pmc FETCH_SIZE -- python3 tools/batch_steps.py --reps 2
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from dynamic3dgaussians_amd import _lib  # noqa: E402
+from dynamic3dgaussians_amd.camera import camera_rig  # noqa: E402
+from dynamic3dgaussians_amd.rasterizer import (GaussianRasterizationSettings,  # noqa: E402
+                                               GaussianRasterizerBatch)
+from dynamic3dgaussians_amd.scene import make_gaussians  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gaussians", type=int, default=300_000)
+    ap.add_argument("--cams", type=int, default=27)
+    ap.add_argument("--features", type=int, default=32)
+    ap.add_argument("--size", type=int, default=800)
+    ap.add_argument("--reps", type=int, default=2)
+    a = ap.parse_args()
+    _lib.load()
+    dev = torch.device("cuda", 0)
+    W = H = a.size
+    g = make_gaussians(a.gaussians, F=a.features, seed=0, device=dev)
+    bg = torch.zeros(3, device=dev)
+    sets = [GaussianRasterizationSettings(
+        image_height=H, image_width=W, tanfovx=c.tanfovx, tanfovy=c.tanfovy, c_x=c.c_x, c_y=c.c_y, bg=bg,
+        viewmatrix=torch.from_numpy(c.viewmatrix.copy()).to(dev),
+        projmatrix=torch.from_numpy(c.projmatrix.copy()).to(dev), sh_degree=0,
+        campos=torch.from_numpy(c.campos.copy()).to(dev), compat="reference") for c in camera_rig(a.cams, W, H)]
+    ras = GaussianRasterizerBatch(sets)
+    gen = torch.Generator(device=dev).manual_seed(1)
+    C = a.cams
+    up = [torch.randn(C, 3, H, W, device=dev, generator=gen), torch.randn(C, 1, H, W, device=dev, generator=gen)]
+    if a.features:
+        up.append(torch.randn(C, a.features, H, W, device=dev, generator=gen))
+    leaves = {k: g[k].clone().requires_grad_(True) for k in ("means3D", "colors", "opacities", "scales", "rotations")}
+    label = torch.ones(a.gaussians, device=dev)
+    for _ in range(a.reps):
+        kw = dict(means3D=leaves["means3D"], means2D=torch.zeros(a.gaussians, 3, device=dev),
+                  opacities=leaves["opacities"], colors_precomp=leaves["colors"], scales=leaves["scales"],
+                  rotations=leaves["rotations"], label=label)
+        if a.features:
+            im, radius, feat, depth, _ = ras(semantic_feature=g["semantic_feature"], **kw)
+            torch.autograd.backward([im, depth, feat], up)
+        else:
+            im, radius, depth, _ = ras(**kw)
+            torch.autograd.backward([im, depth], up)
+    torch.cuda.synchronize()
+    print("batch steps done", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -4,7 +4,10 @@
 FETCH_SIZE counts half the bytes of wide coalesced reads -> x2.  Writes the
 per-stage bytes to profiles/pmc_traffic.json for bench.py's roofline.traffic.
 
-    python tools/pmc_traffic.py FETCH_counter_collection.csv WRITE_counter_collection.csv
+    python tools/pmc_traffic.py FETCH_counter_collection.csv WRITE_counter_collection.csv [CAMS]
+
+CAMS = cameras per launch of the profiled program (tools/batch_steps.py: 27);
+the file keeps bytes per camera (bench.py multiplies by its cameras per launch).
 """
 import collections
 import csv
@@ -41,9 +44,12 @@ def main():
         wb = write.get(k, 0.0) * 1024.0
         stages[k[0]] += fb + wb
         detail[k[1]] = {"fetch_bytes_x2": fb, "write_bytes": wb}
-    out = {"bytes_per_launch": {k: int(v) for k, v in stages.items()}, "kernels": detail,
+    cams = int(sys.argv[3]) if len(sys.argv) > 3 else 1
+    out = {"bytes_per_camera": {k: int(v / cams) for k, v in stages.items()},
+           "bytes_per_launch": {k: int(v) for k, v in stages.items()}, "cams_per_launch": cams, "kernels": detail,
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate passes), FETCH_SIZE x2 "
-                     "(gfx950 correction), KB -> bytes; tools/stage_bench.py --features 32"}
+                     "(gfx950 correction), KB -> bytes; tools/batch_steps.py (300k Gaussians, "
+                     f"{cams} cameras 800x800 per launch, F = 32)"}
     path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
                         "pmc_traffic.json")
     json.dump(out, open(path, "w"), indent=1)

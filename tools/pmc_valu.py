@@ -19,9 +19,11 @@ def main():
             if key in r["Kernel_Name"]:
                 tot[key][r["Counter_Name"]] += float(r["Counter_Value"])
                 disp[key].add(r["Dispatch_Id"])
-    out = {"kernels": {k: {c: round(v / len(disp[k])) for c, v in d.items()} for k, d in tot.items()},
-           "method": "rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_SALU SQ_WAVES; per launch; "
-                     "tools/stage_bench.py --features 32"}
+    cams = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+    out = {"kernels": {k: {c: round(v / len(disp[k]) / cams) for c, v in d.items()} for k, d in tot.items()},
+           "per": "camera", "cams_per_launch": cams,
+           "method": "rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_SALU SQ_WAVES; per launch / cameras "
+                     f"per launch; tools/batch_steps.py ({cams} cameras per launch)"}
     path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
                         "pmc_valu.json")
     json.dump(out, open(path, "w"), indent=1)
