@@ -54,15 +54,21 @@ __device__ inline bool wave_any(bool p) { return __ballot(p) != 0ull; }
 // render_bwd 5.23 vs 5.55 ms per 27-camera step -- in camera-major order
 // every strip in flight adds into the same camera's accumulation records,
 // and the contended float atomics cost more than the cache locality gains.
+#ifndef GS_CAM_GROUP
+#define GS_CAM_GROUP 64  // cameras interleaved at a time (>= the batch: all of them)
+#endif
 __device__ inline void cam_slot(int bid, int C, int per_cam, int& cam, int& slot) {
 #ifdef GS_CAM_MAJOR
   (void)C;
   cam = bid / per_cam;
   slot = bid - cam * per_cam;
 #else
-  (void)per_cam;
-  cam = bid % C;
-  slot = bid / C;
+  // groups of GS_CAM_GROUP cameras one after the other, camera-minor inside
+  const int G = GS_CAM_GROUP < C ? GS_CAM_GROUP : C;
+  const int grp = bid / (G * per_cam), r = bid - grp * G * per_cam;
+  const int g0 = grp * G, gn = C - g0 < G ? C - g0 : G;  // the last group may be smaller
+  cam = g0 + r % gn;
+  slot = r / gn;
 #endif
 }
 template <class A>
