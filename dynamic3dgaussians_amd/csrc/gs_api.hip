@@ -150,7 +150,7 @@ TileArgs tile_args(int P, int W, int H, void* geom, void* image) {
   t.bsum = at<uint32_t>(image, il.bsum);
   t.meta = at<uint32_t>(image, il.meta);
   t.ranges = at<uint2>(image, il.ranges);
-  t.order = at<uint32_t>(image, il.order);
+  t.order = at<uint4>(image, il.order);
   return t;
 }
 }  // namespace
@@ -345,6 +345,7 @@ static int render_impl(const gs_gaussians* g, const gs_camera* cams, int C, int 
   RenderArgs ra{};
   ra.W = W; ra.H = H; ra.grid_x = gx; ra.num_tiles = gx * gy; ra.F = g->F; ra.compat = compat;
   ra.order = ta.order;
+  ra.smax = at<uint32_t>(image, il.smax);
   ra.ranges = ta.ranges; ra.point_list = total > 0 ? static_cast<const uint32_t*>(binning) : nullptr;
   ra.rec = rec; ra.feats = g->semantic_feature;
   ra.bg = cams[0].background;
@@ -388,8 +389,9 @@ static int backward_impl(const gs_gaussians* g, const gs_camera* cams, int C, co
   if (g->F > 0 && !accumulate) (void)hipMemsetAsync(dL_dsemantic, 0, sizeof(float) * (size_t)g->F * P, s);
   RenderBwdArgs ra{};
   ra.W = W; ra.H = H; ra.grid_x = gx; ra.num_tiles = gx * gy; ra.F = g->F; ra.compat = compat; ra.P = P;
-  ra.order = at<uint32_t>(image, il.order);
+  ra.order = at<uint4>(image, il.order);
   ra.ranges = at<uint2>(image, il.ranges);
+  ra.smax = at<uint32_t>(image, il.smax);
   ra.point_list = static_cast<const uint32_t*>(binning);
   ra.rec = at<float>(geom, gl.rec);
   ra.feats = g->semantic_feature;

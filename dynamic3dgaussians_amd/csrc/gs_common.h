@@ -140,7 +140,7 @@ struct SortLayout {
 // reference's num_rendered (bounding-rect instances), longest tile, status
 enum ImgMeta { M_L = 0, M_MAXN = 1, M_LREF = 2, M_STATUS = 3 };
 struct ImgLayout {
-  size_t ranges, n_contrib, thist, ttotal, bsum, meta, order, total;
+  size_t ranges, n_contrib, thist, ttotal, bsum, meta, order, smax, total;
   int64_t tiles;
   __host__ __device__ ImgLayout(int W, int H) {
     tiles = (int64_t)((W + TILE - 1) / TILE) * ((H + TILE - 1) / TILE);
@@ -152,7 +152,10 @@ struct ImgLayout {
     ttotal = o;    o = align_up(o + sizeof(uint32_t) * t, 256);
     bsum = o;      o = align_up(o + sizeof(uint32_t) * TB_BLOCKS, 256);  // per-block rect instances
     meta = o;      o = align_up(o + sizeof(uint32_t) * 4, 256);
-    order = o;     o = align_up(o + sizeof(uint32_t) * t, 256);   // tiles, longest list first
+    // dispatch records {tile, range.x, range.y, 0}, longest list first: one
+    // 16-B load gives a blend workgroup its tile and list
+    order = o;     o = align_up(o + sizeof(uint32_t) * 4 * t, 256);
+    smax = o;      o = align_up(o + sizeof(uint32_t) * 4 * t, 256);  // per strip item: longest pixel walk (forward -> backward)
     total = o;
   }
 };

@@ -66,11 +66,12 @@ struct PreprocessBwdArgs {
 
 struct RenderArgs {
   int W, H, grid_x, num_tiles, F, compat;
-  const uint32_t* order;  // num_tiles: dispatch order of the tiles (longest list first)
+  const uint4* order;  // num_tiles: dispatch records {tile, range.x, range.y, 0}, longest list first
   const uint2* ranges;
   const uint32_t* point_list;
   const float* rec;
   const float* feats;  // P x F
+  uint32_t* smax;      // 4 x num_tiles: per strip item (dispatch order) the longest pixel walk (max n_contrib)
   const float* bg;     // 3
   float* out_color;
   float* out_feature;
@@ -81,12 +82,13 @@ struct RenderArgs {
 
 struct RenderBwdArgs {
   int W, H, grid_x, num_tiles, F, compat, P;
-  const uint32_t* order;  // num_tiles: dispatch order of the tiles (longest list first)
+  const uint4* order;  // num_tiles: dispatch records {tile, range.x, range.y, 0}, longest list first
   const uint2* ranges;
   const uint32_t* point_list;
   const float* rec;
   const float* feats;
   const float* bg;
+  const uint32_t* smax;  // 4 x num_tiles: the forward's per-strip walk lengths
   const float* alphas;
   const uint32_t* n_contrib;
   const float* dL_dpix;
@@ -118,7 +120,7 @@ struct TileArgs {
   uint32_t* bsum;        // TB_BLOCKS: bounding-rect instances per block (the reference's count)
   uint32_t* meta;        // 4
   uint2* ranges;         // num_tiles
-  uint32_t* order;       // num_tiles: tiles by descending list length (dispatch order)
+  uint4* order;          // num_tiles: dispatch records {tile, range.x, range.y, 0}, longest list first
   uint64_t* keys;        // L
   uint64_t* keys2;       // L (sort twin for long tiles)
   uint32_t* plist;       // L
@@ -163,6 +165,7 @@ __host__ __device__ inline RenderArgs cam_render_args(const RenderArgs& a0, cons
   const int64_t go = c * cb.geom_stride, io = c * cb.img_stride, hw = (int64_t)a0.W * a0.H;
   a.order = shift_bytes(a0.order, io);
   a.ranges = shift_bytes(a0.ranges, io);
+  a.smax = shift_bytes(a0.smax, io);
   a.n_contrib = shift_bytes(a0.n_contrib, io);
   a.rec = shift_bytes(a0.rec, go);
   a.point_list = shift_bytes(a0.point_list, cb.bin_off[c]);
@@ -177,6 +180,7 @@ __host__ __device__ inline RenderBwdArgs cam_render_bwd_args(const RenderBwdArgs
   const int64_t go = c * cb.geom_stride, io = c * cb.img_stride, hw = (int64_t)a0.W * a0.H;
   a.order = shift_bytes(a0.order, io);
   a.ranges = shift_bytes(a0.ranges, io);
+  a.smax = shift_bytes(a0.smax, io);
   a.n_contrib = shift_bytes(a0.n_contrib, io);
   a.rec = shift_bytes(a0.rec, go);
   a.point_list = shift_bytes(a0.point_list, cb.bin_off[c]);

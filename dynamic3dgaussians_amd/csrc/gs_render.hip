@@ -74,17 +74,13 @@ __device__ inline void cam_slot(int bid, int C, int per_cam, int& cam, int& slot
 template <class A>
 __device__ inline int num_tiles_of(const A& a) { return a.num_tiles; }
 
-// Tile of dispatch slot `i`: the plan's order puts the longest tile lists
-// first (tile_offsets_kernel), so the long-running workgroups start early and
-// short ones fill the end of the launch instead of a few long ones trailing.
-__device__ inline int tile_of(const uint32_t* __restrict__ order, int i) {
-#ifdef GS_NO_TILE_ORDER
-  (void)order;
-  return i;
-#else
-  return (int)order[i];
-#endif
-}
+// Dispatch record of slot `i`: {tile, range.x, range.y, 0}.  The plan's
+// order puts the longest tile lists first (tile_order_kernel), so the
+// long-running workgroups start early and short ones fill the end of the
+// launch instead of a few long ones trailing; the record carries the tile's
+// list range too, so a workgroup starts with one 16-B load instead of two
+// dependent ones.
+__device__ inline uint4 tile_rec(const uint4* __restrict__ order, int i) { return order[i]; }
 
 // Work counters for kernel tuning (tools/render_stats.py); compiled only into
 // the "stats" build variant (-DGS_STATS), never into the product library.
@@ -160,8 +156,18 @@ __device__ inline RecRegs load_rec(const uint32_t* __restrict__ point_list, cons
 // record: h = (-a/2, -b, -c/2).  power = -1/2 (a dx^2 + c dy^2) - b dx dy
 // (CR/forward.cu:353-355) in a fixed fma order shared by the forward and the
 // backward kernel, so both make bit-identical alpha decisions.
+// The exponent is carried in base 2: the half conic is scaled by log2(e) once
+// per record, so alpha = opacity * 2^power' costs one v_exp_f32 and no
+// multiply per pixel (GS_OLD_MATH: natural-base exponent, exp(x) = 2^(x log2 e)).
+#ifdef GS_OLD_MATH
+constexpr float HC_SCALE = 1.0f;
+__device__ inline float gauss_exp(float p) { return fast_exp(p); }
+#else
+constexpr float HC_SCALE = 1.4426950408889634f;
+__device__ inline float gauss_exp(float p) { return __builtin_amdgcn_exp2f(p); }
+#endif
 __device__ inline float4 half_conic(const float4& q0, const float4& q1) {
-  return make_float4(-0.5f * q0.z, -q0.w, -0.5f * q1.x, 0.0f);
+  return make_float4((-0.5f * HC_SCALE) * q0.z, -HC_SCALE * q0.w, (-0.5f * HC_SCALE) * q1.x, 0.0f);
 }
 __device__ inline float gauss_power(float dx, float dy, const float4& h) {
   return fmaf(h.x * dx, dx, fmaf(h.z * dy, dy, (h.y * dx) * dy));
@@ -225,8 +231,7 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
   cam_slot(blockIdx.x, cb.C, num_tiles_of(a0) * 4 / GS_WPB_FWD, cam, bslot);
   const RenderArgs ca = cam_render_args(a0, cb, cam);
   const int W = ca.W, H = ca.H, grid_x = ca.grid_x, num_tiles = ca.num_tiles;
-  const uint32_t* __restrict__ order = ca.order;
-  const uint2* __restrict__ ranges = ca.ranges;
+  const uint4* __restrict__ order = ca.order;
   const uint32_t* __restrict__ point_list = ca.point_list;
   const float* __restrict__ rec = ca.rec;
   const float* __restrict__ feats = ca.feats;
@@ -255,7 +260,8 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
   // strip item = tile * 4 + wave (dispatch order, see strip_item)
   const int lane = threadIdx.x & 63, lw = threadIdx.x >> 6;  // lw: LDS slot of the wave
   const int item = strip_item(bslot, num_tiles, GS_WPB_FWD) + lw;
-  const int tile = tile_of(order, item >> 2), wave = item & 3;
+  const uint4 trec = tile_rec(order, item >> 2);
+  const int tile = (int)trec.x, wave = item & 3;
   const int tx = tile % grid_x, ty = tile / grid_x;
   const int qx0 = strip_x0(tx, wave), qy0 = strip_y0(ty, wave);  // lane = strip pixel (lane % STRIP_W, lane / STRIP_W)
   const int px = qx0 + lane % STRIP_W, py = qy0 + lane / STRIP_W;
@@ -263,7 +269,7 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
   const float pfx = (float)px, pfy = (float)py;
   const float sx0 = (float)qx0, sx1 = sx0 + (float)(STRIP_W - 1);
   const float sy0 = (float)qy0, sy1 = sy0 + (float)(STRIP_H - 1);
-  const uint2 range = ranges[tile];
+  const uint2 range = make_uint2(trec.y, trec.z);
 
   float T = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f, Dp = 0.f;
   float SF[NSF];
@@ -393,8 +399,8 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
         const float pa = gauss_power(a0.x - pfx, a0.y - pfy, make_float4(a0.z, a0.w, a1.x, 0.f));
         float pb = gauss_power(b0.x - pfx, b0.y - pfy, make_float4(b0.z, b0.w, b1.x, 0.f));
         pb = two ? pb : 1.0f;
-        const float ala = fminf(0.99f, a1.y * fast_exp(pa));
-        const float alb = fminf(0.99f, b1.y * fast_exp(pb));
+        const float ala = fminf(0.99f, a1.y * gauss_exp(pa));
+        const float alb = fminf(0.99f, b1.y * gauss_exp(pb));
         blend_step(ja, a1, a2, pa, ala);
         blend_step(jb, b1, b2, pb, alb);
         if constexpr (MF) {
@@ -431,7 +437,7 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
       const float4 r2 = s_rec[lw][j][2];
       const float dx = r0.x - pfx, dy = r0.y - pfy;
       const float power = gauss_power(dx, dy, make_float4(r0.z, r0.w, r1.x, 0.f));
-      const float alpha = fminf(0.99f, r1.y * fast_exp(power));
+      const float alpha = fminf(0.99f, r1.y * gauss_exp(power));
       const float test_T = T * (1 - alpha);
       // Branch-free blend (CR/forward.cu:350-380): non-blending lanes add
       // zero-weighted terms, and T / last / live are selected, so the loop
@@ -474,6 +480,11 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
   }
 blend_done:
   STAT_WAVE(16, 20, st_it);
+  {
+    // the strip's longest pixel walk: where the backward starts its walk
+    const uint32_t wl = wave_max_u(inside ? last : 0u);
+    if (lane == 0) ca.smax[item] = wl;
+  }
   if constexpr (MF) {
     if (nb > 0) flush(nb);
   }
@@ -504,6 +515,14 @@ blend_done:
     // channel fb*32 + (r&3) + 8(r>>2) + 4(l>>5), strip pixel (l&31) + 32 blk.
     float t_lo, t_hi;
     swap32(T, T, t_lo, t_hi);  // T of strip pixel (l&31) and (l&31)+32
+#ifndef GS_OLD_EPILOGUE
+    // Buffer stores: one per-lane byte offset (pixel + the lane's channel
+    // quarter) and the register's channel in the scalar offset, so the 16 x FB
+    // stores per pixel cost no address arithmetic on the vector ALUs.
+    const bool small = (uint64_t)F * HW * 4u < 0x7FFFFFFFull;
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(out_feature, (short)0,
+                                                        small ? (int)((uint64_t)F * HW * 4u) : 0, 0x00020000);
+#endif
 #pragma unroll
     for (int blk = 0; blk < 2; ++blk) {
       const int p = (lane & 31) + 32 * blk;
@@ -511,6 +530,22 @@ blend_done:
       if (qx < W && qy < H) {
         const size_t pix = (size_t)qy * W + qx;
         const float Tp = blk ? t_hi : t_lo;
+#ifndef GS_OLD_EPILOGUE
+        if (small) {
+          const uint32_t voff = (uint32_t)(pix + (size_t)(4 * (lane >> 5)) * HW) * 4u;
+#pragma unroll
+          for (int fb = 0; fb < FB; ++fb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int chs = fb * 32 + (r & 3) + 8 * (r >> 2);  // channel minus the lane's quarter
+              const int ch = chs + 4 * (lane >> 5);
+              const float b = (COMPAT == COMPAT_REFERENCE && ch < 3) ? bg[ch < 3 ? ch : 0] : 0.0f;
+              __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[2 * fb + blk][r] + Tp * b), rsrc, (int)voff,
+                                                    (int)((uint32_t)chs * (uint32_t)HW * 4u), 0);
+            }
+          continue;
+        }
+#endif
 #pragma unroll
         for (int fb = 0; fb < FB; ++fb)
 #pragma unroll
@@ -560,8 +595,7 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
   cam_slot(blockIdx.x, cb.C, num_tiles_of(a0) * 4 / GS_WPB_BWD, cam, bslot);
   const RenderBwdArgs ca = cam_render_bwd_args(a0, cb, cam);
   const int W = ca.W, H = ca.H, grid_x = ca.grid_x, num_tiles = ca.num_tiles;
-  const uint32_t* __restrict__ order = ca.order;
-  const uint2* __restrict__ ranges = ca.ranges;
+  const uint4* __restrict__ order = ca.order;
   const uint32_t* __restrict__ point_list = ca.point_list;
   const float* __restrict__ rec = ca.rec;
   const float* __restrict__ feats = ca.feats;
@@ -589,7 +623,8 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
   // strip item = tile * 4 + wave (dispatch order, see strip_item)
   const int lane = threadIdx.x & 63, lw = threadIdx.x >> 6;  // lw: LDS slot of the wave
   const int item = strip_item(bslot, num_tiles, GS_WPB_BWD) + lw;
-  const int tile = tile_of(order, item >> 2), wave = item & 3;
+  const uint4 trec = tile_rec(order, item >> 2);
+  const int tile = (int)trec.x, wave = item & 3;
   const int tx = tile % grid_x, ty = tile / grid_x;
   const int qx0 = strip_x0(tx, wave), qy0 = strip_y0(ty, wave);  // lane = strip pixel (lane % STRIP_W, lane / STRIP_W)
   const int px = qx0 + lane % STRIP_W, py = qy0 + lane / STRIP_W;
@@ -598,7 +633,7 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
   const float sx0 = (float)qx0, sx1 = sx0 + (float)(STRIP_W - 1);
   const float sy0 = (float)qy0, sy1 = sy0 + (float)(STRIP_H - 1);
   const float cx = sx0 + 0.5f * (STRIP_W - 1), cy = sy0 + 0.5f * (STRIP_H - 1);  // strip centre
-  const uint2 range = ranges[tile];
+  const uint2 range = make_uint2(trec.y, trec.z);
   const size_t HW = (size_t)H * W, pix = inside ? (size_t)py * W + px : 0;
 
   const float T_final = inside ? 1 - alphas[pix] : 0.0f;
@@ -612,6 +647,9 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
   const float dLd = inside && dL_ddepth ? dL_ddepth[pix] : 0.f;
   const float dLa = inside && dL_dalpha ? dL_dalpha[pix] : 0.f;
   const float bg_dot = bg[0] * dLp[0] + bg[1] * dLp[1] + bg[2] * dLp[2];
+#ifndef GS_OLD_MATH
+  const float tf_bg = T_final * bg_dot;  // the background term's per-pixel factor (exact in reference mode: T_final = 1)
+#endif
   float dLf_own[FIXED_FEAT ? F : 1];  // fixed mode: f . dL/dF feeds dL/dalpha
   if constexpr (FIXED_FEAT) {
 #pragma unroll
@@ -632,28 +670,40 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
     if (row < 3) src = dL_dpix ? dL_dpix + (size_t)row * HW : nullptr;
     else if (row == 3) src = dL_ddepth;
     else if (row - 4 < FW) src = dL_dfeat ? dL_dfeat + (size_t)(row - 4) * HW : nullptr;
+    // a lane's 8 pixels are one run of a strip row: two 16-B loads when the
+    // run lies inside the image and the rows are 16-B aligned (W % 4 == 0)
+    auto load8 = [&](const float* base, int p8, float (&x)[8]) {
+      const int qy = qy0 + p8 / STRIP_W, qx = qx0 + p8 % STRIP_W;
+#ifndef GS_OLD_PROLOGUE
+      if (STRIP_W % 8 == 0 && (W & 3) == 0 && qx + 8 <= W && qy < H &&
+          (reinterpret_cast<uintptr_t>(base) & 15) == 0) {
+        if (base) {
+          const float4* v = reinterpret_cast<const float4*>(base + (size_t)qy * W + qx);
+          const float4 a = v[0], b = v[1];
+          x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w; x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) x[j] = 0.f;
+        }
+        return;
+      }
+#endif
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const bool qin = qx + j < W && qy < H;
+        x[j] = (base && qin) ? base[(size_t)qy * W + qx + j] : 0.f;
+      }
+    };
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int p8 = 32 * s + kp0;
-      const int qy = qy0 + p8 / STRIP_W;
       float xw[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int qx = qx0 + p8 % STRIP_W + j;
-        const bool qin = qx < W && qy < H;
-        xw[j] = (src && qin) ? src[(size_t)qy * W + qx] : 0.f;
-      }
+      load8(src, p8, xw);
       split_bf16(xw, Xwh[s], Xwl[s]);
 #pragma unroll
       for (int cb = 0; cb < CB; ++cb) {
-        const float* fsrc = dL_dfeat ? dL_dfeat + (size_t)(16 * cb + row) * HW : nullptr;
         float xf[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int qx = qx0 + p8 % STRIP_W + j;
-          const bool qin = qx < W && qy < H;
-          xf[j] = (fsrc && qin) ? fsrc[(size_t)qy * W + qx] : 0.f;
-        }
+        load8(dL_dfeat ? dL_dfeat + (size_t)(16 * cb + row) * HW : nullptr, p8, xf);
         split_bf16(xf, Bfh[cb][s], Bfl[cb][s]);
       }
     }
@@ -667,6 +717,16 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const int g = lane & 15;
+    // every id the commits below need, read up front (independent LDS reads,
+    // one wait) instead of one dependent read per atomic
+    uint32_t fgid[4], agid[(WB * A_FEAT + 63) / 64];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) fgid[r] = f_bits(s_slot[lw][(lane >> 4) * 4 + r].w);
+#pragma unroll
+    for (int t = 0; t < (WB * A_FEAT + 63) / 64; ++t) {
+      const int i = lane + 64 * t;
+      agid[t] = i < WB * A_FEAT ? f_bits(s_slot[lw][i / A_FEAT].w) : 0u;
+    }
     bf16x8 Wh[2], Wl[2], Uh[2], Ul[2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -747,12 +807,15 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
-    for (int i = lane; i < WB * A_FEAT; i += 64) {
+    for (int t = 0; t < (WB * A_FEAT + 63) / 64; ++t) {
+      const int i = lane + 64 * t;
+      if (i >= WB * A_FEAT) break;
       const int slot = i / A_FEAT;
+      const uint32_t gi = agid[t];
 #ifdef GS_EXP_NO_ACC_ATOMIC
-      if (slot < nb && s_out[i] == 12345.f) acc[(size_t)ACC_STRIDE * f_bits(s_slot[lw][slot].w) + (i - A_FEAT * slot)] = 0.f;
+      if (slot < nb && s_out[i] == 12345.f) acc[(size_t)ACC_STRIDE * gi + (i - A_FEAT * slot)] = 0.f;
 #else
-      if (slot < nb) atomicAdd(acc + (size_t)ACC_STRIDE * f_bits(s_slot[lw][slot].w) + (i - A_FEAT * slot), s_out[i]);
+      if (slot < nb) atomicAdd(acc + (size_t)ACC_STRIDE * gi + (i - A_FEAT * slot), s_out[i]);
 #endif
     }
     if constexpr (FW > 0) {
@@ -776,10 +839,11 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int slot = (lane >> 4) * 4 + r;
+        const uint32_t gi = fgid[r];
 #ifdef GS_EXP_NO_FEAT_ATOMIC
-        if (slot < nb && cf[r] == 12345.f) dsem[(size_t)f_bits(s_slot[lw][slot].w) * F + 16 * cb + g] = 0.f;
+        if (slot < nb && cf[r] == 12345.f) dsem[(size_t)gi * F + 16 * cb + g] = 0.f;
 #else
-        if (slot < nb) atomicAdd(dsem + (size_t)f_bits(s_slot[lw][slot].w) * F + 16 * cb + g, cf[r]);
+        if (slot < nb) atomicAdd(dsem + (size_t)gi * F + 16 * cb + g, cf[r]);
 #endif
       }
     }
@@ -796,7 +860,8 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
   float Q = 0.f, lcd = 0.f, la = 0.f;
   int nb = 0;  // batch fill
 
-  const uint32_t wmax = __builtin_amdgcn_readfirstlane(wave_max_u(last));
+  // the strip's longest pixel walk, from the forward (max n_contrib)
+  const uint32_t wmax = __builtin_amdgcn_readfirstlane(ca.smax[item]);
   const uint32_t top = range.x + wmax;  // exclusive end of this wave's walk
   STAT(14, 1);
   STAT(15, wmax);
@@ -820,6 +885,10 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
       s_rec[lw][lane][2] = make_float4(q.q2.x, q.q2.y, 0.f, 0.f);
     }
     const uint32_t chunk_gid = q.gid;  // lane j: id of the chunk's j-th record
+#ifndef GS_OLD_MATH
+    // chunk entry j is in front of this pixel's last contributor iff j < lrel
+    const int lrel = (int)last - (int)(c0 - range.x);
+#endif
     uint64_t mask = __ballot(keep);
     STAT(8, 1);
     STAT(9, hi - c0);
@@ -840,9 +909,14 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
       const float dx = r0.x - pfx, dy = r0.y - pfy;
       const float op = r1.y;
       const float power = gauss_power(dx, dy, make_float4(r0.z, r0.w, r1.x, 0.f));
-      const float G = fast_exp(power);
+      const float G = gauss_exp(power);
       const float alpha = fminf(0.99f, op * G);
+#ifdef GS_OLD_MATH
       const bool valid = (k < last) && !(power > 0.0f) && !(alpha < ALPHA_MIN);
+#else
+      (void)k;
+      const bool valid = (j < lrel) && !(power > 0.0f) && !(alpha < ALPHA_MIN);
+#endif
       STAT(11, 1);
       STAT_INC(st_it);
       STAT(12, wave_any(valid));
@@ -865,7 +939,11 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
           cdot += fd;
         }
         Q = fmaf(la, lcd - Q, Q);
+#ifdef GS_OLD_MATH
         const float dL_dopa = fmaf(-T_final * rinv, bg_dot, (cdot - Q) * T);
+#else
+        const float dL_dopa = fmaf(-tf_bg, rinv, (cdot - Q) * T);
+#endif
         lcd = cdot;
         la = alpha;
         u = G * dL_dopa;

@@ -227,11 +227,13 @@ __global__ __launch_bounds__(OFF_T) void tile_offsets_kernel(const uint32_t* __r
 // plan -> header-read path the host waits for.
 __global__ __launch_bounds__(OFF_T) void tile_order_kernel(const uint32_t* __restrict__ ttotal0, int T,
                                                            const uint32_t* __restrict__ meta0,
-                                                           uint32_t* __restrict__ order0, CamBatch cb) {
+                                                           const uint2* __restrict__ ranges0,
+                                                           uint4* __restrict__ order0, CamBatch cb) {
   const int64_t io = blockIdx.x * cb.img_stride;  // one workgroup per camera
   const uint32_t* __restrict__ ttotal = shift_bytes(ttotal0, io);
   const uint32_t* __restrict__ meta = shift_bytes(meta0, io);
-  uint32_t* __restrict__ order = shift_bytes(order0, io);
+  const uint2* __restrict__ ranges = shift_bytes(ranges0, io);
+  uint4* __restrict__ order = shift_bytes(order0, io);
   __shared__ uint32_t s_obin[OFF_T];
   __shared__ uint32_t s_owsum[OFF_T / 64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -256,8 +258,11 @@ __global__ __launch_bounds__(OFF_T) void tile_order_kernel(const uint32_t* __res
   for (int w = 0; w < wave; ++w) base += s_owsum[w];
   s_obin[tid] = base;
   __syncthreads();
-  for (int t = a0; t < a1; ++t)
-    order[atomicAdd(&s_obin[OFF_T - 1 - min(ttotal[t] >> sh, (uint32_t)(OFF_T - 1))], 1u)] = (uint32_t)t;
+  for (int t = a0; t < a1; ++t) {
+    const uint2 r = ranges[t];
+    order[atomicAdd(&s_obin[OFF_T - 1 - min(ttotal[t] >> sh, (uint32_t)(OFF_T - 1))], 1u)] =
+        make_uint4((uint32_t)t, r.x, r.y, 0u);
+  }
 }
 
 // One tile per workgroup: LSD radix sort of its (depth bits << 32 | id) keys
@@ -412,7 +417,8 @@ __global__ __launch_bounds__(NT) void tile_sort_kernel(TileArgs a0, CamBatch cb,
   uint64_t* __restrict__ keys = ta.keys;
   uint64_t* __restrict__ keys2 = ta.keys2;
   uint32_t* __restrict__ plist = ta.plist;
-  const uint2 r = ta.ranges[ta.order[blockIdx.x]];  // longest tiles first
+  const uint4 o = ta.order[blockIdx.x];  // longest tiles first
+  const uint2 r = make_uint2(o.y, o.z);
   const int n = (int)(r.y - r.x);
   if (n == 0 || n <= lo || n > hi) return;
   if (n == 1) {
@@ -446,7 +452,8 @@ void launch_tile_plan(const TileArgs& a, const CamBatch& cb, int prefiltered, hi
 }
 
 void launch_tile_order(const TileArgs& a, const CamBatch& cb, hipStream_t s) {
-  hipLaunchKernelGGL(tile_order_kernel, dim3(cb.C), dim3(OFF_T), 0, s, a.ttotal, a.num_tiles, a.meta, a.order, cb);
+  hipLaunchKernelGGL(tile_order_kernel, dim3(cb.C), dim3(OFF_T), 0, s, a.ttotal, a.num_tiles, a.meta, a.ranges, a.order,
+                     cb);
 }
 
 void launch_tile_bucket(const TileArgs& a, const CamBatch& cb, hipStream_t s) {
