@@ -30,7 +30,7 @@ VARIANT = os.environ.get("GSPLAT_VARIANT", "")
 if VARIANT:
     LIB = os.path.join(OUT_DIR, f"libgsplat_hip_{VARIANT}.so")
     BUILD_DIR = os.path.join(OUT_DIR, f"obj_{VARIANT}")
-VARIANT_FLAGS = {"": [], "stats": ["-DGS_STATS"],
+VARIANT_FLAGS = {"": [], "stats": ["-DGS_STATS"], "stamps": ["-DGS_STAMPS"], "stamps_fine": ["-DGS_STAMPS", "-DGS_STAMPS_FINE"],
                  # timing experiments only (results are wrong by construction)
                  "exp_nofeat": ["-DGS_EXP_NO_FEAT_ATOMIC"], "exp_noacc": ["-DGS_EXP_NO_ACC_ATOMIC"],
                  "exp_noatomic": ["-DGS_EXP_NO_FEAT_ATOMIC", "-DGS_EXP_NO_ACC_ATOMIC"],

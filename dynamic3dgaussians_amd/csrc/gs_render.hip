@@ -108,6 +108,46 @@ __device__ unsigned long long g_stats[32];
 #define STAT_WAVE(i_max, i_hist, v) ((void)0)
 #endif
 
+// Wave-lifetime stamps (diagnostic "stamps" build only, -DGS_STAMPS): each
+// wave stores its stamps (s_memtime ticks since its start: loop start, loop
+// end, last output issued, outputs drained) into a host-provided buffer, one
+// 4 x u64 record per wave (forward waves first, backward waves at
+// g_stamp_bwd_off); plain per-wave stores, so the stamps add no contended
+// atomics.  The stamps serialise around themselves: read the shares.
+#ifdef GS_STAMPS
+__device__ unsigned long long* g_stamp_buf;
+__device__ long long g_stamp_bwd_off;
+__device__ inline unsigned long long stamp() {
+  __builtin_amdgcn_sched_barrier(0);
+  const unsigned long long t = __builtin_amdgcn_s_memtime();
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define STAMP(v) const unsigned long long v = stamp()
+__device__ inline void stamp_store(long long wave_id, unsigned long long a, unsigned long long b,
+                                   unsigned long long c, unsigned long long d, unsigned long long e = 0,
+                                   unsigned long long f = 0, unsigned long long g = 0, unsigned long long h = 0) {
+  if ((threadIdx.x & 63) == 0 && g_stamp_buf) {
+    unsigned long long* o = g_stamp_buf + 8 * wave_id;
+    o[0] = a; o[1] = b; o[2] = c; o[3] = d; o[4] = e; o[5] = f; o[6] = g; o[7] = h;
+  }
+}
+// prologue stages of the backward, each after a full wait (GS_STAMPS_FINE):
+// the stage latencies in isolation (the waits serialise the prologue)
+#ifdef GS_STAMPS_FINE
+#define FINE_STAMP(v) __builtin_amdgcn_s_waitcnt(0); const unsigned long long v = stamp()
+#else
+#define FINE_STAMP(v) const unsigned long long v = 0
+#endif
+extern "C" int gs_stamps_set(void* buf, long long bwd_off) {
+  int e = (int)hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_buf), &buf, sizeof(buf), 0, hipMemcpyHostToDevice);
+  if (e) return e;
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_bwd_off), &bwd_off, sizeof(bwd_off), 0, hipMemcpyHostToDevice);
+}
+#else
+#define STAMP(v) ((void)0)
+#endif
+
 // exp(x) as one v_exp_f32 (2^x) on x*log2(e): ~3 ulp instead of libm's
 // correctly-rounded-ish 14-instruction sequence.  Forward and backward use
 // the same function, so their alpha decisions agree bit for bit.
@@ -227,6 +267,7 @@ template <int F, int COMPAT>
 __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu(fwd_waves_per_simd<F>(), 8))) void render_fwd_kernel(
     RenderArgs a0, CamBatch cb) {
   // camera c of the batch: workgroups are dealt camera-minor (see cam_slot)
+  STAMP(ts0);
   int cam, bslot;
   cam_slot(blockIdx.x, cb.C, num_tiles_of(a0) * 4 / GS_WPB_FWD, cam, bslot);
   const RenderArgs ca = cam_render_args(a0, cb, cam);
@@ -345,6 +386,9 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
   STAT_DECL(st_it);
   STAT(6, 1);
   STAT(7, range.y - range.x);
+#ifdef GS_STAMPS
+  const unsigned long long ts1 = stamp();
+#endif
   if (!wave_any(live != 0u)) goto blend_done;
   for (uint32_t c0 = range.x; c0 < range.y; c0 += CHUNK) {
     const bool keep = (c0 + lane < range.y) && !strip_culled(q, sx0, sx1, sy0, sy1);
@@ -480,6 +524,7 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
   }
 blend_done:
   STAT_WAVE(16, 20, st_it);
+  STAMP(ts2);
   {
     // the strip's longest pixel walk: where the backward starts its walk
     const uint32_t wl = wave_max_u(inside ? last : 0u);
@@ -557,6 +602,12 @@ blend_done:
       }
     }
   }
+#ifdef GS_STAMPS
+  STAMP(ts3);
+  __builtin_amdgcn_s_waitcnt(0);
+  STAMP(ts4);
+  stamp_store((long long)blockIdx.x * GS_WPB_FWD + lw, ts1 - ts0, ts2 - ts0, ts3 - ts0, ts4 - ts0);
+#endif
 }
 
 // ------------------------------------------------------------------ backward
@@ -591,6 +642,7 @@ template <int F, int COMPAT>
 __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu(bwd_waves_per_simd<F, COMPAT>(), 8))) void render_bwd_kernel(
     RenderBwdArgs a0, CamBatch cb) {
   // camera c of the batch: workgroups are dealt camera-minor (see cam_slot)
+  STAMP(ts0);
   int cam, bslot;
   cam_slot(blockIdx.x, cb.C, num_tiles_of(a0) * 4 / GS_WPB_BWD, cam, bslot);
   const RenderBwdArgs ca = cam_render_bwd_args(a0, cb, cam);
@@ -636,6 +688,9 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
   const uint2 range = make_uint2(trec.y, trec.z);
   const size_t HW = (size_t)H * W, pix = inside ? (size_t)py * W + px : 0;
 
+#ifdef GS_STAMPS
+  FINE_STAMP(tA);
+#endif
   const float T_final = inside ? 1 - alphas[pix] : 0.0f;
   float T = T_final;
   const uint32_t last = inside ? n_contrib[pix] : 0u;
@@ -656,6 +711,10 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
     for (int c = 0; c < F; ++c) dLf_own[c] = inside && dL_dfeat ? dL_dfeat[(size_t)c * HW + pix] : 0.f;
   }
 
+#ifdef GS_STAMPS
+  asm volatile("" ::"v"(T_final), "v"(last), "v"(dLp[0]), "v"(dLp[1]), "v"(dLp[2]), "v"(dLd), "v"(dLa));
+  FINE_STAMP(tB);
+#endif
   // Constant matrix operands.  Lane l, k-step s (pixels 32s .. 32s+31) holds
   // strip pixels p = 32s + 8(l>>4) + j, j = 0..7 (8 consecutive pixels of one
   // strip row: column p % STRIP_W, row p / STRIP_W):
@@ -709,6 +768,9 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
     }
   }
 
+#ifdef GS_STAMPS
+  FINE_STAMP(tC);
+#endif
   // Contract the batch's nb slots and commit their sums (one atomic per
   // (Gaussian, component); slots >= nb hold stale weights whose results are
   // dropped -- the matrix rows are independent).
@@ -875,6 +937,13 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
     const uint32_t n0 = c0 > range.x + CHUNK ? c0 - CHUNK : range.x;
     gnext = load_gid(point_list, n0 + lane, top - 1);
   }
+#ifdef GS_STAMPS
+#ifdef GS_STAMPS_FINE
+  if (top > range.x) asm volatile("" ::"v"(q.q0.x), "v"(gnext));
+#endif
+  FINE_STAMP(tD);
+  const unsigned long long ts1 = stamp();
+#endif
   for (uint32_t hi = top; hi > range.x;) {
     const uint32_t c0 = hi > range.x + CHUNK ? hi - CHUNK : range.x;
     const bool keep = (c0 + lane < hi) && !strip_culled(q, sx0, sx1, sy0, sy1);
@@ -960,7 +1029,15 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
     hi = c0;
   }
   STAT_WAVE(17, 25, st_it);
+  STAMP(ts2);
   if (nb > 0) flush(nb);
+#ifdef GS_STAMPS
+  STAMP(ts3);
+  __builtin_amdgcn_s_waitcnt(0);
+  STAMP(ts4);
+  stamp_store(g_stamp_bwd_off + (long long)blockIdx.x * GS_WPB_BWD + lw, ts1 - ts0, ts2 - ts0, ts3 - ts0, ts4 - ts0,
+              tA ? tA - ts0 : 0, tB ? tB - ts0 : 0, tC ? tC - ts0 : 0, tD ? tD - ts0 : 0);
+#endif
 }
 
 // ------------------------------------------------------------------ dispatch

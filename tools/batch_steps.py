@@ -12,6 +12,7 @@ import argparse
 import os
 import sys
 
+import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -30,6 +31,7 @@ def main():
     ap.add_argument("--features", type=int, default=32)
     ap.add_argument("--size", type=int, default=800)
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--stamps", action="store_true", help="read the stamps build's wave-lifetime shares")
     a = ap.parse_args()
     _lib.load()
     dev = torch.device("cuda", 0)
@@ -49,6 +51,16 @@ def main():
         up.append(torch.randn(C, a.features, H, W, device=dev, generator=gen))
     leaves = {k: g[k].clone().requires_grad_(True) for k in ("means3D", "colors", "opacities", "scales", "rotations")}
     label = torch.ones(a.gaussians, device=dev)
+    stamps = None
+    if a.stamps:  # one 4 x u64 record per blend wave of the last launch (gs_stamps_set)
+        import ctypes
+        L = _lib.load(auto_build=False)
+        T = ((W + 15) // 16) * ((H + 15) // 16)
+        nf = T * 4 * C
+        buf = torch.zeros(2 * nf * 8, dtype=torch.int64, device=dev)
+        L.gs_stamps_set.argtypes = [ctypes.c_void_p, ctypes.c_longlong]
+        assert L.gs_stamps_set(ctypes.c_void_p(buf.data_ptr()), nf) == 0
+        stamps = (buf, nf)
     for _ in range(a.reps):
         kw = dict(means3D=leaves["means3D"], means2D=torch.zeros(a.gaussians, 3, device=dev),
                   opacities=leaves["opacities"], colors_precomp=leaves["colors"], scales=leaves["scales"],
@@ -60,6 +72,23 @@ def main():
             im, radius, depth, _ = ras(**kw)
             torch.autograd.backward([im, depth], up)
     torch.cuda.synchronize()
+    if a.stamps:
+        import json
+        st = stamps[0].cpu().numpy().reshape(-1, 8).astype(np.float64)
+        nf = stamps[1]
+        out = {}
+        for name, v in (("render_fwd", st[:nf]), ("render_bwd", st[nf:])):
+            v = v[v[:, 3] > 0]
+            tot = v[:, 3].sum()
+            out[name] = {"start": round(v[:, 0].sum() / tot, 4), "loop": round((v[:, 1] - v[:, 0]).sum() / tot, 4),
+                         "tail_issue": round((v[:, 2] - v[:, 1]).sum() / tot, 4),
+                         "drain": round((v[:, 3] - v[:, 2]).sum() / tot, 4), "waves": int(len(v)),
+                         "ticks_per_wave": round(float(tot / max(len(v), 1)))}
+            if v[:, 4:].any():  # GS_STAMPS_FINE: backward prologue stages after full waits
+                d = np.diff(np.concatenate([np.zeros((len(v), 1)), v[:, 4:8]], axis=1), axis=1)
+                out[name]["prologue"] = {k: round(float(d[:, i].sum() / tot), 4) for i, k in
+                                         enumerate(["to_record", "pixel_loads", "operands", "first_chunk"])}
+        print(json.dumps(out), flush=True)
     print("batch steps done", flush=True)
 
 
