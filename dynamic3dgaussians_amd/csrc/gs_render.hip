@@ -729,41 +729,69 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
     if (row < 3) src = dL_dpix ? dL_dpix + (size_t)row * HW : nullptr;
     else if (row == 3) src = dL_ddepth;
     else if (row - 4 < FW) src = dL_dfeat ? dL_dfeat + (size_t)(row - 4) * HW : nullptr;
-    // a lane's 8 pixels are one run of a strip row: two 16-B loads when the
-    // run lies inside the image and the rows are 16-B aligned (W % 4 == 0)
-    auto load8 = [&](const float* base, int p8, float (&x)[8]) {
-      const int qy = qy0 + p8 / STRIP_W, qx = qx0 + p8 % STRIP_W;
-#ifndef GS_OLD_PROLOGUE
-      if (STRIP_W % 8 == 0 && (W & 3) == 0 && qx + 8 <= W && qy < H &&
-          (reinterpret_cast<uintptr_t>(base) & 15) == 0) {
-        if (base) {
-          const float4* v = reinterpret_cast<const float4*>(base + (size_t)qy * W + qx);
-          const float4 a = v[0], b = v[1];
-          x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w; x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
-        } else {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) x[j] = 0.f;
-        }
-        return;
-      }
+    // A lane's 8 pixels are one run of a strip row.  Fast path (the strip
+    // lies inside the image, rows and planes 16-B aligned -- decided once per
+    // wave): every operand row with two 16-B loads, all issued back to back
+    // and split after (a per-row branch made the compiler wait for each row
+    // before issuing the next).  Absent planes read the alpha image and are
+    // zeroed after.  Slow path: per-pixel loads with bounds.
+    const float* fplane0 = dL_dfeat ? dL_dfeat + (size_t)row * HW : nullptr;
+    const bool lane_ok = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(fplane0) |
+                           reinterpret_cast<uintptr_t>(alphas)) & 15) == 0;
+    const bool fast = (W & 3) == 0 && (HW & 3) == 0 && qx0 + STRIP_W <= W && qy0 + STRIP_H <= H &&
+                      __ballot(!lane_ok) == 0ull;
+#ifdef GS_OLD_PROLOGUE
+    if (false) {
+#else
+    if (fast) {
 #endif
+      const float* sp = src ? src : alphas;
+      float4 rw[2][2], rf[CB1][2][2];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const bool qin = qx + j < W && qy < H;
-        x[j] = (base && qin) ? base[(size_t)qy * W + qx + j] : 0.f;
+      for (int s = 0; s < 2; ++s) {
+        const int p8 = 32 * s + kp0;
+        const size_t o = (size_t)(qy0 + p8 / STRIP_W) * W + qx0 + p8 % STRIP_W;
+        rw[s][0] = *reinterpret_cast<const float4*>(sp + o);
+        rw[s][1] = *reinterpret_cast<const float4*>(sp + o + 4);
+#pragma unroll
+        for (int cb = 0; cb < CB; ++cb) {
+          const float* fp = fplane0 ? fplane0 + (size_t)(16 * cb) * HW : alphas;
+          rf[cb][s][0] = *reinterpret_cast<const float4*>(fp + o);
+          rf[cb][s][1] = *reinterpret_cast<const float4*>(fp + o + 4);
+        }
       }
-    };
+      auto unpack = [](const float4 (&v)[2], bool on, float (&x)[8]) {
+        x[0] = on ? v[0].x : 0.f; x[1] = on ? v[0].y : 0.f; x[2] = on ? v[0].z : 0.f; x[3] = on ? v[0].w : 0.f;
+        x[4] = on ? v[1].x : 0.f; x[5] = on ? v[1].y : 0.f; x[6] = on ? v[1].z : 0.f; x[7] = on ? v[1].w : 0.f;
+      };
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int p8 = 32 * s + kp0;
-      float xw[8];
-      load8(src, p8, xw);
-      split_bf16(xw, Xwh[s], Xwl[s]);
+      for (int s = 0; s < 2; ++s) {
+        float x[8];
+        unpack(rw[s], src != nullptr, x);
+        split_bf16(x, Xwh[s], Xwl[s]);
 #pragma unroll
-      for (int cb = 0; cb < CB; ++cb) {
-        float xf[8];
-        load8(dL_dfeat ? dL_dfeat + (size_t)(16 * cb + row) * HW : nullptr, p8, xf);
-        split_bf16(xf, Bfh[cb][s], Bfl[cb][s]);
+        for (int cb = 0; cb < CB; ++cb) {
+          unpack(rf[cb][s], fplane0 != nullptr, x);
+          split_bf16(x, Bfh[cb][s], Bfl[cb][s]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int p8 = 32 * s + kp0;
+        const int qy = qy0 + p8 / STRIP_W, qx = qx0 + p8 % STRIP_W;
+        float xw[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xw[j] = (src && qx + j < W && qy < H) ? src[(size_t)qy * W + qx + j] : 0.f;
+        split_bf16(xw, Xwh[s], Xwl[s]);
+#pragma unroll
+        for (int cb = 0; cb < CB; ++cb) {
+          const float* fsrc = fplane0 ? fplane0 + (size_t)(16 * cb) * HW : nullptr;
+          float xf[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) xf[j] = (fsrc && qx + j < W && qy < H) ? fsrc[(size_t)qy * W + qx + j] : 0.f;
+          split_bf16(xf, Bfh[cb][s], Bfl[cb][s]);
+        }
       }
     }
   }
