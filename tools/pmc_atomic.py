@@ -1,0 +1,40 @@
+#!/usr/bin/env python3
+"""Memory-side float-atomic requests per launch from a rocprofv3
+--pmc TCC_EA0_ATOMIC_sum run (each request = one 64-B atomic segment,
+MI355X_MICROARCH.md "Global float atomics"), per camera, written to
+profiles/pmc_atomic.json for bench.py's roofline.atomics view.
+
+    python tools/pmc_atomic.py ATOMIC_counter_collection.csv [CAMS]
+"""
+import collections
+import csv
+import json
+import os
+import sys
+
+KERNELS = {"render_bwd": "render_bwd", "render_fwd": "render_fwd", "preprocess_bwd": "preprocess_bwd"}
+
+
+def main():
+    tot = collections.defaultdict(float)
+    disp = collections.defaultdict(set)
+    for r in csv.DictReader(open(sys.argv[1])):
+        if not r["Counter_Name"].startswith("TCC_EA0_ATOMIC"):
+            continue
+        for key, stage in KERNELS.items():
+            if key in r["Kernel_Name"]:
+                tot[stage] += float(r["Counter_Value"])
+                disp[stage].add(r["Dispatch_Id"])
+    cams = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+    out = {"requests_per_camera": {k: int(tot[k] / len(disp[k]) / cams) for k in tot},
+           "bytes_per_request": 64, "cams_per_launch": cams,
+           "method": "rocprofv3 --pmc TCC_EA0_ATOMIC_sum on tools/batch_steps.py (27-camera launches), "
+                     "per launch / cameras per launch"}
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_atomic.json")
+    with open(path, "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
