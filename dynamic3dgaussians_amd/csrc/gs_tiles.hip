@@ -291,11 +291,21 @@ __device__ inline uint64_t match_digit8(uint32_t d, uint64_t valid) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+#ifndef GS_BS_BITS
+#define GS_BS_BITS 10
+#endif
+constexpr int BS_BITS = GS_BS_BITS, BS_BINS = 1 << BS_BITS;
+constexpr int BS_KPT = 8;       // keys per thread held in registers
+constexpr int BS_RUN_MAX = 48;  // longest per-thread run handed to the insertion sort
+
 template <int NT>
 struct RadixSmem {
   static constexpr int TS_WAVES = NT / 64;
-  uint32_t wcnt[TS_WAVES][256];  // per-wave digit counts, then per-wave bases
-  uint32_t wsum[4];              // digit-scan partials (the first 256 threads)
+  union {
+    uint32_t wcnt[TS_WAVES][256];  // radix: per-wave digit counts, then per-wave bases
+    uint32_t bcnt[BS_BINS];        // bucket sort: bucket counts, then bucket starts
+  };
+  uint32_t wsum[TS_WAVES > 4 ? TS_WAVES : 4];  // scan partials
   int skip, unsorted;
   uint32_t dmin, dmax;  // depth-bit range of the tile
 };
@@ -406,6 +416,123 @@ __device__ __attribute__((always_inline)) KP tile_radix_sort(KP A, KP B, int n, 
   return src;
 }
 
+// MSD bucket sort of a tile held in LDS -- the common case.  The top
+// BS_BITS bits of the tile's depth-bit span pick one of BS_BINS buckets
+// (counted with returning LDS atomics: the returned count is the key's slot
+// in its bucket), one scan turns the counts into bucket starts, one scatter
+// places the keys, and every thread insertion-sorts its contiguous run of
+// BS_BINS / NT buckets by the full (depth bits << 32 | id) key -- the
+// reference's (depth, index) order, with no stability requirement anywhere
+// since the final comparison is on the unique full key.  Three barriers
+// after the counts instead of the radix sort's five per 8-bit pass.  Returns
+// false, with A untouched, when the tile has more keys than the registers
+// hold or some thread's run is longer than BS_RUN_MAX (depths crowded into
+// few buckets): the caller then runs the radix sort.
+
+template <int NT>
+__device__ __attribute__((always_inline)) bool tile_bucket_sort(const uint64_t* A, uint64_t* B, int n,
+                                                                RadixSmem<NT>& sm) {
+  uint32_t* cnt = sm.bcnt;
+  uint32_t* wsum = sm.wsum;
+  // BPT bins per owning thread (the first BS_BINS / BPT threads)
+  constexpr int BPT = BS_BINS >= NT ? BS_BINS / NT : 1, NW = NT / 64;
+  static_assert(BS_BINS % BPT == 0, "bins per thread");
+  const bool owner = threadIdx.x < BS_BINS / BPT;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (n > BS_KPT * NT) return false;
+  if (tid == 0) { sm.dmin = 0xFFFFFFFFu; sm.dmax = 0u; sm.skip = 0; }
+  uint32_t lmin = 0xFFFFFFFFu, lmax = 0u;
+  uint64_t k[BS_KPT];
+#pragma unroll
+  for (int j = 0; j < BS_KPT; ++j) {
+    const int i = tid + j * NT;
+    k[j] = i < n ? A[i] : 0ull;
+    if (i < n) {
+      lmin = min(lmin, (uint32_t)(k[j] >> 32));
+      lmax = max(lmax, (uint32_t)(k[j] >> 32));
+    }
+  }
+  if (owner) {
+#pragma unroll
+    for (int b = 0; b < BPT; ++b) cnt[tid * BPT + b] = 0u;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    lmin = min(lmin, (uint32_t)__shfl_xor((int)lmin, o, 64));
+    lmax = max(lmax, (uint32_t)__shfl_xor((int)lmax, o, 64));
+  }
+  __syncthreads();
+  if (lane == 0) {
+    atomicMin(&sm.dmin, lmin);
+    atomicMax(&sm.dmax, lmax);
+  }
+  __syncthreads();
+  const uint32_t dmin = sm.dmin, span = sm.dmax - dmin;
+  const int nbits = span ? 32 - __builtin_clz(span) : 0;
+  const int shift = nbits > BS_BITS ? nbits - BS_BITS : 0;
+  uint32_t bk[BS_KPT], rk[BS_KPT];
+#pragma unroll
+  for (int j = 0; j < BS_KPT; ++j) {
+    const int i = tid + j * NT;
+    bk[j] = (((uint32_t)(k[j] >> 32)) - dmin) >> shift;
+    rk[j] = i < n ? atomicAdd(&cnt[bk[j]], 1u) : 0u;
+  }
+  __syncthreads();
+  // thread t owns bins [t BPT, (t + 1) BPT): its run of keys in bucket order
+  uint32_t c[BPT], run = 0;
+#pragma unroll
+  for (int b = 0; b < BPT; ++b) {
+    c[b] = owner ? cnt[tid * BPT + b] : 0u;
+    run += c[b];
+  }
+  uint32_t inc = run;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
+  }
+  if (lane == 63) wsum[wave] = inc;
+  if (run > BS_RUN_MAX) sm.skip = 1;
+  __syncthreads();
+  if (sm.skip) return false;  // uniform: a crowded tile goes to the radix sort
+  uint32_t base = inc - run;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) base += w < wave ? wsum[w] : 0u;
+  if (owner) {
+    uint32_t e = base;
+#pragma unroll
+    for (int b = 0; b < BPT; ++b) {
+      cnt[tid * BPT + b] = e;  // own bins only: no barrier before the next reads
+      e += c[b];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < BS_KPT; ++j)
+    if (tid + j * NT < n) B[cnt[bk[j]] + rk[j]] = k[j];
+  __syncthreads();
+  // insertion sort of the thread's run by the full key
+  for (uint32_t a = base + 1; a < base + run; ++a) {
+    const uint64_t v = B[a];
+    uint32_t b = a;
+    while (b > base && B[b - 1] > v) {
+      B[b] = B[b - 1];
+      --b;
+    }
+    B[b] = v;
+  }
+  __syncthreads();
+  return true;
+}
+
+#ifdef GS_STATS
+// stats build only: [0] tiles sorted in LDS, [1] of them by the radix fallback
+__device__ unsigned long long g_sort_stats[2];
+extern "C" int gs_sort_stats_read(unsigned long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sort_stats), sizeof(g_sort_stats), 0, hipMemcpyDeviceToHost);
+}
+#endif
+
 // One tile per workgroup of NT threads (tiles of length lo < n <= hi; the
 // others exit).  Keys sorted in LDS up to `cap` (the launch's dynamic LDS),
 // in global memory beyond.
@@ -428,7 +555,21 @@ __global__ __launch_bounds__(NT) void tile_sort_kernel(TileArgs a0, CamBatch cb,
   if (n <= cap) {
     for (int i = threadIdx.x; i < n; i += NT) s_key[i] = keys[r.x + i];
     __syncthreads();
-    const uint64_t* out = tile_radix_sort<uint64_t*, NT>(s_key, s_key + cap, n, sm);
+    const uint64_t* out;
+#ifndef GS_NO_BUCKET_SORT
+    if (tile_bucket_sort<NT>(s_key, s_key + cap, n, sm)) {
+      out = s_key + cap;
+    } else
+#endif
+    {
+#ifdef GS_STATS
+      if (threadIdx.x == 0) atomicAdd(&g_sort_stats[1], 1ull);
+#endif
+      out = tile_radix_sort<uint64_t*, NT>(s_key, s_key + cap, n, sm);
+    }
+#ifdef GS_STATS
+    if (threadIdx.x == 0) atomicAdd(&g_sort_stats[0], 1ull);
+#endif
     for (int i = threadIdx.x; i < n; i += NT) plist[r.x + i] = (uint32_t)out[i];
   } else {  // longer than the LDS capacity of this launch: sort in global memory
     const uint64_t* out = tile_radix_sort<uint64_t*, NT>(keys + r.x, keys2 + r.x, n, sm);

@@ -109,6 +109,47 @@ def test_preprocess_and_binning_bitexact(kw):
     assert 0.0 <= frac < 1.0
 
 
+@pytest.mark.parametrize("mode", ["ties", "crowded", "ties_crowded"])
+def test_binning_depth_ties_and_crowded_depths(mode):
+    """The per-tile sort's two paths (gs_tiles.hip): the MSD bucket sort with
+    per-thread insertion sorts, and the radix sort it falls back to when the
+    depths crowd into few buckets.  'ties': groups of Gaussians share a mean
+    (bit-identical depths, so the list order inside a group is the Gaussian
+    index, as the reference's stable sort leaves it); 'crowded': most means
+    on a thin shell at one distance from the camera, a few elsewhere (most of
+    a tile's keys in one or two buckets of its span: the radix path)."""
+    inp = H.scene(P=4000, W=96, H=64)
+    m = inp["means3D"].clone()
+    g = torch.Generator().manual_seed(3)
+    if "ties" in mode:
+        src = torch.randint(0, m.shape[0], (m.shape[0] // 2,), generator=g)
+        dst = torch.randperm(m.shape[0], generator=g)[: m.shape[0] // 2]
+        m[dst] = m[src]
+    if "crowded" in mode:
+        # 90 % of the means on a thin shell around the camera, the rest where
+        # they were: each tile's depth span is set by the few outliers while
+        # most of its keys share one or two buckets
+        c = inp["campos"].float()
+        d = m - c
+        r = d.norm(dim=1, keepdim=True)
+        shell = c + d / r * r.median() * (1 + 1e-4 * torch.rand(m.shape[0], 1, generator=g))
+        pick = torch.rand(m.shape[0], generator=g) < 0.9
+        m = torch.where(pick[:, None], shell, m)
+    inp["means3D"] = m.contiguous()
+    gg = H.gpu_forward(inp)
+    o = H.oracle_forward(inp)
+    P, W, Hh = m.shape[0], inp["image_width"], inp["image_height"]
+    st_g = H.export_state(P, W, Hh, gg)
+    assert gg[0] == o[0]
+    H.check_tile_lists(st_g, o[6], W, Hh)
+    L = _lib.load(auto_build=False)
+    if hasattr(L, "gs_sort_stats_read"):  # stats build: which sort path ran
+        import ctypes
+        buf = (ctypes.c_ulonglong * 2)()
+        L.gs_sort_stats_read(buf)
+        print(f"{mode}: tiles sorted in LDS {buf[0]}, radix fallbacks {buf[1]}")
+
+
 # ---------------------------------------------------------------- forward
 
 @pytest.mark.parametrize("compat", ["reference", "fixed"])
