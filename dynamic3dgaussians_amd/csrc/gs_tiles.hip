@@ -291,27 +291,35 @@ __device__ inline uint64_t match_digit8(uint32_t d, uint64_t valid) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+// Bucket bits of the MSD sort: 2^10 buckets, 2^11 for the longer length
+// classes of long-tile scenes (tile_sort_launches).
 #ifndef GS_BS_BITS
 #define GS_BS_BITS 10
 #endif
-constexpr int BS_BITS = GS_BS_BITS, BS_BINS = 1 << BS_BITS;
-constexpr int BS_KPT = 8;       // keys per thread held in registers
+#ifndef GS_BS_BITS_LONG
+#define GS_BS_BITS_LONG 11
+#endif
+constexpr int BS_BITS = GS_BS_BITS, BS_BITS_LONG = GS_BS_BITS_LONG;
+#ifndef GS_BS_KPT
+#define GS_BS_KPT 8
+#endif
+constexpr int BS_KPT = GS_BS_KPT;  // keys per thread held in registers
 constexpr int BS_RUN_MAX = 48;  // longest per-thread run handed to the insertion sort
 
-template <int NT>
+template <int NT, int BINS>
 struct RadixSmem {
   static constexpr int TS_WAVES = NT / 64;
   union {
     uint32_t wcnt[TS_WAVES][256];  // radix: per-wave digit counts, then per-wave bases
-    uint32_t bcnt[BS_BINS];        // bucket sort: bucket counts, then bucket starts
+    uint32_t bcnt[BINS];           // bucket sort: bucket counts, then bucket starts
   };
   uint32_t wsum[TS_WAVES > 4 ? TS_WAVES : 4];  // scan partials
   int skip, unsorted;
   uint32_t dmin, dmax;  // depth-bit range of the tile
 };
 
-template <class KP, int TS_THREADS>
-__device__ __attribute__((always_inline)) KP tile_radix_sort(KP A, KP B, int n, RadixSmem<TS_THREADS>& sm) {
+template <class KP, int TS_THREADS, int BINS>
+__device__ __attribute__((always_inline)) KP tile_radix_sort(KP A, KP B, int n, RadixSmem<TS_THREADS, BINS>& sm) {
   constexpr int TS_WAVES = TS_THREADS / 64;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint64_t lt = (1ull << lane) - 1ull;
@@ -429,9 +437,10 @@ __device__ __attribute__((always_inline)) KP tile_radix_sort(KP A, KP B, int n, 
 // hold or some thread's run is longer than BS_RUN_MAX (depths crowded into
 // few buckets): the caller then runs the radix sort.
 
-template <int NT>
+template <int NT, int BITS>
 __device__ __attribute__((always_inline)) bool tile_bucket_sort(const uint64_t* A, uint64_t* B, int n,
-                                                                RadixSmem<NT>& sm) {
+                                                                RadixSmem<NT, (1 << BITS)>& sm) {
+  constexpr int BS_BINS = 1 << BITS;
   uint32_t* cnt = sm.bcnt;
   uint32_t* wsum = sm.wsum;
   // BPT bins per owning thread (the first BS_BINS / BPT threads)
@@ -469,7 +478,7 @@ __device__ __attribute__((always_inline)) bool tile_bucket_sort(const uint64_t* 
   __syncthreads();
   const uint32_t dmin = sm.dmin, span = sm.dmax - dmin;
   const int nbits = span ? 32 - __builtin_clz(span) : 0;
-  const int shift = nbits > BS_BITS ? nbits - BS_BITS : 0;
+  const int shift = nbits > BITS ? nbits - BITS : 0;
   uint32_t bk[BS_KPT], rk[BS_KPT];
 #pragma unroll
   for (int j = 0; j < BS_KPT; ++j) {
@@ -536,10 +545,10 @@ extern "C" int gs_sort_stats_read(unsigned long long* out) {
 // One tile per workgroup of NT threads (tiles of length lo < n <= hi; the
 // others exit).  Keys sorted in LDS up to `cap` (the launch's dynamic LDS),
 // in global memory beyond.
-template <int NT>
+template <int NT, int BITS>
 __global__ __launch_bounds__(NT) void tile_sort_kernel(TileArgs a0, CamBatch cb, int cap, int lo, int hi) {
   extern __shared__ uint64_t s_key[];  // 2 x cap keys
-  __shared__ RadixSmem<NT> sm;
+  __shared__ RadixSmem<NT, (1 << BITS)> sm;
   const TileArgs ta = cam_tile_args(a0, cb, blockIdx.y);
   uint64_t* __restrict__ keys = ta.keys;
   uint64_t* __restrict__ keys2 = ta.keys2;
@@ -557,7 +566,7 @@ __global__ __launch_bounds__(NT) void tile_sort_kernel(TileArgs a0, CamBatch cb,
     __syncthreads();
     const uint64_t* out;
 #ifndef GS_NO_BUCKET_SORT
-    if (tile_bucket_sort<NT>(s_key, s_key + cap, n, sm)) {
+    if (tile_bucket_sort<NT, BITS>(s_key, s_key + cap, n, sm)) {
       out = s_key + cap;
     } else
 #endif
@@ -565,14 +574,14 @@ __global__ __launch_bounds__(NT) void tile_sort_kernel(TileArgs a0, CamBatch cb,
 #ifdef GS_STATS
       if (threadIdx.x == 0) atomicAdd(&g_sort_stats[1], 1ull);
 #endif
-      out = tile_radix_sort<uint64_t*, NT>(s_key, s_key + cap, n, sm);
+      out = tile_radix_sort<uint64_t*, NT, (1 << BITS)>(s_key, s_key + cap, n, sm);
     }
 #ifdef GS_STATS
     if (threadIdx.x == 0) atomicAdd(&g_sort_stats[0], 1ull);
 #endif
     for (int i = threadIdx.x; i < n; i += NT) plist[r.x + i] = (uint32_t)out[i];
   } else {  // longer than the LDS capacity of this launch: sort in global memory
-    const uint64_t* out = tile_radix_sort<uint64_t*, NT>(keys + r.x, keys2 + r.x, n, sm);
+    const uint64_t* out = tile_radix_sort<uint64_t*, NT, (1 << BITS)>(keys + r.x, keys2 + r.x, n, sm);
     for (int i = threadIdx.x; i < n; i += NT) plist[r.x + i] = (uint32_t)out[i];
   }
 }
@@ -619,9 +628,19 @@ template <int NT>
 static void tile_sort_launches(const TileArgs& a, const CamBatch& cb, int64_t max_len, hipStream_t s) {
   const dim3 grid(a.num_tiles, cb.C), block(NT);
   const int big = 0x7FFFFFFF;
+  // the short class sorts with BS_BITS bucket bits; the longer classes of the
+  // wide (512-thread, long-tile) launches with BS_BITS_LONG.  Measured: 1080p /
+  // 1M Gaussians sort 1.02 -> 0.85 ms per 4 cameras at 11 bits; the bench
+  // scene's few longer tiles (256-thread launches) are faster at 10 bits
+  // (0.54 vs 0.60 ms per step).
+  constexpr bool long_bits = NT >= 512 && BS_BITS_LONG != BS_BITS;
   auto launch = [&](int cap, int lo, int hi) {
-    hipLaunchKernelGGL(tile_sort_kernel<NT>, grid, block, 2 * sizeof(uint64_t) * (cap > 0 ? cap : 1), s, a, cb,
-                       cap > 0 ? cap : 1, lo, hi);
+    if (lo == 0 || !long_bits)
+      hipLaunchKernelGGL((tile_sort_kernel<NT, BS_BITS>), grid, block, 2 * sizeof(uint64_t) * (cap > 0 ? cap : 1), s,
+                         a, cb, cap > 0 ? cap : 1, lo, hi);
+    else
+      hipLaunchKernelGGL((tile_sort_kernel<NT, BS_BITS_LONG>), grid, block,
+                         2 * sizeof(uint64_t) * (cap > 0 ? cap : 1), s, a, cb, cap > 0 ? cap : 1, lo, hi);
   };
   if (max_len < 0) {  // unknown lengths: the LDS classes and the global-memory class
     launch(TS_CAP, 0, TS_CAP);
