@@ -142,7 +142,7 @@ TileArgs tile_args(int P, int W, int H, void* geom, void* image) {
   t.P = P; t.W = W; t.H = H;
   t.grid_x = (W + TILE - 1) / TILE; t.grid_y = (H + TILE - 1) / TILE;
   t.num_tiles = (int)il.tiles;
-  t.rect = at<uint16_t>(geom, gl.rect);
+  t.rect = at<uint4>(geom, gl.rect);
   t.tiles = at<uint32_t>(geom, gl.tiles);
   t.rec = at<float>(geom, gl.rec);
   t.thist = at<uint32_t>(image, il.thist);
@@ -267,7 +267,7 @@ static int plan_impl(const gs_gaussians* g, const gs_camera* cams, int C, int pr
   a.cov3D = at<float>(geom, gl.cov3D);
   a.clamped = at<uint8_t>(geom, gl.clamped);
   a.tiles = at<uint32_t>(geom, gl.tiles);
-  a.rect = at<uint16_t>(geom, gl.rect);
+  a.rect = at<uint4>(geom, gl.rect);
   a.status = reinterpret_cast<int*>(ta.meta + M_STATUS);
   if (prefiltered)  // culled-but-prefiltered flags
     for (int c = 0; c < C; ++c) (void)hipMemsetAsync(shift_bytes(a.status, c * cb.img_stride), 0, 4, s);

@@ -101,7 +101,10 @@ struct GeomLayout {
     cov3D = o;     o = align_up(o + sizeof(float) * 6 * P, 256);
     clamped = o;   o = align_up(o + P, 256);
     tiles = o;     o = align_up(o + sizeof(uint32_t) * P, 256);
-    rect = o;      o = align_up(o + sizeof(uint16_t) * 4 * P, 256);  // tile rect x0,y0,x1,y1
+    // binning record, 16 B: tile rect x0 | y0 << 16, x1 | y1 << 16, depth
+    // bits, tiles_touched -- everything the plan and bucket passes read, in
+    // one 16-B load (the depth alone used to cost a 64-B render-record line)
+    rect = o;      o = align_up(o + sizeof(uint32_t) * 4 * P, 256);
     total = o;
   }
 };

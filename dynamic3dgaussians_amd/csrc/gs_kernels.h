@@ -28,7 +28,7 @@ struct PreprocessArgs {
   float* cov3D;
   uint8_t* clamped;
   uint32_t* tiles;
-  uint16_t* rect;  // P x 4: binning tile rect [x0, x1) x [y0, y1) (empty when culled)
+  uint4* rect;     // P: binning record {x0 | y0 << 16, x1 | y1 << 16, depth bits, tiles_touched} (rect [x0, x1) x [y0, y1), empty when culled)
   int* status;
 };
 
@@ -112,7 +112,7 @@ int launch_radix_sort(int64_t n, uint64_t* keys0, uint32_t* vals0, uint64_t* key
 // Tile binning (gs_tiles.hip).
 struct TileArgs {
   int P, W, H, grid_x, grid_y, num_tiles;
-  const uint16_t* rect;  // P x 4 (binning rect)
+  const uint4* rect;     // P: binning record (PreprocessArgs::rect)
   const uint32_t* tiles; // P: the reference's tiles_touched
   const float* rec;      // P x REC (depth)
   uint32_t* thist;       // TB_BLOCKS x num_tiles

@@ -196,7 +196,7 @@ __global__ __launch_bounds__(256) void preprocess_fwd_kernel(PreprocessArgs a0, 
   const PreprocessArgs a = cam_args(a0, batch, blockIdx.y);
   a.radii[g] = 0;
   a.tiles[g] = 0;
-  reinterpret_cast<ushort4*>(a.rect)[g] = make_ushort4(0, 0, 0, 0);
+  a.rect[g] = make_uint4(0u, 0u, 0u, 0u);
   const V3 p = ld3(a.means3D + 3 * g);
   const V3 pv = xf43(a.view, p);
   if (pv.z <= 0.0f) {  // in_frustum, Q8
@@ -272,8 +272,8 @@ __global__ __launch_bounds__(256) void preprocess_fwd_kernel(PreprocessArgs a0, 
   const float fy1 = fminf(fmaxf(floorf((py + ey) / TILE) + 1.f, (float)rmin.y), (float)rmax.y);
   const int bx0 = (int)fx0, by0 = (int)fy0;
   const int bx1 = max((int)fx1, bx0), by1 = max((int)fy1, by0);
-  reinterpret_cast<ushort4*>(a.rect)[g] =
-      make_ushort4((uint16_t)bx0, (uint16_t)by0, (uint16_t)bx1, (uint16_t)by1);
+  a.rect[g] = make_uint4((uint32_t)bx0 | ((uint32_t)by0 << 16), (uint32_t)bx1 | ((uint32_t)by1 << 16),
+                         __float_as_uint(pv.z), (uint32_t)((rmax.y - rmin.y) * (rmax.x - rmin.x)));
 }
 
 void launch_preprocess_fwd(const PreprocessArgs& a, const CamBatch& cb, hipStream_t s) {

@@ -59,14 +59,13 @@ __global__ __launch_bounds__(TB_THREADS) void tile_hist_kernel(TileArgs a0, CamB
     int x0 = 0, y0 = 0, w = 0, n = 0;
     uint64_t key = 0;
     if (g < g1) {
-      const ushort4 r = reinterpret_cast<const ushort4*>(a.rect)[g];
-      x0 = r.x;
-      y0 = r.y;
-      w = (int)r.z - (int)r.x;
-      n = w * ((int)r.w - (int)r.y);
-      if (WRITE && n > 0)
-        key = ((uint64_t)__float_as_uint(a.rec[(size_t)REC * g + R_DEPTH]) << 32) | (uint32_t)g;
-      if (!WRITE) rect_n += a.tiles[g];
+      const uint4 r = a.rect[g];  // {x0 | y0 << 16, x1 | y1 << 16, depth bits, tiles_touched}
+      x0 = (int)(r.x & 0xFFFFu);
+      y0 = (int)(r.x >> 16);
+      w = (int)(r.y & 0xFFFFu) - x0;
+      n = w * ((int)(r.y >> 16) - y0);
+      if (WRITE && n > 0) key = ((uint64_t)r.z << 32) | (uint32_t)g;
+      if (!WRITE) rect_n += r.w;
     }
     auto emit = [&](int x, int y, uint64_t k) {
       const uint32_t u = (uint32_t)(y * gx + x - t0);
