@@ -39,7 +39,8 @@ VARIANT_FLAGS = {"": [], "stats": ["-DGS_STATS"], "stamps": ["-DGS_STAMPS"], "st
                  "exp_oldmath": ["-DGS_OLD_MATH"], "exp_oldepi": ["-DGS_OLD_EPILOGUE"], "exp_oldpro": ["-DGS_OLD_PROLOGUE"], "exp_radixsort": ["-DGS_NO_BUCKET_SORT"], "exp_bs8": ["-DGS_BS_BITS=8"], "exp_bs9": ["-DGS_BS_BITS=9"], "exp_bs11": ["-DGS_BS_BITS=11"], "exp_bs12": ["-DGS_BS_BITS=12"],
                  "exp_ssmall512": ["-DGS_SORT_SMALL=512"], "exp_ssmall768": ["-DGS_SORT_SMALL=768"],
                  "exp_ssmall1536": ["-DGS_SORT_SMALL=1536"], "exp_cammajor": ["-DGS_CAM_MAJOR"], "exp_camg4": ["-DGS_CAM_GROUP=4"], "exp_camg9": ["-DGS_CAM_GROUP=9"], "exp_camg2": ["-DGS_CAM_GROUP=2"],
-                 "exp_kpt16": ["-DGS_BS_KPT=16"], "exp_bsl10": ["-DGS_BS_BITS_LONG=10"], "exp_bsl12": ["-DGS_BS_BITS_LONG=12"]}
+                 "exp_kpt16": ["-DGS_BS_KPT=16"], "exp_bsl10": ["-DGS_BS_BITS_LONG=10"], "exp_bsl12": ["-DGS_BS_BITS_LONG=12"],
+                 "exp_tbb64": ["-DGS_TB_BLOCKS=64"], "exp_tbb128": ["-DGS_TB_BLOCKS=128"]}
 ARCH = os.environ.get("GSPLAT_OFFLOAD_ARCH", "gfx950")
 
 # Per-file flags.  The preprocess kernels are compiled without FMA

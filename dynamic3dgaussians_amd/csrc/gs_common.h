@@ -82,7 +82,10 @@ __host__ __device__ inline int64_t sort_blocks(int64_t n) {
 // Tile bucketing geometry (gs_tiles.hip): TB_BLOCKS workgroups each own a
 // contiguous slice of the Gaussians and histogram their instances over (a
 // range of at most TB_BINS) tiles in LDS.
-constexpr int TB_BLOCKS = 256;
+#ifndef GS_TB_BLOCKS
+#define GS_TB_BLOCKS 256
+#endif
+constexpr int TB_BLOCKS = GS_TB_BLOCKS;  // per camera; a multiple of 64 (tile_rowscan_kernel, tile_offsets_kernel)
 #ifndef GS_TB_THREADS
 #define GS_TB_THREADS 1024
 #endif

@@ -110,14 +110,14 @@ __global__ __launch_bounds__(TB_THREADS) void tile_hist_kernel(TileArgs a0, CamB
 // scan over the blocks (each block's offset inside the tile) and the tile
 // total.  A workgroup takes RS_T tiles; thread (bg, tt) walks blocks
 // 16 bg .. 16 bg + 15 of tile tt (16 tiles x 4 B = one 64-B piece per block
-// row and load), the 16 block-group partial sums are scanned through LDS.
-static_assert(TB_BLOCKS == 256, "tile_rowscan_kernel: 16 block groups of 16 blocks");
-constexpr int RS_T = 16;
+// row and load), the RS_BG block-group partial sums are scanned through LDS.
+static_assert(TB_BLOCKS % 64 == 0 && TB_BLOCKS <= 256, "tile_rowscan_kernel: 4 to 16 block groups of 16 blocks");
+constexpr int RS_BG = TB_BLOCKS / 16, RS_T = 256 / RS_BG;
 __global__ __launch_bounds__(256) void tile_rowscan_kernel(uint32_t* __restrict__ thist0,
                                                            uint32_t* __restrict__ ttotal0, int T, CamBatch cb) {
   uint32_t* __restrict__ thist = shift_bytes(thist0, blockIdx.y * cb.img_stride);
   uint32_t* __restrict__ ttotal = shift_bytes(ttotal0, blockIdx.y * cb.img_stride);
-  __shared__ uint32_t s_part[16][RS_T];
+  __shared__ uint32_t s_part[RS_BG][RS_T];
   const int tid = threadIdx.x, tt = tid % RS_T, bg = tid / RS_T;
   const int t = blockIdx.x * RS_T + tt;
   const bool ok = t < T;
@@ -132,7 +132,7 @@ __global__ __launch_bounds__(256) void tile_rowscan_kernel(uint32_t* __restrict_
   __syncthreads();
   uint32_t off = 0, tot = 0;
 #pragma unroll
-  for (int g = 0; g < 16; ++g) {
+  for (int g = 0; g < RS_BG; ++g) {
     const uint32_t x = s_part[g][tt];
     off += g < bg ? x : 0u;
     tot += x;
