@@ -87,33 +87,53 @@ class FusedAdam(torch.optim.Optimizer):
                         decoupled_weight_decay=False)
         super().__init__(params, defaults)
 
+    def _next_step(self, p, state) -> float:
+        """Advance the parameter's step count (the CPU tensor state['step'],
+        as torch.optim.Adam keeps it) and return it as a float.  The float is
+        cached against the tensor's identity and version, so the usual step
+        costs one in-place fill instead of an add plus a device-less .item();
+        a step tensor replaced or modified from outside is re-read."""
+        st = state["step"]
+        c = self._step_cache.get(id(p))
+        t = (c[2] if (c is not None and c[0] is st and c[1] == st._version) else float(st.item())) + 1.0
+        st.fill_(t)
+        self._step_cache[id(p)] = (st, st._version, t)
+        return t
+
     @torch.no_grad()
     def step(self, closure=None, stats=None):
         loss = None
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        if not hasattr(self, "_step_cache"):
+            self._step_cache = {}
+            self._args_cache = {}
+        if len(self._step_cache) > 64:  # parameters replaced by densification: drop stale entries
+            live = {id(p) for g_ in self.param_groups for p in g_["params"]}
+            self._step_cache = {k: v for k, v in self._step_cache.items() if k in live}
         entries = []
         dev = None
         for group in self.param_groups:
             beta1, beta2 = group["betas"]
             for p in group["params"]:
-                if p.grad is None:
+                g = p.grad
+                if g is None:
                     continue
                 if not (p.is_cuda and p.dtype == torch.float32 and p.is_contiguous()):
                     raise _lib.GsplatError("FusedAdam needs contiguous fp32 device parameters")
-                if p.grad.is_sparse:
+                if g.is_sparse:
                     raise _lib.GsplatError("FusedAdam does not support sparse gradients")
                 state = self.state[p]
                 if len(state) == 0:  # torch.optim.Adam's lazy state init
                     state["step"] = torch.tensor(0.0, dtype=torch.float32)
                     state["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     state["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                state["step"] += 1.0
-                t = state["step"].item()
+                t = self._next_step(p, state)
                 bc1 = 1 - beta1 ** t
                 bc2 = 1 - beta2 ** t
-                g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
+                if not g.is_contiguous():
+                    g = g.contiguous()
                 entries.append((p, g, state["exp_avg"], state["exp_avg_sq"], (group["lr"] / bc1) * -1,
                                 bc2 ** 0.5, group))
                 dev = p.device
@@ -126,6 +146,7 @@ class FusedAdam(torch.optim.Optimizer):
         if dev is None:
             return loss
         L = _lib.load()
+        stream = _stream(dev)
         first = True
         for b in range(0, max(len(entries), 1), MAX_TENSORS):
             chunk = entries[b:b + MAX_TENSORS]
@@ -137,13 +158,18 @@ class FusedAdam(torch.optim.Optimizer):
             if not by_hyper:
                 by_hyper = {(0.9, 0.999, 1e-8): []}
             for (b1, b2, eps), es in by_hyper.items():
-                args = _lib.GsAdamArgs(n_tensors=len(es), beta1=b1, beta2=b2, eps=eps)
+                # the launch's argument block is reused from step to step; only
+                # the per-step fields are rewritten
+                key = (b, b1, b2, eps, len(es))
+                args = self._args_cache.get(key)
+                if args is None:
+                    args = self._args_cache[key] = _lib.GsAdamArgs(n_tensors=len(es), beta1=b1, beta2=b2, eps=eps)
                 for k, (p, g, m, v, step_size, bc2s, _) in enumerate(es):
-                    args.t[k] = _lib.GsAdamTensor(param=p.data_ptr(), grad=g.data_ptr(), exp_avg=m.data_ptr(),
-                                                  exp_avg_sq=v.data_ptr(), numel=p.numel(),
-                                                  step_size=step_size, bc2_sqrt=bc2s)
+                    tk = args.t[k]
+                    tk.param, tk.grad, tk.exp_avg, tk.exp_avg_sq = p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr()
+                    tk.numel, tk.step_size, tk.bc2_sqrt = p.numel(), step_size, bc2s
                 sp = ctypes.byref(st) if (first and st is not None) else None
-                _lib.check(L.gs_adam_step(ctypes.byref(args), sp, _stream(dev)), "adam step")
+                _lib.check(L.gs_adam_step(ctypes.byref(args), sp, stream), "adam step")
                 first = False
         if stats is not None:
             stats[0]["seen"] = stats[1] > 0

@@ -100,6 +100,13 @@ def main():
     for _ in range(20):
         step(False)
     torch.cuda.synchronize()
+    if os.environ.get("HOST_STEP_PROFILE"):
+        from torch.profiler import ProfilerActivity, profile
+        with profile(activities=[ProfilerActivity.CPU]) as prof:
+            for _ in range(20):
+                step(False)
+            torch.cuda.synchronize()
+        print(prof.key_averages().table(sort_by="self_cpu_time_total", row_limit=30), flush=True)
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step(True)
