@@ -184,3 +184,37 @@ def test_step_with_fused_stats_equals_separate():
         assert torch.equal(p1[k].detach(), p2[k].detach()), k
     for k in ("max_2D_radius", "means2D_gradient_accum", "denom", "seen"):
         assert torch.equal(v1[k], v2[k]), k
+
+
+def test_fused_adam_step_counts_follow_external_changes():
+    """FusedAdam caches each parameter's step count against its state tensor;
+    a step tensor replaced (load_state_dict, state surgery) or changed in place
+    from outside must be re-read, exactly as torch.optim.Adam reads it."""
+    from dynamic3dgaussians_amd.optim import FusedAdam
+    ref = make_params(P=4099, seed=3)
+    ours = _clone(ref)
+    o_ref = make_opt(torch.optim.Adam, ref)
+    o_ours = make_opt(FusedAdam, ours)
+
+    def both_step(step):
+        set_grads(ref, step)
+        set_grads(ours, step)
+        o_ref.step()
+        o_ours.step()
+
+    for step in range(3):
+        both_step(step)
+    for o, ps in ((o_ref, ref), (o_ours, ours)):
+        o.state[ps["means3D"]]["step"] = torch.tensor(40.0)   # replaced tensor
+        o.state[ps["log_scales"]]["step"].fill_(7.0)           # changed in place
+    both_step(3)
+    for o, ps in ((o_ref, ref), (o_ours, ours)):
+        assert float(o.state[ps["means3D"]]["step"]) == 41.0
+        assert float(o.state[ps["log_scales"]]["step"]) == 8.0
+    # a state_dict round trip (new step tensors) mid-training
+    o_ours.load_state_dict(o_ours.state_dict())
+    for step in range(4, 6):
+        both_step(step)
+    assert_params_equal(ref, ours)
+    for k in ref:
+        assert float(o_ours.state[ours[k]]["step"]) == float(o_ref.state[ref[k]]["step"])
