@@ -299,7 +299,13 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
   __shared__ float s_fw[GS_WPB_FWD][MF ? WBF + 1 : 1][68];  // +1: a pair may overfill by one
 
   // strip item = tile * 4 + wave (dispatch order, see strip_item)
+#ifdef GS_FWD_ULW
+  // the wave's LDS slot as a scalar: LDS addresses of the survivors' records
+  // become scalar arithmetic
+  const int lane = threadIdx.x & 63, lw = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#else
   const int lane = threadIdx.x & 63, lw = threadIdx.x >> 6;  // lw: LDS slot of the wave
+#endif
   const int item = strip_item(bslot, num_tiles, GS_WPB_FWD) + lw;
   const uint4 trec = tile_rec(order, item >> 2);
   const int tile = (int)trec.x, wave = item & 3;
@@ -400,6 +406,13 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
     }
     const uint32_t chunk_gid = q.gid;  // lane j: id of the chunk's j-th record
     uint64_t mask = __ballot(keep);
+#ifdef GS_FWD_SLAST
+    // list position (+1) of the chunk's first record as a scalar: a blending
+    // survivor's `last` is one select against an SGPR, no vector add
+    const uint32_t lbase = __builtin_amdgcn_readfirstlane(c0 - range.x + 1);
+#else
+    const uint32_t lbase = c0 - range.x + 1;
+#endif
     STAT(0, 1);
     STAT(1, range.y - c0 < CHUNK ? range.y - c0 : CHUNK);
     STAT(2, __builtin_popcountll(mask));
@@ -422,7 +435,7 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
         C2 = fmaf(r2.x, w, C2);
         Dp = fmaf(r2.y, w, Dp);
         T = blend ? test_T : T;
-        last = blend ? c0 + j - range.x + 1 : last;
+        last = blend ? lbase + (uint32_t)j : last;
         if constexpr (MF) {
           if (wave_any(blend)) {  // park it; the batch is flushed after the pair
             s_fw[lw][nb][lane] = w;  // 0 on non-blending lanes
@@ -496,7 +509,7 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
       C2 = fmaf(r2.x, w, C2);
       Dp = fmaf(r2.y, w, Dp);
       T = blend ? test_T : T;
-      last = blend ? c0 + j - range.x + 1 : last;
+      last = blend ? lbase + (uint32_t)j : last;
       STAT(4, wave_any(blend));
       STAT(5, __builtin_popcountll(__ballot(blend)));
       STAT(18, wave_any(blend) && ((__ballot(blend) & 0xFFFFFFFFull) == 0 || (__ballot(blend) >> 32) == 0));
@@ -673,7 +686,11 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
   __shared__ float4 s_slot[GS_WPB_BWD][WB];  // (mean x - cx, mean y - cy, opacity, id bits)
 
   // strip item = tile * 4 + wave (dispatch order, see strip_item)
+#ifdef GS_BWD_ULW
+  const int lane = threadIdx.x & 63, lw = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#else
   const int lane = threadIdx.x & 63, lw = threadIdx.x >> 6;  // lw: LDS slot of the wave
+#endif
   const int item = strip_item(bslot, num_tiles, GS_WPB_BWD) + lw;
   const uint4 trec = tile_rec(order, item >> 2);
   const int tile = (int)trec.x, wave = item & 3;

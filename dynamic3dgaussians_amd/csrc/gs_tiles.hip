@@ -74,6 +74,30 @@ __global__ __launch_bounds__(TB_THREADS) void tile_hist_kernel(TileArgs a0, CamB
         else atomicAdd(&s_bin[u], 1u);
       }
     };
+#ifdef GS_BUCKET_BATCH
+    if (WRITE) {
+      // All of the lane's slot claims first, then all of its key stores: the
+      // returning LDS atomics issue back to back instead of each waiting for
+      // the previous instance's store (one LDS round trip per rect instead of
+      // one per instance).  The wave's longest small rect bounds the unroll.
+      const int nl = (n > 0 && n <= LANE_TILES) ? n : 0;
+      const int nmax = (int)__builtin_amdgcn_readfirstlane(wave_max_u((uint32_t)nl));
+      uint32_t slot[LANE_TILES];
+      int x = x0, y = y0;
+#pragma unroll
+      for (int k = 0; k < LANE_TILES; ++k) {
+        slot[k] = 0xFFFFFFFFu;
+        if (k < nmax) {
+          const uint32_t u = (uint32_t)(y * gx + x - t0);
+          if (k < nl && u < (uint32_t)nt) slot[k] = atomicAdd(&s_bin[u], 1u);
+          if (++x == x0 + w) { x = x0; ++y; }
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < LANE_TILES; ++k)
+        if (k < nmax && slot[k] != 0xFFFFFFFFu) a.keys[slot[k]] = key;
+    } else
+#endif
     if (n > 0 && n <= LANE_TILES) {
       const int h = n / w;
       for (int y = y0; y < y0 + h; ++y)
