@@ -1,5 +1,5 @@
-# Batched bucket claims (product) vs the serial claim/store loop
-# (exp_bkt_serial): GPU suite on the product, then interleaved bench runs at
+# Batched bucket claims (exp_bkt_batch, -DGS_BUCKET_BATCH) vs the product's serial
+# claim/store loop (measured as the product in r02f; not kept): GPU suite, then interleaved bench runs at
 # the bench scene and at BASELINE configs[4] scale.  -> gpurun_out/r2f_bkt
 set -o pipefail
 R=$GRAFT_REPO_ROOT
@@ -11,7 +11,7 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
 tail -2 $O/tests.log
 fi
 for rep in $(seq 1 ${REPS:-3}); do
-for v in - exp_bkt_serial; do
+for v in - exp_bkt_batch; do
   n=$v; [ "$v" = "-" ] && v="" && n=product
   GSPLAT_VARIANT=$v timeout -k 10 200 python bench.py --no-cpu-baseline > $O/b_${n}_$rep.json 2> $O/b_${n}_$rep.err || { tail -5 $O/b_${n}_$rep.err; exit 1; }
   python -c "import json; d=json.load(open('$O/b_${n}_$rep.json')); print('bench', '$n', d['value'], d['ms_per_step'], {k: round(v,3) for k, v in d['stages_ms_per_step'].items()})"

@@ -1,4 +1,4 @@
-# Polynomial exponent (product) vs the previous tree (variant "old", tools/build_rev.sh HEAD):
+# Polynomial exponent (then the product; reverted) vs the previous tree (variant "old", tools/build_rev.sh HEAD):
 # GPU suite on the product, then interleaved bench runs at
 # the bench scene and at BASELINE configs[4] scale.  -> gpurun_out/r2f_poly
 set -o pipefail
