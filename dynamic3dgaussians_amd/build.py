@@ -43,7 +43,8 @@ VARIANT_FLAGS = {"": [], "stats": ["-DGS_STATS"], "stamps": ["-DGS_STAMPS"], "st
                  "exp_tbb64": ["-DGS_TB_BLOCKS=64"], "exp_tbb128": ["-DGS_TB_BLOCKS=128"],
                  "exp_fulw": ["-DGS_FWD_ULW", "-DGS_FWD_SLAST"],
                  "exp_ulw": ["-DGS_FWD_ULW", "-DGS_FWD_SLAST", "-DGS_BWD_ULW"],
-                 "exp_bkt_batch": ["-DGS_BUCKET_BATCH"]}
+                 "exp_bkt_batch": ["-DGS_BUCKET_BATCH"],
+                 "exp_fdummy": ["-DGS_FWD_DUMMY"], "exp_fdummy_ulw": ["-DGS_FWD_DUMMY", "-DGS_FWD_ULW", "-DGS_FWD_SLAST"]}
 ARCH = os.environ.get("GSPLAT_OFFLOAD_ARCH", "gfx950")
 
 # Per-file flags.  The preprocess kernels are compiled without FMA

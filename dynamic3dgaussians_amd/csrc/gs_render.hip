@@ -294,7 +294,13 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
   constexpr int NSF = (!MF && F > 0) ? F : 1;
   constexpr int WBF = 16;                    // Gaussians per matrix batch
   // per record: (x, y, -a/2, -b) (-c/2, opacity, r, g) (b, depth, -, -)
+#ifdef GS_FWD_DUMMY
+  // + slot CHUNK: an empty record (zero conic and opacity: power 0, alpha 0)
+  // standing in for the missing second survivor of a pair
+  __shared__ float4 s_rec[GS_WPB_FWD][CHUNK + 1][3];
+#else
   __shared__ float4 s_rec[GS_WPB_FWD][CHUNK][3];
+#endif
   // batch weights [slot][pixel] (row pad 4: conflict-free writes and reads)
   __shared__ float s_fw[GS_WPB_FWD][MF ? WBF + 1 : 1][68];  // +1: a pair may overfill by one
 
@@ -317,6 +323,9 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
   const float sx0 = (float)qx0, sx1 = sx0 + (float)(STRIP_W - 1);
   const float sy0 = (float)qy0, sy1 = sy0 + (float)(STRIP_H - 1);
   const uint2 range = make_uint2(trec.y, trec.z);
+#ifdef GS_FWD_DUMMY
+  if (lane < 3) s_rec[lw][CHUNK][lane] = make_float4(0.f, 0.f, 0.f, 0.f);
+#endif
 
   float T = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f, Dp = 0.f;
   float SF[NSF];
@@ -448,14 +457,20 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
         const int ja = __builtin_ctzll(mask);
         mask &= mask - 1;
         const bool two = mask != 0;
+#ifdef GS_FWD_DUMMY
+        const int jb = two ? __builtin_ctzll(mask) : CHUNK;
+#else
         const int jb = two ? __builtin_ctzll(mask) : ja;
+#endif
         if (two) mask &= mask - 1;
         STAT(3, two ? 2 : 1);
         const float4 a0 = s_rec[lw][ja][0], a1 = s_rec[lw][ja][1], a2 = s_rec[lw][ja][2];
         const float4 b0 = s_rec[lw][jb][0], b1 = s_rec[lw][jb][1], b2 = s_rec[lw][jb][2];
         const float pa = gauss_power(a0.x - pfx, a0.y - pfy, make_float4(a0.z, a0.w, a1.x, 0.f));
         float pb = gauss_power(b0.x - pfx, b0.y - pfy, make_float4(b0.z, b0.w, b1.x, 0.f));
+#ifndef GS_FWD_DUMMY
         pb = two ? pb : 1.0f;
+#endif
         const float ala = fminf(0.99f, a1.y * gauss_exp(pa));
         const float alb = fminf(0.99f, b1.y * gauss_exp(pb));
         blend_step(ja, a1, a2, pa, ala);
