@@ -407,6 +407,13 @@ __device__ inline void cov3d_bwd(V3 scale, float mod, float4 rot, const float d[
 // per output), so a batch costs one pass over the Gaussian state instead of
 // C read-modify-write passes.  Every output element is written, so outputs
 // need no zero-fill.
+#ifndef GS_PBWD_GROUP
+#define GS_PBWD_GROUP 2
+#endif
+constexpr int PB_GROUP = GS_PBWD_GROUP;  // cameras whose operands are requested together
+// SH: the SH-coefficient backward is compiled in (launched when a.shs is set);
+// the precomputed-colour instantiation carries none of its registers.
+template <bool SH>
 __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdArgs a, CamBatch cb) {
   const int g = blockIdx.x * 256 + threadIdx.x;
   if (g >= a.P) return;
@@ -420,21 +427,51 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdArgs a
   float dcov[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   float st_acc = 0.f, st_den = 0.f, st_rad = 0.f;
   bool any_vis = false, sh_written = ac != 0;
-  for (int c = 0; c < cb.C; ++c) {
+  // The cameras are walked in groups of PB_GROUP: every operand of a group
+  // (radius, accumulation record, conic, 3D covariance of each camera) is
+  // requested before the first of them is used, so the group's loads are in
+  // flight together instead of one dependent round trip (radius, then the
+  // rest) per camera.  The sums still run camera by camera in order.
+  float c3pre[6];
+  if (a.cov3D_precomp) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) c3pre[i] = a.cov3D_precomp[6 * g + i];
+  }
+  for (int cg = 0; cg < cb.C; cg += PB_GROUP) {
+    int radk[PB_GROUP];
+    float acck[PB_GROUP][A_FEAT], c3k[PB_GROUP][6], cck[PB_GROUP];
+    float4 conk[PB_GROUP];
+#pragma unroll
+    for (int k = 0; k < PB_GROUP; ++k) {
+      const int c = cg + k < cb.C ? cg + k : cb.C - 1;  // a short last group re-reads a valid camera
+      const float* acc = a.acc + ((size_t)c * a.P + g) * ACC_STRIDE;
+#pragma unroll
+      for (int i = 0; i < A_FEAT; ++i) acck[k][i] = acc[i];
+      radk[k] = a.radii[(size_t)c * a.P + g];
+      const float* rec = shift_bytes(a.rec, c * cb.geom_stride) + (size_t)REC * g;
+      conk[k] = reinterpret_cast<const float4*>(rec)[0];  // x, y, a, b
+      cck[k] = rec[R_CC];
+      const float* c3 = a.cov3D_precomp ? c3pre : shift_bytes(a.cov3D, c * cb.geom_stride) + 6 * g;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) c3k[k][i] = c3[i];
+    }
+#pragma unroll
+  for (int k = 0; k < PB_GROUP; ++k) {
+    const int c = cg + k;
+    if (c >= cb.C) break;
     const bool first = c == 0;
     auto add = [&](float& sum, float v) { sum = first ? v : sum + v; };
-    const float* acc = a.acc + ((size_t)c * a.P + g) * ACC_STRIDE;
-    const int rad = a.radii[(size_t)c * a.P + g];
+    const float* acc = acck[k];
+    const int rad = radk[k];
     const bool vis = rad > 0;
-    const float* rec = shift_bytes(a.rec, c * cb.geom_stride) + (size_t)REC * g;
     // blend gradients -> output tensors (zero for culled Gaussians: never touched)
     // dL/dmean2D = sum over pixels of dL/dG * dG/d(offset) * ndc scale
     // (CR/backward.cu:616-621): from the blend kernel's basis sums (AccField),
     // the conic and ddelx_dx = 0.5 W, ddely_dy = 0.5 H (:520-521).
     float am0 = 0.f, am1 = 0.f;
     if (vis) {
-      const float4 con = reinterpret_cast<const float4*>(rec)[0];  // x, y, a, b
-      const float cc = rec[R_CC];
+      const float4 con = conk[k];
+      const float cc = cck[k];
       const float sex = acc[A_MX], sey = acc[A_MY];
       am0 = (-con.z * sex - con.w * sey) * (0.5f * (float)a.W);
       am1 = (-cc * sey - con.w * sex) * (0.5f * (float)a.H);
@@ -460,11 +497,7 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdArgs a
     const float c_x = cb.c_x[c], c_y = cb.c_y[c], tan_fovx = cb.tanx[c], tan_fovy = cb.tany[c];
     const float focal_y = (float)a.H / (2.0f * tan_fovy);  // CR/rasterizer_impl.cu:398-399
     const float focal_x = (float)a.W / (2.0f * tan_fovx);
-    const float* c3 = a.cov3D_precomp ? a.cov3D_precomp + 6 * g
-                                      : shift_bytes(a.cov3D, c * cb.geom_stride) + 6 * g;
-    float c3v[6];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) c3v[i] = c3[i];
+    const float(&c3v)[6] = c3k[k];
     // dL/dconic = -1/2 sum e (dx^2, dx dy, dy^2) (CR/backward.cu:622-624)
     const float dcx = -0.5f * acc[A_CA], dcy = -0.5f * acc[A_CB], dcz = -0.5f * acc[A_CC];
     Ewa e;
@@ -532,7 +565,7 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdArgs a
     dmc[0] += (v[2] - v[3] * mul3) * dd;
     dmc[1] += (v[6] - v[7] * mul3) * dd;
     dmc[2] += (v[10] - v[11] * mul3) * dd;
-    if (a.shs) {
+    if (SH && a.shs) {
       const uint8_t* clamped = shift_bytes(a.clamped, c * cb.geom_stride);
       sh_bwd(a.D, a.M, mean, ld3(cb.campos + 3 * c), a.shs, g, clamped[g], dcol_c, a.dsh, dmc, mk,
              sh_written ? 1 : 0);
@@ -544,6 +577,7 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdArgs a
 #pragma unroll
     for (int i = 0; i < 6; ++i) dcov[i] = any_vis ? dcov[i] + dcv[i] : dcv[i];
     any_vis = true;
+  }
   }
   float dscale[3] = {0.f, 0.f, 0.f}, drot[4] = {0.f, 0.f, 0.f, 0.f};
   if (any_vis && a.scales)
@@ -580,7 +614,10 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdArgs a
 
 void launch_preprocess_bwd(const PreprocessBwdArgs& a, const CamBatch& cb, hipStream_t s) {
   if (a.P <= 0) return;
-  hipLaunchKernelGGL(preprocess_bwd_kernel, dim3((a.P + 255) / 256), dim3(256), 0, s, a, cb);
+  if (a.shs)
+    hipLaunchKernelGGL(preprocess_bwd_kernel<true>, dim3((a.P + 255) / 256), dim3(256), 0, s, a, cb);
+  else
+    hipLaunchKernelGGL(preprocess_bwd_kernel<false>, dim3((a.P + 255) / 256), dim3(256), 0, s, a, cb);
 }
 
 }  // namespace gs
