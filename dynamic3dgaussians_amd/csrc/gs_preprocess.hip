@@ -198,15 +198,10 @@ __global__ __launch_bounds__(256) void preprocess_fwd_kernel(PreprocessArgs a0, 
   a.tiles[g] = 0;
   a.rect[g] = make_uint4(0u, 0u, 0u, 0u);
   const V3 p = ld3(a.means3D + 3 * g);
-  const V3 pv = xf43(a.view, p);
-  if (pv.z <= 0.0f) {  // in_frustum, Q8
-    if (a.prefiltered) atomicOr(a.status, 1);
-    return;
-  }
-  const float4 ph = xf44(a.proj, p);
-  const float pw = 1.0f / (ph.w + 0.0000001f);
-  const float ppx = ph.x * pw, ppy = ph.y * pw;
-
+  // The 3D covariance does not depend on the camera: the batch's camera 0
+  // stores it for every Gaussian (before the frustum test, so a Gaussian
+  // camera 0 does not see still has it) and preprocess_bwd reads it there
+  // once per Gaussian; the other cameras compute it without storing.
   float c3[6];
   if (a.cov3D_precomp) {
 #pragma unroll
@@ -224,9 +219,19 @@ __global__ __launch_bounds__(256) void preprocess_fwd_kernel(PreprocessArgs a0, 
     c3[0] = DOT3(0, 0); c3[1] = DOT3(0, 1); c3[2] = DOT3(0, 2);
     c3[3] = DOT3(1, 1); c3[4] = DOT3(1, 2); c3[5] = DOT3(2, 2);
 #undef DOT3
+    if (blockIdx.y == 0) {
 #pragma unroll
-    for (int i = 0; i < 6; ++i) a.cov3D[6 * g + i] = c3[i];
+      for (int i = 0; i < 6; ++i) a.cov3D[6 * g + i] = c3[i];
+    }
   }
+  const V3 pv = xf43(a.view, p);
+  if (pv.z <= 0.0f) {  // in_frustum, Q8
+    if (a.prefiltered) atomicOr(a.status, 1);
+    return;
+  }
+  const float4 ph = xf44(a.proj, p);
+  const float pw = 1.0f / (ph.w + 0.0000001f);
+  const float ppx = ph.x * pw, ppy = ph.y * pw;
   Ewa e;
   ewa_setup(p, a.view, a.W, a.H, a.c_x, a.c_y, a.focal_x, a.focal_y, a.tan_fovx, a.tan_fovy, e);
   float cov[3];
@@ -432,14 +437,17 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdArgs a
   // requested before the first of them is used, so the group's loads are in
   // flight together instead of one dependent round trip (radius, then the
   // rest) per camera.  The sums still run camera by camera in order.
-  float c3pre[6];
-  if (a.cov3D_precomp) {
+  // the 3D covariance: precomputed, or stored by camera 0's preprocess
+  // (preprocess_fwd_kernel) -- one read per Gaussian for all cameras
+  float c3v[6];
+  {
+    const float* c3 = a.cov3D_precomp ? a.cov3D_precomp + 6 * g : a.cov3D + 6 * g;
 #pragma unroll
-    for (int i = 0; i < 6; ++i) c3pre[i] = a.cov3D_precomp[6 * g + i];
+    for (int i = 0; i < 6; ++i) c3v[i] = c3[i];
   }
   for (int cg = 0; cg < cb.C; cg += PB_GROUP) {
     int radk[PB_GROUP];
-    float acck[PB_GROUP][A_FEAT], c3k[PB_GROUP][6], cck[PB_GROUP];
+    float acck[PB_GROUP][A_FEAT], cck[PB_GROUP];
     float4 conk[PB_GROUP];
 #pragma unroll
     for (int k = 0; k < PB_GROUP; ++k) {
@@ -451,9 +459,6 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdArgs a
       const float* rec = shift_bytes(a.rec, c * cb.geom_stride) + (size_t)REC * g;
       conk[k] = reinterpret_cast<const float4*>(rec)[0];  // x, y, a, b
       cck[k] = rec[R_CC];
-      const float* c3 = a.cov3D_precomp ? c3pre : shift_bytes(a.cov3D, c * cb.geom_stride) + 6 * g;
-#pragma unroll
-      for (int i = 0; i < 6; ++i) c3k[k][i] = c3[i];
     }
 #pragma unroll
   for (int k = 0; k < PB_GROUP; ++k) {
@@ -497,7 +502,6 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdArgs a
     const float c_x = cb.c_x[c], c_y = cb.c_y[c], tan_fovx = cb.tanx[c], tan_fovy = cb.tany[c];
     const float focal_y = (float)a.H / (2.0f * tan_fovy);  // CR/rasterizer_impl.cu:398-399
     const float focal_x = (float)a.W / (2.0f * tan_fovx);
-    const float(&c3v)[6] = c3k[k];
     // dL/dconic = -1/2 sum e (dx^2, dx dy, dy^2) (CR/backward.cu:622-624)
     const float dcx = -0.5f * acc[A_CA], dcy = -0.5f * acc[A_CB], dcz = -0.5f * acc[A_CC];
     Ewa e;
