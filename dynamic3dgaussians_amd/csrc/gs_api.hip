@@ -132,6 +132,7 @@ struct PlanInfo {
   int C = 0;
   int64_t L = -1;        // the batch's total list instances
   int64_t max_len = -1;  // its longest tile
+  SortClasses sort;       // where the sort's length classes sit in the dispatch order
 };
 thread_local PlanInfo g_plan;
 
@@ -284,13 +285,19 @@ static int plan_impl(const gs_gaussians* g, const gs_camera* cams, int C, int pr
   // The one host read of the forward (CR/rasterizer_impl.cu:287), one for
   // the whole batch: the list instance counts size the binning buffer; the
   // reference's counts and the rest of the headers ride along.
-  uint32_t host[GS_MAX_CAMS][4];
+  uint32_t host[GS_MAX_CAMS][M_WORDS];
   hipError_t he = hipMemcpy2DAsync(host, sizeof(host[0]), ta.meta, (size_t)cb.img_stride, sizeof(host[0]), C,
                                    hipMemcpyDeviceToHost, s);
   if (he == hipSuccess) he = hipStreamSynchronize(s);
   if (he != hipSuccess) return fail((int)he, "num_rendered readback: %s", hipGetErrorString(he));
   int64_t max_len = 0, total = 0;
+  SortClasses sc;
+  sc.valid = true;
+  sc.q1 = 0x7FFFFFFF;
   for (int c = 0; c < C; ++c) {
+    sc.p1 = (int)host[c][M_SORT_P1] > sc.p1 ? (int)host[c][M_SORT_P1] : sc.p1;
+    sc.p2 = (int)host[c][M_SORT_P2] > sc.p2 ? (int)host[c][M_SORT_P2] : sc.p2;
+    sc.q1 = (int)host[c][M_SORT_Q1] < sc.q1 ? (int)host[c][M_SORT_Q1] : sc.q1;
     if (prefiltered && (host[c][M_STATUS] & 1u))
       return fail(-2, "Point is filtered although prefiltered is set. This shouldn't happen!");
     if (host[c][M_STATUS] & 2u) return fail(-1, "more than 2^32 tile instances");
@@ -303,6 +310,7 @@ static int plan_impl(const gs_gaussians* g, const gs_camera* cams, int C, int pr
   g_plan.C = C;
   g_plan.L = total;
   g_plan.max_len = max_len;
+  g_plan.sort = C > 0 ? sc : SortClasses{};
   (void)compat;
   return 0;
 }
@@ -338,7 +346,7 @@ static int render_impl(const gs_gaussians* g, const gs_camera* cams, int C, int 
     const bool known = g_plan.image == image && g_plan.C == C && g_plan.L == total;
     {
       StageTimer t(s, GS_STAGE_SORT);
-      launch_tile_sort(ta, cb, known ? g_plan.max_len : -1, total, s);
+      launch_tile_sort(ta, cb, known ? g_plan.max_len : -1, total, known ? g_plan.sort : SortClasses{}, s);
     }
     if (int e = check("tile sort", debug, s)) return e;
   }

@@ -144,7 +144,9 @@ struct SortLayout {
 // header {L, max tile length, -, status}.
 // header: M_L = list instances (after the exact tile test), M_LREF = the
 // reference's num_rendered (bounding-rect instances), longest tile, status
-enum ImgMeta { M_L = 0, M_MAXN = 1, M_LREF = 2, M_STATUS = 3 };
+enum ImgMeta { M_L = 0, M_MAXN = 1, M_LREF = 2, M_STATUS = 3,
+               // tile-order prefixes for the sort launches (tile_offsets_kernel)
+               M_SORT_P1 = 4, M_SORT_Q1 = 5, M_SORT_P2 = 6, M_WORDS = 8 };
 struct ImgLayout {
   size_t ranges, n_contrib, thist, ttotal, bsum, meta, order, smax, total;
   int64_t tiles;
@@ -157,7 +159,7 @@ struct ImgLayout {
     thist = o;     o = align_up(o + sizeof(uint32_t) * TB_BLOCKS * t, 256);
     ttotal = o;    o = align_up(o + sizeof(uint32_t) * t, 256);
     bsum = o;      o = align_up(o + sizeof(uint32_t) * TB_BLOCKS, 256);  // per-block rect instances
-    meta = o;      o = align_up(o + sizeof(uint32_t) * 4, 256);
+    meta = o;      o = align_up(o + sizeof(uint32_t) * M_WORDS, 256);
     // dispatch records {tile, range.x, range.y, 0}, longest list first: one
     // 16-B load gives a blend workgroup its tile and list
     order = o;     o = align_up(o + sizeof(uint32_t) * 4 * t, 256);

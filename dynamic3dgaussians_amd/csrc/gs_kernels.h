@@ -156,7 +156,17 @@ void launch_tile_bucket(const TileArgs& a, const CamBatch& cb, hipStream_t s);
 // dispatch order of the blend / sort kernels (tiles by descending list length)
 void launch_tile_order(const TileArgs& a, const CamBatch& cb, hipStream_t s);
 // max_len: the longest tile over the batch (-1: unknown); L: the batch's total instances
-void launch_tile_sort(const TileArgs& a, const CamBatch& cb, int64_t max_len, int64_t L, hipStream_t s);
+// Dispatch-order extents of the sort's length classes over the batch (plan
+// header M_SORT_*: p1 / p2 = max over cameras of the prefixes holding every
+// tile longer than GS_SORT_SMALL / TS_CAP, q1 = min over cameras of the
+// prefix of tiles known to be longer than GS_SORT_SMALL); valid = false:
+// every class launch covers all tiles.
+struct SortClasses {
+  bool valid = false;
+  int p1 = 0, q1 = 0, p2 = 0;
+};
+void launch_tile_sort(const TileArgs& a, const CamBatch& cb, int64_t max_len, int64_t L, const SortClasses& sc,
+                      hipStream_t s);
 
 // Camera c of a batch: image-buffer, geometry, binning and image pointers of
 // camera 0 -> camera c (point_list = the batch's binning base).

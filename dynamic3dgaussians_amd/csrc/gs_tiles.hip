@@ -32,6 +32,11 @@
 
 namespace gs {
 
+// tile length up to which the tile sort runs in its short (small-LDS) class
+#ifndef GS_SORT_SMALL
+#define GS_SORT_SMALL 1024
+#endif
+
 // Instances of one rect handled by one lane; larger rects are spread over the
 // wave (a full-screen Gaussian must not serialize its wave for 2,500 tiles).
 constexpr int LANE_TILES = 16;
@@ -185,9 +190,9 @@ __global__ __launch_bounds__(OFF_T) void tile_offsets_kernel(const uint32_t* __r
   uint32_t* __restrict__ meta = shift_bytes(meta0, io);
   __shared__ unsigned long long s_sum[OFF_T / 64];
   __shared__ unsigned long long s_lref;
-  __shared__ uint32_t s_max;
+  __shared__ uint32_t s_max, s_cnt[3];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (tid == 0) { s_max = 0; s_lref = 0; }
+  if (tid == 0) { s_max = 0; s_lref = 0; s_cnt[0] = s_cnt[1] = s_cnt[2] = 0; }
   const int per = (T + OFF_T - 1) / OFF_T;
   const int a0 = min(T, tid * per), a1 = min(T, a0 + per);
   unsigned long long sum = 0;
@@ -214,6 +219,7 @@ __global__ __launch_bounds__(OFF_T) void tile_offsets_kernel(const uint32_t* __r
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     if (lane == 0) atomicAdd(&s_lref, v);
   }
+  __syncthreads();  // s_max complete (read by the sort-class counts below)
   unsigned long long woff = 0, total = 0;
 #pragma unroll
   for (int w = 0; w < OFF_T / 64; ++w) {
@@ -228,8 +234,31 @@ __global__ __launch_bounds__(OFF_T) void tile_offsets_kernel(const uint32_t* __r
     ranges[t] = v ? make_uint2((uint32_t)run, (uint32_t)(run + v)) : make_uint2(0u, 0u);
     run += v;
   }
+  // Where the sort's length classes sit in tile_order_kernel's dispatch order
+  // (descending by the bucket v >> sh, the same sh): the tiles longer than
+  // GS_SORT_SMALL all lie in the prefix of the P1 tiles whose bucket reaches
+  // (GS_SORT_SMALL + 1) >> sh, the Q1 tiles whose bucket exceeds
+  // GS_SORT_SMALL >> sh are all long, and the P2 prefix likewise holds every
+  // tile longer than TS_CAP -- so each class launch covers only its part.
+  {
+    const uint32_t mxl = s_max;
+    const int sh = mxl >= OFF_T ? (32 - __builtin_clz(mxl)) - 10 : 0;
+    uint32_t p1 = 0, q1 = 0, p2 = 0;
+    for (int t = a0; t < a1; ++t) {
+      const uint32_t b = ttotal[t] >> sh;
+      p1 += b >= ((uint32_t)(GS_SORT_SMALL + 1) >> sh) ? 1u : 0u;
+      q1 += b > ((uint32_t)GS_SORT_SMALL >> sh) ? 1u : 0u;
+      p2 += b >= ((uint32_t)(TS_CAP + 1) >> sh) ? 1u : 0u;
+    }
+    if (p1) atomicAdd(&s_cnt[0], p1);
+    if (q1) atomicAdd(&s_cnt[1], q1);
+    if (p2) atomicAdd(&s_cnt[2], p2);
+  }
   __syncthreads();
   if (tid == 0) {
+    meta[M_SORT_P1] = s_cnt[0];
+    meta[M_SORT_Q1] = s_cnt[1];
+    meta[M_SORT_P2] = s_cnt[2];
     const unsigned long long lref = s_lref;
     // ranges are 32-bit, as in the reference
     const uint32_t ovf = (total > 0xFFFFFFFFull || lref > 0xFFFFFFFFull) ? 2u : 0u;
@@ -569,14 +598,14 @@ extern "C" int gs_sort_stats_read(unsigned long long* out) {
 // others exit).  Keys sorted in LDS up to `cap` (the launch's dynamic LDS),
 // in global memory beyond.
 template <int NT, int BITS>
-__global__ __launch_bounds__(NT) void tile_sort_kernel(TileArgs a0, CamBatch cb, int cap, int lo, int hi) {
+__global__ __launch_bounds__(NT) void tile_sort_kernel(TileArgs a0, CamBatch cb, int cap, int lo, int hi, int ofs) {
   extern __shared__ uint64_t s_key[];  // 2 x cap keys
   __shared__ RadixSmem<NT, (1 << BITS)> sm;
   const TileArgs ta = cam_tile_args(a0, cb, blockIdx.y);
   uint64_t* __restrict__ keys = ta.keys;
   uint64_t* __restrict__ keys2 = ta.keys2;
   uint32_t* __restrict__ plist = ta.plist;
-  const uint4 o = ta.order[blockIdx.x];  // longest tiles first
+  const uint4 o = ta.order[blockIdx.x + ofs];  // longest tiles first; the launch covers [ofs, ofs + grid)
   const uint2 r = make_uint2(o.y, o.z);
   const int n = (int)(r.y - r.x);
   if (n == 0 || n <= lo || n > hi) return;
@@ -644,12 +673,10 @@ void launch_tile_bucket(const TileArgs& a, const CamBatch& cb, hipStream_t s) {
 // workgroups per CU, the long ones follow with LDS for their length (and
 // global memory beyond TS_CAP_LONG).  Bench batch (27 cameras): sort 0.94 ->
 // 0.80 ms per step with the small class at 1024 keys.
-#ifndef GS_SORT_SMALL
-#define GS_SORT_SMALL 1024
-#endif
 template <int NT>
-static void tile_sort_launches(const TileArgs& a, const CamBatch& cb, int64_t max_len, hipStream_t s) {
-  const dim3 grid(a.num_tiles, cb.C), block(NT);
+static void tile_sort_launches(const TileArgs& a, const CamBatch& cb, int64_t max_len, const SortClasses& sc,
+                               hipStream_t s) {
+  const dim3 block(NT);
   const int big = 0x7FFFFFFF;
   // the short class sorts with BS_BITS bucket bits; the longer classes of the
   // wide (512-thread, long-tile) launches with BS_BITS_LONG.  Measured: 1080p /
@@ -657,32 +684,40 @@ static void tile_sort_launches(const TileArgs& a, const CamBatch& cb, int64_t ma
   // scene's few longer tiles (256-thread launches) are faster at 10 bits
   // (0.54 vs 0.60 ms per step).
   constexpr bool long_bits = NT >= 512 && BS_BITS_LONG != BS_BITS;
-  auto launch = [&](int cap, int lo, int hi) {
+  // a class covers the dispatch-order positions [ofs, ofs + n) (SortClasses)
+  auto launch = [&](int cap, int lo, int hi, int ofs, int n) {
+    if (n <= 0) return;
+    const dim3 grid(n, cb.C);
     if (lo == 0 || !long_bits)
       hipLaunchKernelGGL((tile_sort_kernel<NT, BS_BITS>), grid, block, 2 * sizeof(uint64_t) * (cap > 0 ? cap : 1), s,
-                         a, cb, cap > 0 ? cap : 1, lo, hi);
+                         a, cb, cap > 0 ? cap : 1, lo, hi, ofs);
     else
       hipLaunchKernelGGL((tile_sort_kernel<NT, BS_BITS_LONG>), grid, block,
-                         2 * sizeof(uint64_t) * (cap > 0 ? cap : 1), s, a, cb, cap > 0 ? cap : 1, lo, hi);
+                         2 * sizeof(uint64_t) * (cap > 0 ? cap : 1), s, a, cb, cap > 0 ? cap : 1, lo, hi, ofs);
   };
+  const int T = a.num_tiles;
   if (max_len < 0) {  // unknown lengths: the LDS classes and the global-memory class
-    launch(TS_CAP, 0, TS_CAP);
-    launch(TS_CAP_LONG, TS_CAP, big);
+    launch(TS_CAP, 0, TS_CAP, 0, T);
+    launch(TS_CAP_LONG, TS_CAP, big, 0, T);
     return;
   }
   const int64_t small = GS_SORT_SMALL;
-  launch((int)(max_len < small ? max_len : small), 0, (int)small);
-  if (max_len > small) launch((int)(max_len < TS_CAP ? max_len : TS_CAP), (int)small, TS_CAP);
-  if (max_len > TS_CAP) launch((int)(max_len < TS_CAP_LONG ? max_len : TS_CAP_LONG), TS_CAP, big);
+  const bool known = sc.valid;
+  const int q1 = known ? sc.q1 : 0;
+  launch((int)(max_len < small ? max_len : small), 0, (int)small, q1, T - q1);
+  if (max_len > small) launch((int)(max_len < TS_CAP ? max_len : TS_CAP), (int)small, TS_CAP, 0, known ? sc.p1 : T);
+  if (max_len > TS_CAP)
+    launch((int)(max_len < TS_CAP_LONG ? max_len : TS_CAP_LONG), TS_CAP, big, 0, known ? sc.p2 : T);
 }
 
-void launch_tile_sort(const TileArgs& a, const CamBatch& cb, int64_t max_len, int64_t L, hipStream_t s) {
+void launch_tile_sort(const TileArgs& a, const CamBatch& cb, int64_t max_len, int64_t L, const SortClasses& sc,
+                      hipStream_t s) {
   // workgroup size by the mean tile length: 256 threads keep short tiles'
   // per-pass overhead low (bench camera: ~660 keys per tile), 512 split long
   // tiles' passes over twice the waves (1080p / 1M Gaussians: ~1800)
   const int64_t mean = a.num_tiles > 0 ? L / ((int64_t)a.num_tiles * cb.C) : 0;
-  if (L >= 0 && mean >= TS_WIDE_MEAN) tile_sort_launches<512>(a, cb, max_len, s);
-  else tile_sort_launches<256>(a, cb, max_len, s);
+  if (L >= 0 && mean >= TS_WIDE_MEAN) tile_sort_launches<512>(a, cb, max_len, sc, s);
+  else tile_sort_launches<256>(a, cb, max_len, sc, s);
 }
 
 }  // namespace gs
