@@ -52,19 +52,24 @@ __global__ __launch_bounds__(TB_THREADS) void tile_hist_kernel(TileArgs a0, CamB
   extern __shared__ uint32_t s_bin[];  // nt counters (hist) or cursors (bucket)
   __shared__ uint32_t s_rect[TB_THREADS / 64];
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+  const int per = (a.P + TB_BLOCKS - 1) / TB_BLOCKS;
+  const int g0 = b * per, g1 = min(a.P, g0 + per);
+  // the first slice's rects are requested before the cursor set-up, so their
+  // latency overlaps it (the set-up ends in a barrier the compiler does not
+  // hoist loads across)
+  uint4 rnext = g0 + tid < g1 ? a.rect[g0 + tid] : make_uint4(0u, 0u, 0u, 0u);
   for (int i = tid; i < nt; i += TB_THREADS)
     s_bin[i] = WRITE ? a.ranges[t0 + i].x + a.thist[(size_t)b * a.num_tiles + t0 + i] : 0u;
   __syncthreads();
-  const int per = (a.P + TB_BLOCKS - 1) / TB_BLOCKS;
-  const int g0 = b * per, g1 = min(a.P, g0 + per);
   const int gx = a.grid_x;
   uint32_t rect_n = 0;
   for (int base = g0; base < g1; base += TB_THREADS) {
     const int g = base + tid;
     int x0 = 0, y0 = 0, w = 0, n = 0;
     uint64_t key = 0;
+    const uint4 r = rnext;  // {x0 | y0 << 16, x1 | y1 << 16, depth bits, tiles_touched}
+    if (base + TB_THREADS < g1 && g + TB_THREADS < g1) rnext = a.rect[g + TB_THREADS];
     if (g < g1) {
-      const uint4 r = a.rect[g];  // {x0 | y0 << 16, x1 | y1 << 16, depth bits, tiles_touched}
       x0 = (int)(r.x & 0xFFFFu);
       y0 = (int)(r.x >> 16);
       w = (int)(r.y & 0xFFFFu) - x0;
