@@ -693,6 +693,15 @@ static void tile_sort_launches(const TileArgs& a, const CamBatch& cb, int64_t ma
   auto launch = [&](int cap, int lo, int hi, int ofs, int n) {
     if (n <= 0) return;
     const dim3 grid(n, cb.C);
+#ifdef GS_SORT_MID512
+    // the tiles past the short class sorted by 512-thread workgroups at the
+    // short class's bucket bits
+    if (NT == 256 && lo > 0) {
+      hipLaunchKernelGGL((tile_sort_kernel<512, BS_BITS>), grid, dim3(512), 2 * sizeof(uint64_t) * (cap > 0 ? cap : 1),
+                         s, a, cb, cap > 0 ? cap : 1, lo, hi, ofs);
+      return;
+    }
+#endif
     if (lo == 0 || !long_bits)
       hipLaunchKernelGGL((tile_sort_kernel<NT, BS_BITS>), grid, block, 2 * sizeof(uint64_t) * (cap > 0 ? cap : 1), s,
                          a, cb, cap > 0 ? cap : 1, lo, hi, ofs);
