@@ -146,8 +146,15 @@ __global__ __launch_bounds__(TB_THREADS) void tile_hist_kernel(TileArgs a0, CamB
 // 16 bg .. 16 bg + 15 of tile tt (16 tiles x 4 B = one 64-B piece per block
 // row and load), the RS_BG block-group partial sums are scanned through LDS.
 static_assert(TB_BLOCKS % 64 == 0 && TB_BLOCKS <= 256, "tile_rowscan_kernel: 4 to 16 block groups of 16 blocks");
-constexpr int RS_BG = TB_BLOCKS / 16, RS_T = 256 / RS_BG;
-__global__ __launch_bounds__(256) void tile_rowscan_kernel(uint32_t* __restrict__ thist0,
+#ifndef GS_RS_THREADS
+#define GS_RS_THREADS 1024
+#endif
+// RS_THREADS threads: RS_T = RS_THREADS / RS_BG tiles per workgroup, so each
+// load instruction of a wave reads 64 consecutive tiles of one block row
+// (256 contiguous bytes at 1024 threads; 4 x 64 B pieces at 256)
+constexpr int RS_THREADS = GS_RS_THREADS;
+constexpr int RS_BG = TB_BLOCKS / 16, RS_T = RS_THREADS / RS_BG;
+__global__ __launch_bounds__(RS_THREADS) void tile_rowscan_kernel(uint32_t* __restrict__ thist0,
                                                            uint32_t* __restrict__ ttotal0, int T, CamBatch cb) {
   uint32_t* __restrict__ thist = shift_bytes(thist0, blockIdx.y * cb.img_stride);
   uint32_t* __restrict__ ttotal = shift_bytes(ttotal0, blockIdx.y * cb.img_stride);
@@ -652,7 +659,7 @@ void launch_tile_plan(const TileArgs& a, const CamBatch& cb, int prefiltered, hi
     hipLaunchKernelGGL(tile_hist_kernel<false>, dim3(TB_BLOCKS, cb.C), dim3(TB_THREADS), sizeof(uint32_t) * nt, s,
                        a, cb, t0, nt);
   }
-  hipLaunchKernelGGL(tile_rowscan_kernel, dim3((T + RS_T - 1) / RS_T, cb.C), dim3(256), 0, s, a.thist, a.ttotal, T,
+  hipLaunchKernelGGL(tile_rowscan_kernel, dim3((T + RS_T - 1) / RS_T, cb.C), dim3(RS_THREADS), 0, s, a.thist, a.ttotal, T,
                      cb);
   hipLaunchKernelGGL(tile_offsets_kernel, dim3(cb.C), dim3(OFF_T), 0, s, a.ttotal, T, a.bsum, a.ranges, a.meta,
                      prefiltered, cb);
