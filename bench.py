@@ -19,8 +19,15 @@ right after it on the same scene and reported as `other_mode`):
           call pattern) over 4 HIP streams, gradients summed by a
           GradientSink.
 
-Scaling is weak: every rank renders its own 27 cameras of a 27*N camera rig
-with the full Gaussian set replicated; value = all ranks' pixels / step time.
+Scaling (headline: weak): every rank renders its own 27 cameras of a 27*N
+camera rig with the full Gaussian set replicated; value = all ranks' pixels /
+step time.  `--cams-total T` makes the headline the north star's step split
+across the ranks instead (BASELINE.json configs[3], strong scaling): ONE rig
+of T cameras, camera c on rank c mod N (distributed.shard_cameras), each rank
+renders its share as one batch, then the gradient all-reduce and Adam;
+value = T cameras' pixels / step time.  At N > 1 the weak headline is
+followed by the same measurement of the 27-camera split step, reported as
+`split_step` (so one driver run gives both curves).
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
@@ -28,8 +35,11 @@ with the full Gaussian set replicated; value = all ranks' pixels / step time.
 
 Prints ONE JSON line (rank 0).  Besides the contract fields it carries
 `roofline` (dominant kernel, live HIP-event timing over the timed region),
-`cpu_baseline` (the CPU oracle on a bounded sample, rank 0 at N=1 only) and
-`psnr_vs_oracle_db` (the rendered image of camera 0 vs the oracle's).
+`cpu_baseline` (north star's naive pure-PyTorch fp32 CPU splat, fwd + autograd
+bwd, on a bounded tile sample of camera 0, on the host's cores; the
+single-thread C oracle beside it as `cpu_baseline.c_oracle`; rank 0 at N=1
+only) and `psnr_vs_oracle_db` (the rendered image of camera 0 vs the
+oracle's).
 """
 from __future__ import annotations
 
@@ -48,7 +58,7 @@ sys.path.insert(0, REPO)
 
 from dynamic3dgaussians_amd import _lib  # noqa: E402
 from dynamic3dgaussians_amd.camera import camera_rig  # noqa: E402
-from dynamic3dgaussians_amd.distributed import GradBucket  # noqa: E402
+from dynamic3dgaussians_amd.distributed import GradBucket, shard_cameras  # noqa: E402
 from dynamic3dgaussians_amd.optim import FusedAdam  # noqa: E402
 from dynamic3dgaussians_amd.rasterizer import (GaussianRasterizationSettings,  # noqa: E402
                                                GaussianRasterizer, GaussianRasterizerBatch, GradientSink)
@@ -64,7 +74,11 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--gaussians", type=int, default=300_000)
-    ap.add_argument("--cams", type=int, default=27, help="cameras per rank per step")
+    ap.add_argument("--cams", type=int, default=27, help="cameras per rank per step (weak scaling)")
+    ap.add_argument("--cams-total", type=int, default=0,
+                    help="strong scaling: one rig of this many cameras split over the ranks (c mod N)")
+    ap.add_argument("--cpu-tiles", type=int, default=10,
+                    help="CPU baseline sample: a TxT block of 16x16 tiles at the centre of camera 0")
     ap.add_argument("--width", type=int, default=800)
     ap.add_argument("--height", type=int, default=800)
     ap.add_argument("--features", type=int, default=32)
@@ -238,12 +252,72 @@ def calc_psnr(img1, img2):
         return float(np.mean(20 * np.log10(1.0 / np.sqrt(mse))))
 
 
+def host_cores():
+    """The host cores this process may use: the scheduler's affinity set,
+    capped by OMP_NUM_THREADS when set (the GPU box exports its CPU share
+    there; os.cpu_count() shows the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
+def torch_cpu_splat(args, params0, cam, img_hip, up):
+    """North star's CPU baseline: a naive pure-PyTorch splat (oracle/torch_splat.py,
+    fp32 dense per-tile algebra, projection as utils/graphics_utils.py:51-74
+    sets it up) of the same scene and camera, forward + autograd backward
+    through the same activations as the step (sigmoid / exp / normalize), on
+    the host's cores, over a bounded sample: the --cpu-tiles^2 tiles at the
+    image centre (every Gaussian is projected; only the sampled tiles blend)."""
+    from oracle import torch_splat as TS
+    cores = host_cores()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(cores)
+    try:
+        gx, gy = (cam.W + 15) // 16, (cam.H + 15) // 16
+        n = max(1, min(args.cpu_tiles, gx, gy))
+        tx0, ty0 = (gx - n) // 2, (gy - n) // 2
+        tiles = [(tx0 + i, ty0 + j) for j in range(n) for i in range(n)]
+        leaf = {k: v.detach().float().cpu().clone().requires_grad_(True) for k, v in params0.items()}
+        view = torch.from_numpy(cam.viewmatrix.copy()).float()
+        proj = torch.from_numpy(cam.projmatrix.copy()).float()
+        t0 = time.perf_counter()
+        color, depth, feat, _ = TS.render(
+            leaf["means3D"], leaf["rgb_colors"], torch.sigmoid(leaf["logit_opacities"]),
+            torch.exp(leaf["log_scales"]), torch.nn.functional.normalize(leaf["unnorm_rotations"]), view, proj,
+            cam.tanfovx, cam.tanfovy, cam.c_x, cam.c_y, cam.W, cam.H, torch.zeros(3),
+            features=leaf.get("semantic_feature"), tiles=tiles)
+        t1 = time.perf_counter()
+        uc, ud, uf = up
+        loss = (color * uc).sum() + (depth * ud).sum()
+        if feat is not None:
+            loss = loss + (feat * uf).sum()
+        loss.backward()
+        t2 = time.perf_counter()
+    finally:
+        torch.set_num_threads(prev)
+    ys = slice(ty0 * 16, min((ty0 + n) * 16, cam.H))
+    xs = slice(tx0 * 16, min((tx0 + n) * 16, cam.W))
+    a = color.detach().numpy()[:, ys, xs].astype(np.float64)
+    b = img_hip[:, ys, xs].astype(np.float64)
+    mse = float(np.mean((a - b) ** 2))
+    npix = (ys.stop - ys.start) * (xs.stop - xs.start)
+    return {"value": round(npix / 1e6 / (t2 - t0), 5), "unit": "Mpix/s", "cores": cores, "kind": "port",
+            "sample": f"camera 0, the {n}x{n} tiles ({npix} px) at the image centre of {cam.W}x{cam.H}; "
+                      f"{args.gaussians} Gaussians projected, F={args.features}; fwd {t1 - t0:.2f}s + "
+                      f"autograd bwd {t2 - t1:.2f}s; oracle/torch_splat.py fp32 on {cores} threads",
+            "psnr_vs_hip_db": round(10 * np.log10(1.0 / mse), 2) if mse > 0 else "inf"}
+
+
 def cpu_baseline(args, params, label, cam, settings, dev):
-    """The CPU oracle (plain C restatement, 1 thread) on one camera of the same
-    scene: forward + backward.  Also returns the PSNR of the HIP render of the
-    same camera against the oracle's, and both renders' PSNR against a
-    ground-truth image (the oracle's render of the scene with its means
-    jittered by N(0, 0.002), seeded: a stand-in for a training target)."""
+    """The CPU baselines on camera 0 of the same scene: north star's naive
+    PyTorch splat (torch_cpu_splat, the reported `cpu_baseline`) and the C
+    oracle (plain C restatement, 1 thread, the whole camera, forward +
+    backward: `cpu_baseline.c_oracle`).  Also returns the PSNR of the HIP
+    render of the same camera against the oracle's, and both renders' PSNR
+    against a ground-truth image (the oracle's render of the scene with its
+    means jittered by N(0, 0.002), seeded: a stand-in for a training target)."""
     from oracle import oracle as O
     with torch.no_grad():
         rv = params2rendervar(params, label)
@@ -288,10 +362,13 @@ def cpu_baseline(args, params, label, cam, settings, dev):
                "gt": "oracle render of the scene with means jittered by N(0, 0.002)",
                "formula": "external.py:84-86 calc_psnr, channel mean"}
     mpix = cam.W * cam.H / 1e6
-    return {"value": round(mpix / (t2 - t0), 4), "unit": "Mpix/s", "cores": 1, "kind": "port",
-            "sample": f"1 of {args.cams} cameras ({cam.W}x{cam.H}, {args.gaussians} Gaussians, "
-                      f"F={args.features}), fwd {t1 - t0:.2f}s + bwd {t2 - t1:.2f}s, "
-                      "oracle/gs_oracle.c single thread"}, psnr, psnr_gt
+    c_oracle = {"value": round(mpix / (t2 - t0), 4), "unit": "Mpix/s", "cores": 1, "kind": "port",
+                "sample": f"the whole camera 0 ({cam.W}x{cam.H}, {args.gaussians} Gaussians, F={args.features}), "
+                          f"fwd {t1 - t0:.2f}s + bwd {t2 - t1:.2f}s, oracle/gs_oracle.c single thread"}
+    up = (torch.from_numpy(dc), torch.from_numpy(dd), torch.from_numpy(df) if args.features else None)
+    cb = torch_cpu_splat(args, params, cam, img, up)
+    cb["c_oracle"] = c_oracle
+    return cb, psnr, psnr_gt
 
 
 def main():
@@ -300,8 +377,16 @@ def main():
     _lib.load()
     torch.manual_seed(args.seed)
 
-    rig = camera_rig(args.cams * world, args.width, args.height, seed=args.seed)
-    my_cams = rig[rank * args.cams:(rank + 1) * args.cams]
+    strong = args.cams_total > 0
+    if strong:
+        # the north star's step: one rig, camera c on rank c mod N
+        if args.cams_total < world:
+            raise SystemExit(f"--cams-total {args.cams_total} < {world} ranks")
+        rig = camera_rig(args.cams_total, args.width, args.height, seed=args.seed)
+        my_cams = [rig[c] for c in shard_cameras(args.cams_total, rank, world)]
+    else:
+        rig = camera_rig(args.cams * world, args.width, args.height, seed=args.seed)
+        my_cams = rig[rank * args.cams:(rank + 1) * args.cams]
     # The per-camera gradients of a step are summed inside the backward
     # kernels (GradientSink: GS_FLAG_ACCUMULATE into per-stream buffers)
     # instead of autograd adding 7 gradient tensors per camera into the
@@ -329,7 +414,10 @@ def main():
         opt = FusedAdam(groups, lr=0.0, eps=1e-15)
     else:
         opt = torch.optim.Adam(groups, lr=0.0, eps=1e-15, fused=optim_kind == "torch_fused")
-    bucket = GradBucket(list(params.values()))
+    # Every parameter's .grad is a view into the all-reduce bucket: the
+    # backward accumulates straight into it (no pack/unpack copies at N > 1);
+    # gradients are cleared by one fill of the bucket.
+    bucket = GradBucket(params, bind_grads=True)
     g = torch.Generator(device=dev).manual_seed(1 + rank)
     H_, W_ = args.height, args.width
     up_color = torch.randn(3, H_, W_, device=dev, generator=g)
@@ -361,30 +449,31 @@ def main():
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(device=dev) for _ in range(n_streams - 1)]
     # one upstream gradient per camera, materialized once (the batch's
     # backward reads [C, ...] images like C per-camera backwards do)
-    C_ = len(settings)
-    up_color_b = up_color.expand(C_, -1, -1, -1).contiguous()
-    up_depth_b = up_depth.expand(C_, -1, -1, -1).contiguous()
-    up_feat_b = up_feat.expand(C_, -1, -1, -1).contiguous() if up_feat is not None else None
-    batch_ras = GaussianRasterizerBatch(settings)
+    def batch_inputs(setts):
+        C_ = len(setts)
+        ups = (up_color.expand(C_, -1, -1, -1).contiguous(), up_depth.expand(C_, -1, -1, -1).contiguous(),
+               up_feat.expand(C_, -1, -1, -1).contiguous() if up_feat is not None else None)
+        return GaussianRasterizerBatch(setts), ups
 
-    def step_batch():
-        opt.zero_grad(set_to_none=True)
+    batch_ras, ups_b = batch_inputs(settings)
+
+    def step_batch(ras=batch_ras, ups=ups_b):
+        bucket.zero_grad()
         rv = params2rendervar(params, label)
-        if up_feat_b is not None:  # G3 call (label + semantic_feature)
-            im, radius, feat, depth, _ = batch_ras(**rv)
-            torch.autograd.backward([im, depth, feat], [up_color_b, up_depth_b, up_feat_b])
-        else:                      # G2 call (label only)
-            im, radius, depth, _ = batch_ras(**rv)
-            torch.autograd.backward([im, depth], [up_color_b, up_depth_b])
+        up_c, up_d, up_f = ups
+        if up_f is not None:  # G3 call (label + semantic_feature)
+            im, radius, feat, depth, _ = ras(**rv)
+            torch.autograd.backward([im, depth, feat], [up_c, up_d, up_f])
+        else:                 # G2 call (label only)
+            im, radius, depth, _ = ras(**rv)
+            torch.autograd.backward([im, depth], [up_c, up_d])
         bucket.all_reduce()
         opt.step()
 
     def step(mode=args.mode):
         if mode == "batch":
             return step_batch()
-        # grads set to None: the activation backward hands every parameter a
-        # fresh gradient (no zero fills, no in-place accumulation launches)
-        opt.zero_grad(set_to_none=os.environ.get("GS_BENCH_GRAD_NONE", "1") != "0")
+        bucket.zero_grad()
         if sink is not None:
             sink.reset()
         rv = params2rendervar(params, label)
@@ -478,8 +567,50 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         other_elapsed = float(t.item())
 
+    def timed(fn):
+        for _ in range(args.warmup):
+            fn()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        ta = time.perf_counter()
+        for _ in range(args.steps):
+            fn()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - ta
+        if world > 1:
+            t = torch.tensor([el], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el
+
+    # The north star's 27-camera step split over the ranks (configs[3], strong
+    # scaling), measured after a weak-scaling headline at N > 1; at N = 1 it
+    # is the headline's own step (27 cameras on one rank).
+    split = None
+    if not strong and args.mode == "batch":
+        n_split = args.cams
+        if world > 1 and n_split >= world:
+            rig_s = camera_rig(n_split, args.width, args.height, seed=args.seed)
+            mine = shard_cameras(n_split, rank, world)
+            ras_s, ups_s = batch_inputs(make_settings([rig_s[c] for c in mine], dev, args.compat))
+            el_s = timed(lambda: step_batch(ras_s, ups_s))
+            cams_rank = [len(shard_cameras(n_split, r, world)) for r in range(world)]
+            del ras_s, ups_s
+        else:
+            el_s, cams_rank = elapsed, [args.cams]
+        ms_s = el_s / args.steps * 1e3
+        split = {"cams_total": n_split, "cams_per_rank": cams_rank, "ms_per_step": round(ms_s, 3),
+                 "value": round(n_split * W_ * H_ / 1e6 / (ms_s / 1e3), 3), "unit": "Mpix/s",
+                 "scaling": "strong", "sharding": "camera c on rank c mod N (distributed.shard_cameras)"}
+
     ms_per_step = elapsed / args.steps * 1e3
-    mpix_total = world * args.cams * W_ * H_ / 1e6
+    n_cams_total = args.cams_total if strong else world * args.cams
+    mpix_total = n_cams_total * W_ * H_ / 1e6
     value = mpix_total / (ms_per_step / 1e3)
 
     # roofline of the dominant stage (live HIP-event durations over the timed region)
@@ -489,7 +620,7 @@ def main():
     avg_ms = stages[dom][0] / max(launches, 1)
     alg_per_launch = alg_bytes_total / max(launches, 1)
     achieved = alg_per_launch / (avg_ms / 1e3) / 1e9 if avg_ms > 0 else 0.0
-    cams_per_launch = args.cams if args.mode == "batch" else 1
+    cams_per_launch = len(my_cams) if args.mode == "batch" else 1
     traffic = load_pmc_traffic(dom, cams_per_launch)
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -501,23 +632,30 @@ def main():
     result = {
         "metric": METRIC, "value": round(value, 3), "unit": "Mpix/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "higher_is_better": True, "scaling": "strong" if strong else "weak", "vs_baseline": None,
+        "dtype": "f32",
+        "dtype_note": ("fp32 blend on the vector ALUs; the feature blend and the backward's per-Gaussian "
+                       "sums as MFMA contractions of 3-piece bf16 splits (products to 2^-26 relative, "
+                       "fp32 accumulation): tests/test_gpu_parity.py holds them to the oracle at 1e-5 / 1e-4"),
         "data": "synthetic",
-        "config": {"workload": f"{args.gaussians // 1000}k Gaussians x {args.cams} cams/rank x "
-                               f"{W_}x{H_}, F={args.features} semantic channels, colors_precomp; "
+        "config": {"workload": (f"{args.gaussians // 1000}k Gaussians x {args.cams_total} cams split over "
+                                f"{world} rank(s)" if strong else
+                                f"{args.gaussians // 1000}k Gaussians x {args.cams} cams/rank") +
+                               f" x {W_}x{H_}, F={args.features} semantic channels, colors_precomp; "
                                "fwd+bwd of every camera + grad all-reduce + Adam",
                    "mode": ("camera batch (GaussianRasterizerBatch: one launch per stage for the rank's "
                             "cameras)" if args.mode == "batch" else "per camera (GaussianRasterizer drop-in)"),
                    "optimizer": optim_kind, "streams": n_streams if args.mode == "percam" else 1,
                    "grad_sum": ("in-kernel (camera sum in preprocess_bwd)" if args.mode == "batch" else
                                 "in-kernel (GradientSink)" if use_sink else "autograd"),
-                   "gaussians": args.gaussians, "cams_per_rank": args.cams, "width": W_,
+                   "gaussians": args.gaussians, "cams_per_rank": len(my_cams), "width": W_,
                    "height": H_, "feature_channels": args.features, "compat": args.compat,
                    "parallelism": f"camera-sharded dp{world}"},
         "roofline": roofline,
         "stages_ms_per_step": {k: round(v, 4) for k, v in stage_ms.items()},
+        "split_step": split,
         "other_mode": {"mode": other, "ms_per_step": round(other_elapsed / args.steps * 1e3, 3),
-                       "value": round(world * args.cams * W_ * H_ / 1e6 / (other_elapsed / args.steps), 3),
+                       "value": round(mpix_total / (other_elapsed / args.steps), 3),
                        "streams": n_streams if other == "percam" else 1},
         "instances_per_cam": int(np.mean([L for L, _, _ in inst])),
         "num_rendered_per_cam": int(np.mean([R for _, _, R in inst])),

@@ -108,6 +108,9 @@ PROTOTYPES = {
                                        c_void_p, c_void_p, c_void_p, c_void_p]),
     "gs_sort_scratch_bytes": (c_size_t, [c_int64]),
     "gs_sort_pairs": (ctypes.c_int, [c_int64, c_void_p, c_void_p, ctypes.c_int, c_void_p, c_void_p]),
+    "gs_check_plan_header": (ctypes.c_int, [c_void_p, c_int64]),
+    "gs_check_ranges": (ctypes.c_int, [c_void_p, c_int64, c_int64, c_int64]),
+    "gs_check_point_list": (ctypes.c_int, [c_void_p, c_int64, c_int64]),
     "gs_test_wave_reduce": (ctypes.c_int, [ctypes.c_int, c_void_p, c_void_p, c_void_p]),
     "gs_timing_enable": (ctypes.c_int, [ctypes.c_int]),
     # include/gs_knn.h

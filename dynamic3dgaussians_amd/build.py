@@ -46,7 +46,8 @@ VARIANT_FLAGS = {"": [], "stats": ["-DGS_STATS"], "stamps": ["-DGS_STAMPS"], "st
                  "exp_bkt_batch": ["-DGS_BUCKET_BATCH"],
                  "exp_fdummy": ["-DGS_FWD_DUMMY"], "exp_fdummy_ulw": ["-DGS_FWD_DUMMY", "-DGS_FWD_ULW", "-DGS_FWD_SLAST"],
                  "exp_pb1": ["-DGS_PBWD_GROUP=1"], "exp_pb3": ["-DGS_PBWD_GROUP=3"],
-                 "exp_mid512": ["-DGS_SORT_MID512"], "exp_rs256": ["-DGS_RS_THREADS=256"]}
+                 "exp_mid512": ["-DGS_SORT_MID512"], "exp_rs256": ["-DGS_RS_THREADS=256"],
+                 "exp_split2": ["-DGS_SPLIT_PIECES=2"], "exp_bwd_wpe2": ["-DGS_BWD_WPE=2"], "exp_fwd_wpe3": ["-DGS_FWD_WPE=3"]}
 ARCH = os.environ.get("GSPLAT_OFFLOAD_ARCH", "gfx950")
 
 # Per-file flags.  The preprocess kernels are compiled without FMA

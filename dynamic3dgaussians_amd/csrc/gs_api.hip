@@ -238,6 +238,76 @@ static int64_t batch_bin_offsets(int C, const int64_t* L, CamBatch* cb) {
   return o;
 }
 
+// ---------------------------------------------------------------- debug checks
+// Host-side validation of the forward's state under `debug` (gsplat_hip.h).
+
+extern "C" int gs_check_plan_header(const uint32_t* hdr, int64_t tiles) {
+  if (!hdr) return fail(-1, "plan header: null");
+  const uint64_t L = hdr[M_L], maxn = hdr[M_MAXN], lref = hdr[M_LREF], st = hdr[M_STATUS];
+  const uint64_t p1 = hdr[M_SORT_P1], q1 = hdr[M_SORT_Q1], p2 = hdr[M_SORT_P2];
+  if (st > 3u) return fail(-3, "plan header: status word %llu has unknown bits", (unsigned long long)st);
+  if (L > lref)
+    return fail(-3, "plan header: %llu list instances exceed the %llu bounding-rect instances",
+                (unsigned long long)L, (unsigned long long)lref);
+  if (maxn > L)
+    return fail(-3, "plan header: longest tile %llu > %llu instances", (unsigned long long)maxn,
+                (unsigned long long)L);
+  if (p1 > (uint64_t)tiles || p2 > p1 || q1 > p1)
+    return fail(-3, "plan header: sort-class prefixes p1=%llu q1=%llu p2=%llu inconsistent with %lld tiles",
+                (unsigned long long)p1, (unsigned long long)q1, (unsigned long long)p2, (long long)tiles);
+  return 0;
+}
+
+extern "C" int gs_check_ranges(const uint32_t* ranges, int64_t tiles, int64_t L, int64_t max_len) {
+  if (!ranges && tiles > 0) return fail(-1, "ranges: null");
+  int64_t next = 0;
+  for (int64_t t = 0; t < tiles; ++t) {
+    const int64_t a = ranges[2 * t], b = ranges[2 * t + 1];
+    if (b < a || b > L)
+      return fail(-3, "ranges: tile %lld has [%lld, %lld) outside [0, %lld]", (long long)t, (long long)a,
+                  (long long)b, (long long)L);
+    if (b > a) {
+      if (a != next)
+        return fail(-3, "ranges: tile %lld starts at %lld, expected %lld (lists not contiguous)", (long long)t,
+                    (long long)a, (long long)next);
+      if (max_len >= 0 && b - a > max_len)
+        return fail(-3, "ranges: tile %lld holds %lld instances > the planned longest %lld", (long long)t,
+                    (long long)(b - a), (long long)max_len);
+      next = b;
+    }
+  }
+  if (next != L) return fail(-3, "ranges: lists cover %lld of %lld instances", (long long)next, (long long)L);
+  return 0;
+}
+
+extern "C" int gs_check_point_list(const uint32_t* ids, int64_t L, int64_t P) {
+  if (!ids && L > 0) return fail(-1, "point list: null");
+  for (int64_t i = 0; i < L; ++i)
+    if ((int64_t)ids[i] >= P)
+      return fail(-3, "point list: entry %lld holds Gaussian id %u >= P = %lld", (long long)i, ids[i], (long long)P);
+  return 0;
+}
+
+// debug mode, after the sort: every camera's ranges and list ids, read back
+static int debug_check_lists(const TileArgs& ta, const CamBatch& cb, const void* binning, const int64_t* L,
+                             int64_t P, int64_t tiles, int64_t max_len, hipStream_t s) {
+  std::vector<uint32_t> rg((size_t)2 * (tiles > 0 ? tiles : 1)), ids;
+  for (int c = 0; c < cb.C; ++c) {
+    hipError_t e = hipMemcpyAsync(rg.data(), shift_bytes(ta.ranges, c * cb.img_stride), 8 * (size_t)tiles,
+                                  hipMemcpyDeviceToHost, s);
+    const int64_t l = L[c] > 0 ? L[c] : 0;
+    ids.resize((size_t)(l > 0 ? l : 1));
+    if (e == hipSuccess && l > 0)
+      e = hipMemcpyAsync(ids.data(), static_cast<const char*>(binning) + cb.bin_off[c], 4 * (size_t)l,
+                         hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return fail((int)e, "debug readback: %s", hipGetErrorString(e));
+    if (int r = gs_check_ranges(rg.data(), tiles, l, max_len)) return r;
+    if (int r = gs_check_point_list(ids.data(), l, P)) return r;
+  }
+  return 0;
+}
+
 static int plan_impl(const gs_gaussians* g, const gs_camera* cams, int C, int prefiltered, int debug, int compat,
                      void* geom, void* image, int32_t* radii, int64_t* num_rendered, int64_t* num_instances,
                      hipStream_t s) {
@@ -295,6 +365,8 @@ static int plan_impl(const gs_gaussians* g, const gs_camera* cams, int C, int pr
   sc.valid = true;
   sc.q1 = 0x7FFFFFFF;
   for (int c = 0; c < C; ++c) {
+    if (debug)
+      if (int e = gs_check_plan_header(host[c], (int64_t)ta.grid_x * ta.grid_y)) return e;
     sc.p1 = (int)host[c][M_SORT_P1] > sc.p1 ? (int)host[c][M_SORT_P1] : sc.p1;
     sc.p2 = (int)host[c][M_SORT_P2] > sc.p2 ? (int)host[c][M_SORT_P2] : sc.p2;
     sc.q1 = (int)host[c][M_SORT_Q1] < sc.q1 ? (int)host[c][M_SORT_Q1] : sc.q1;
@@ -349,6 +421,9 @@ static int render_impl(const gs_gaussians* g, const gs_camera* cams, int C, int 
       launch_tile_sort(ta, cb, known ? g_plan.max_len : -1, total, known ? g_plan.sort : SortClasses{}, s);
     }
     if (int e = check("tile sort", debug, s)) return e;
+    if (debug)
+      if (int e = debug_check_lists(ta, cb, binning, L, P, (int64_t)gx * gy, known ? g_plan.max_len : -1, s))
+        return e;
   }
   RenderArgs ra{};
   ra.W = W; ra.H = H; ra.grid_x = gx; ra.num_tiles = gx * gy; ra.F = g->F; ra.compat = compat;

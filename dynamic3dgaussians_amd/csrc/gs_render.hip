@@ -222,32 +222,78 @@ __device__ inline bool strip_culled(const RecRegs& q, float sx0, float sx1, floa
 }
 
 // ------------------------------------------------------------------ bf16 split products
-// fp32 contractions on the bf16 matrix cores (16x the fp32 MFMA rate): every
-// operand is split x = hi + lo into two bf16 (x - hi is exact in fp32) and
-// a*b is summed as hi*hi + hi*lo + lo*hi with fp32 accumulation, ~2^-17
-// relative per product (the dropped lo*lo and the split residues).
+// fp32 contractions on the bf16 matrix cores (16x the fp32 MFMA rate).  Every
+// fp32 operand is split into NSP bf16 pieces, x = p0 + p1 + p2 + r, each piece
+// the bf16 rounding of what the previous ones leave (x - p0 and x - p0 - p1
+// are exact in fp32), so |r| <= 2^-27 |x| for three pieces: x is carried to
+// fp32's 24 bits.  A product a*b is summed as the piece products p_i q_j with
+// i + j < NSP (NSP = 3: 6 products; the dropped ones are <= 2^-26 |ab|, under
+// fp32's own 2^-24 rounding of a product), smallest first, into the fp32
+// accumulator.  Each bf16 x bf16 product is exact in fp32.
+// GS_SPLIT_PIECES=2 is the round-2 two-piece split (3 products, ~2^-17 per
+// product), kept for timing comparisons only.
+#ifndef GS_SPLIT_PIECES
+#define GS_SPLIT_PIECES 3
+#endif
+constexpr int NSP = GS_SPLIT_PIECES;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+struct bsplit {
+  bf16x8 p[NSP];
+};
 
 __device__ inline float4_t mfma_bf16(const bf16x8& a, const bf16x8& b, float4_t c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
-__device__ inline f32x16 mfma32_bf16(const bf16x8& a, const bf16x8& b, f32x16 c) {
+__device__ inline f32x16 mfma_bf16(const bf16x8& a, const bf16x8& b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
-__device__ inline void split_bf16(const float (&x)[8], bf16x8& hi, bf16x8& lo) {
+__device__ inline void split_bf16(const float (&x)[8], bsplit& s) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const __bf16 h = (__bf16)x[j];
-    hi[j] = h;
-    lo[j] = (__bf16)(x[j] - (float)h);
+    float r = x[j];
+#pragma unroll
+    for (int i = 0; i < NSP; ++i) {
+      const __bf16 h = (__bf16)r;
+      s.p[i][j] = h;
+      if (i + 1 < NSP) r -= (float)h;
+    }
   }
 }
-// 3-term split product (a_hi b_hi + a_hi b_lo + a_lo b_hi) accumulated into c
-__device__ inline float4_t mfma3(const bf16x8& ah, const bf16x8& al, const bf16x8& bh, const bf16x8& bl,
-                                 float4_t c) {
-  c = mfma_bf16(ah, bh, c);
-  c = mfma_bf16(ah, bl, c);
-  return mfma_bf16(al, bh, c);
+// c += a * b over the split pieces (i + j < NSP), the smallest products first
+template <class Acc>
+__device__ inline Acc mfma_split(const bsplit& a, const bsplit& b, Acc c) {
+#pragma unroll
+  for (int o = NSP - 1; o >= 0; --o)
+#pragma unroll
+    for (int i = 0; i <= o; ++i) c = mfma_bf16(a.p[i], b.p[o - i], c);
+  return c;
+}
+// c += a * x with x split here, one piece at a time (fewer live registers
+// than mfma_split: x's pieces never coexist); largest products first
+template <class Acc>
+__device__ inline Acc mfma_split_x(const bsplit& a, const float (&x)[8], Acc c) {
+  float r[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) r[e] = x[e];
+#pragma unroll
+  for (int j = 0; j < NSP; ++j) {
+    bf16x8 b;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      b[e] = (__bf16)r[e];
+      if (j + 1 < NSP) r[e] -= (float)b[e];
+    }
+#pragma unroll
+    for (int i = 0; i + j < NSP; ++i) c = mfma_bf16(a.p[i], b, c);
+  }
+  return c;
+}
+// c += a * b for an operand a that is exact in bf16 (b split)
+template <class Acc>
+__device__ inline Acc mfma_exact_split(const bf16x8& a, const bsplit& b, Acc c) {
+#pragma unroll
+  for (int i = NSP - 1; i >= 0; --i) c = mfma_bf16(a, b.p[i], c);
+  return c;
 }
 
 // ------------------------------------------------------------------ forward
@@ -356,7 +402,7 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
     for (int fb = 0; fb < FB; ++fb) {
-      bf16x8 Ah, Al;
+      bsplit A;
       {
         float fa[8];
 #pragma unroll
@@ -365,23 +411,17 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
           const uint32_t g = (uint32_t)__shfl((int)gidv, k, 64);
           fa[j] = k < n ? feats[(size_t)g * F + fb * 32 + (ln & 31)] : 0.f;
         }
-        split_bf16(fa, Ah, Al);
+        split_bf16(fa, A);
       }
 #pragma unroll
       for (int blk = 0; blk < 2; ++blk) {
-        bf16x8 Bh, Bl;
-        {
-          float x[8];
+        float x[8];
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const int k = 8 * h + j;
-            x[j] = k < n ? s_fw[lw][k][(ln & 31) + 32 * blk] : 0.f;
-          }
-          split_bf16(x, Bh, Bl);
+        for (int j = 0; j < 8; ++j) {
+          const int k = 8 * h + j;
+          x[j] = k < n ? s_fw[lw][k][(ln & 31) + 32 * blk] : 0.f;
         }
-        acc[2 * fb + blk] = mfma32_bf16(Ah, Bh, acc[2 * fb + blk]);
-        acc[2 * fb + blk] = mfma32_bf16(Ah, Bl, acc[2 * fb + blk]);
-        acc[2 * fb + blk] = mfma32_bf16(Al, Bh, acc[2 * fb + blk]);
+        acc[2 * fb + blk] = mfma_split_x(A, x, acc[2 * fb + blk]);
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -694,7 +734,15 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
   constexpr int FW = F < 16 ? F : 0;          // feature rows 4.. of the colour block (F = 4, 8)
   constexpr bool FIXED_FEAT = (COMPAT != COMPAT_REFERENCE) && F > 0;
   // per record: (x, y, -a/2, -b) (-c/2, opacity, r, g) (b, depth, -, -)
-  __shared__ float4 s_rec[GS_WPB_BWD][CHUNK][3];
+  __shared__ float4 s_rec[GS_WPB_BWD][CHUNK][2];
+  __shared__ float2 s_rec2[GS_WPB_BWD][CHUNK];  // (b, depth)
+  // Colour block operand rows 0..3 (dL/dC_r,g,b, dL/dD) of the strip, split,
+  // in the A layout: [k-step][piece][row][pixel group of 8].  Kept in LDS
+  // (1.5 KiB) rather than in 24 VGPRs when the colour block carries no
+  // feature rows (F = 0 or >= 16): every lane reads row (l&15)&3, so rows
+  // 4..15 of the colour sums hold copies nobody reads.
+  constexpr bool XW_LDS = (FW == 0);
+  __shared__ bf16x8 s_xw[GS_WPB_BWD][XW_LDS ? 2 : 1][NSP][4][4];
   // batch weights [slot][pixel] (row pad 4: the operand reads are conflict-free)
   __shared__ float s_w[GS_WPB_BWD][WB][68];
   __shared__ float s_u[GS_WPB_BWD][WB][68];
@@ -752,9 +800,22 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
   // strip row: column p % STRIP_W, row p / STRIP_W):
   //   Xw: row l&15 of the colour block: 0..2 dL/dC, 3 dL/dD, 4.. dL/dF (F < 16)
   //   Bf: dL/dF[p][16cb + (l&15)] (F >= 16; B operand of the feature blocks)
-  bf16x8 Xwh[2], Xwl[2];
-  bf16x8 Bfh[CB1][2], Bfl[CB1][2];
+  bsplit Xw[XW_LDS ? 1 : 2];
+  bsplit Bf[CB1][2];
   const int kp0 = 8 * (lane >> 4);  // first strip pixel of the lane at k-step 0
+  // the colour block operand of k-step s: into LDS (rows 0..3) or registers
+  auto store_xw = [&](const float (&x)[8], int s) {
+    if constexpr (XW_LDS) {
+      bsplit t;
+      split_bf16(x, t);
+      if ((lane & 15) < 4) {
+#pragma unroll
+        for (int i = 0; i < NSP; ++i) s_xw[lw][s][i][lane & 15][lane >> 4] = t.p[i];
+      }
+    } else {
+      split_bf16(x, Xw[s]);
+    }
+  };
   {
     const int row = lane & 15;
     const float* src = nullptr;
@@ -800,11 +861,11 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
       for (int s = 0; s < 2; ++s) {
         float x[8];
         unpack(rw[s], src != nullptr, x);
-        split_bf16(x, Xwh[s], Xwl[s]);
+        store_xw(x, s);
 #pragma unroll
         for (int cb = 0; cb < CB; ++cb) {
           unpack(rf[cb][s], fplane0 != nullptr, x);
-          split_bf16(x, Bfh[cb][s], Bfl[cb][s]);
+          split_bf16(x, Bf[cb][s]);
         }
       }
     } else {
@@ -815,14 +876,14 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
         float xw[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) xw[j] = (src && qx + j < W && qy < H) ? src[(size_t)qy * W + qx + j] : 0.f;
-        split_bf16(xw, Xwh[s], Xwl[s]);
+        store_xw(xw, s);
 #pragma unroll
         for (int cb = 0; cb < CB; ++cb) {
           const float* fsrc = fplane0 ? fplane0 + (size_t)(16 * cb) * HW : nullptr;
           float xf[8];
 #pragma unroll
           for (int j = 0; j < 8; ++j) xf[j] = (fsrc && qx + j < W && qy < H) ? fsrc[(size_t)qy * W + qx + j] : 0.f;
-          split_bf16(xf, Bfh[cb][s], Bfl[cb][s]);
+          split_bf16(xf, Bf[cb][s]);
         }
       }
     }
@@ -849,28 +910,51 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
       const int i = lane + 64 * t;
       agid[t] = i < WB * A_FEAT ? f_bits(s_slot[lw][i / A_FEAT].w) : 0u;
     }
-    bf16x8 Wh[2], Wl[2], Uh[2], Ul[2];
+    // All sums of the batch first, one k-step (32 pixels) at a time, so that
+    // only one k-step's split weights are live:
+    //   cw: colour / depth (/ small features) C[row][slot] = sum_p Xw[row][p] w[slot][p]
+    //   cu: geometry rows, the monomials of the lane's pixels against u
+    //   cf: features C[slot][ch] = sum_p w[slot][p] dL/dF[p][ch]
+    float4_t cw = float4_t{0.f, 0.f, 0.f, 0.f};
+    float4_t cu = float4_t{0.f, 0.f, 0.f, 0.f};
+    float4_t cf[CB1];
+#pragma unroll
+    for (int cb = 0; cb < CB1; ++cb) cf[cb] = float4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int p0 = 32 * s + 8 * (lane >> 4);
-      float x[8], y[8];
-      const float4 a0 = *reinterpret_cast<const float4*>(&s_w[lw][g][p0]);
-      const float4 a1 = *reinterpret_cast<const float4*>(&s_w[lw][g][p0 + 4]);
-      const float4 b0 = *reinterpret_cast<const float4*>(&s_u[lw][g][p0]);
-      const float4 b1 = *reinterpret_cast<const float4*>(&s_u[lw][g][p0 + 4]);
-      x[0] = a0.x; x[1] = a0.y; x[2] = a0.z; x[3] = a0.w; x[4] = a1.x; x[5] = a1.y; x[6] = a1.z; x[7] = a1.w;
-      y[0] = b0.x; y[1] = b0.y; y[2] = b0.z; y[3] = b0.w; y[4] = b1.x; y[5] = b1.y; y[6] = b1.z; y[7] = b1.w;
-      split_bf16(x, Wh[s], Wl[s]);
-      split_bf16(y, Uh[s], Ul[s]);
-    }
-    // colour / depth (/ small features): C[row][slot] = sum_p Xw[row][p] w[slot][p]
-    float4_t cw = float4_t{0.f, 0.f, 0.f, 0.f};
-    float4_t cu = float4_t{0.f, 0.f, 0.f, 0.f};
+      {
+        // the weights w: colour block and features
+        bsplit Ws;
+        {
+          float x[8];
+          const float4 a0 = *reinterpret_cast<const float4*>(&s_w[lw][g][p0]);
+          const float4 a1 = *reinterpret_cast<const float4*>(&s_w[lw][g][p0 + 4]);
+          x[0] = a0.x; x[1] = a0.y; x[2] = a0.z; x[3] = a0.w; x[4] = a1.x; x[5] = a1.y; x[6] = a1.z; x[7] = a1.w;
+          split_bf16(x, Ws);
+        }
+        if constexpr (XW_LDS) {
+          bsplit xw;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      // geometry rows: the monomials 1, X, Y, X^2, XY, Y^2 of the lane's
-      // pixels (X = 2 (px - cx) = 2 col - (STRIP_W - 1), Y = 2 row - (STRIP_H - 1)
-      // for strip pixel p = 32s + 8(l>>4) + j)
+          for (int i = 0; i < NSP; ++i) xw.p[i] = s_xw[lw][s][i][lane & 3][(lane >> 4) & 3];
+          cw = mfma_split(xw, Ws, cw);
+        } else {
+          cw = mfma_split(Xw[s], Ws, cw);
+        }
+#pragma unroll
+        for (int cb = 0; cb < CB; ++cb) cf[cb] = mfma_split(Ws, Bf[cb][s], cf[cb]);
+      }
+      // the weights u: geometry rows, the monomials 1, X, Y, X^2, XY, Y^2 of
+      // the lane's pixels (X = 2 (px - cx) = 2 col - (STRIP_W - 1),
+      // Y = 2 row - (STRIP_H - 1) for strip pixel p = 32s + 8(l>>4) + j)
+      bsplit Us;
+      {
+        float y[8];
+        const float4 b0 = *reinterpret_cast<const float4*>(&s_u[lw][g][p0]);
+        const float4 b1 = *reinterpret_cast<const float4*>(&s_u[lw][g][p0 + 4]);
+        y[0] = b0.x; y[1] = b0.y; y[2] = b0.z; y[3] = b0.w; y[4] = b1.x; y[5] = b1.y; y[6] = b1.z; y[7] = b1.w;
+        split_bf16(y, Us);
+      }
       bf16x8 xu;
       {
         // recomputed at every flush (an opaque copy of the lane index keeps
@@ -892,9 +976,7 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
           xu[j] = (__bf16)fmaf(X, fmaf(cc, X, cb), ca);
         }
       }
-      cw = mfma3(Xwh[s], Xwl[s], Wh[s], Wl[s], cw);
-      cu = mfma_bf16(xu, Uh[s], cu);
-      cu = mfma_bf16(xu, Ul[s], cu);
+      cu = mfma_exact_split(xu, Us, cu);
     }
     // lane l < 16 holds rows 0..3 of slot l; rows 4, 5 of cu come from lane l + 16
     const float s_xy = __shfl_down(cu[0], 16, 64);
@@ -955,17 +1037,14 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
     // channel 16cb + (l&15) of slots (l>>4)*4 + r
 #pragma unroll
     for (int cb = 0; cb < CB; ++cb) {
-      float4_t cf = float4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < 2; ++s) cf = mfma3(Wh[s], Wl[s], Bfh[cb][s], Bfl[cb][s], cf);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int slot = (lane >> 4) * 4 + r;
         const uint32_t gi = fgid[r];
 #ifdef GS_EXP_NO_FEAT_ATOMIC
-        if (slot < nb && cf[r] == 12345.f) dsem[(size_t)gi * F + 16 * cb + g] = 0.f;
+        if (slot < nb && cf[cb][r] == 12345.f) dsem[(size_t)gi * F + 16 * cb + g] = 0.f;
 #else
-        if (slot < nb) atomicAdd(dsem + (size_t)gi * F + 16 * cb + g, cf[r]);
+        if (slot < nb) atomicAdd(dsem + (size_t)gi * F + 16 * cb + g, cf[cb][r]);
 #endif
       }
     }
@@ -1011,7 +1090,7 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
       const float4 h = half_conic(q.q0, q.q1);
       s_rec[lw][lane][0] = make_float4(q.q0.x, q.q0.y, h.x, h.y);
       s_rec[lw][lane][1] = make_float4(h.z, q.q1.y, q.q1.z, q.q1.w);
-      s_rec[lw][lane][2] = make_float4(q.q2.x, q.q2.y, 0.f, 0.f);
+      s_rec2[lw][lane] = q.q2;
     }
     const uint32_t chunk_gid = q.gid;  // lane j: id of the chunk's j-th record
 #ifndef GS_OLD_MATH
@@ -1034,7 +1113,7 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
       const uint32_t k = c0 + j - range.x;  // position in the tile list
       const float4 r0 = s_rec[lw][j][0];
       const float4 r1 = s_rec[lw][j][1];
-      const float4 r2 = s_rec[lw][j][2];
+      const float2 r2 = s_rec2[lw][j];
       const float dx = r0.x - pfx, dy = r0.y - pfy;
       const float op = r1.y;
       const float power = gauss_power(dx, dy, make_float4(r0.z, r0.w, r1.x, 0.f));

@@ -11,7 +11,7 @@ all_reduce (train.py:288-290, external.py:136-140).
 """
 from __future__ import annotations
 
-from typing import Dict, Iterable, List
+from typing import Dict, Iterable, List, Mapping, Sequence
 
 import torch
 import torch.distributed as dist
@@ -20,6 +20,12 @@ import torch.distributed as dist
 def shard_cameras(n_cams: int, rank: int, world: int) -> List[int]:
     """Camera c goes to rank c mod world."""
     return [c for c in range(n_cams) if c % world == rank]
+
+
+class StaleBucketError(RuntimeError):
+    """A tensor the bucket was built over has been replaced or resized (the
+    reference's densification rebinds variables[...] and the optimizer's
+    Parameters, external.py:202-204, 273-275): build a new GradBucket."""
 
 
 class GradBucket:
@@ -35,33 +41,114 @@ class GradBucket:
     the common starting value.  Summing the totals themselves would multiply
     the history by world_size every step.  Synchronisation points are the
     construction, every all_reduce(), and resync() -- call it after changing
-    the extras identically on every rank outside a step (e.g. the
-    densification reset of the accumulators, external.py:237-240).
+    the extras' VALUES identically on every rank outside a step.
+
+    Densification (external.py:202-204, 237-240, 273-275) does not change
+    values in place: it binds NEW tensors into the variables dict and NEW
+    Parameters into the optimizer, with a different Gaussian count.  A bucket
+    cannot follow that; all_reduce() and resync() therefore check that every
+    tensor is still the live object with the size the bucket was built for
+    and raise StaleBucketError otherwise -- build a new GradBucket after every
+    densification.  To let the check see replacements, pass the containers
+    the caller rebinds: `params` may be a dict (name -> Parameter, e.g. the
+    params dict the optimizer groups are built from) and `extras_from` a
+    (dict, keys) pair (e.g. (variables, ["means2D_gradient_accum", "denom"])).
+
+    bind_grads=True makes every parameter's .grad a view into the flat
+    buffer: the backward accumulates straight into the bucket, so
+    all_reduce() needs no pack/unpack copies of the gradients.  Clear the
+    gradients with zero_grad() (one fill of the buffer) instead of the
+    optimizer's zero_grad(set_to_none=True), which would unbind them.
     """
 
-    def __init__(self, params: Iterable[torch.Tensor], extras: Dict[str, torch.Tensor] | None = None):
-        self.params = [p for p in params]
+    def __init__(self, params: Iterable[torch.Tensor] | Mapping[str, torch.Tensor],
+                 extras: Dict[str, torch.Tensor] | None = None,
+                 extras_from: tuple[Mapping[str, torch.Tensor], Sequence[str]] | None = None,
+                 bind_grads: bool = False):
+        if isinstance(params, Mapping):
+            self._param_src, self._param_keys = params, list(params.keys())
+            self.params = [params[k] for k in self._param_keys]
+        else:
+            self._param_src, self._param_keys = None, None
+            self.params = list(params)
         self.extras = dict(extras or {})
-        sizes = [p.numel() for p in self.params] + [t.numel() for t in self.extras.values()]
+        self._extra_src = None
+        if extras_from is not None:
+            src, keys = extras_from
+            self._extra_src = src
+            for k in keys:
+                self.extras[k] = src[k]
+        self._param_numel = [p.numel() for p in self.params]
+        self._extra_numel = {k: t.numel() for k, t in self.extras.items()}
+        sizes = self._param_numel + list(self._extra_numel.values())
         self.sizes = sizes
         dev = self.params[0].device
         self.flat = torch.zeros(sum(sizes), dtype=torch.float32, device=dev)
+        self.bound = bind_grads
+        self._views = []
+        o = 0
+        for p in self.params:
+            n = p.numel()
+            self._views.append(self.flat[o:o + n].view_as(p))
+            o += n
+        if bind_grads:
+            for p, v in zip(self.params, self._views):
+                p.grad = v
         self._base = {}
         self.resync()
+
+    # ---------------------------------------------------------------- checks
+    def check_live(self) -> None:
+        """Raise StaleBucketError if a parameter or extra was replaced or
+        resized since construction, or a bound gradient was unbound."""
+        if self._param_src is not None:
+            for k, p in zip(self._param_keys, self.params):
+                if self._param_src.get(k) is not p:
+                    raise StaleBucketError(f"parameter '{k}' was replaced (densification?): "
+                                           "build a new GradBucket")
+        for i, (p, n) in enumerate(zip(self.params, self._param_numel)):
+            if p.numel() != n:
+                raise StaleBucketError(f"parameter {i} changed size {n} -> {p.numel()}: build a new GradBucket")
+        if self._extra_src is not None:
+            for k, t in self.extras.items():
+                if k in self._extra_src and self._extra_src[k] is not t:
+                    raise StaleBucketError(f"statistic '{k}' was replaced (densification?): "
+                                           "build a new GradBucket")
+        for k, t in self.extras.items():
+            if t.numel() != self._extra_numel[k]:
+                raise StaleBucketError(f"statistic '{k}' changed size: build a new GradBucket")
+        if self.bound:
+            for i, (p, v) in enumerate(zip(self.params, self._views)):
+                if p.grad is None or p.grad.data_ptr() != v.data_ptr():
+                    raise StaleBucketError(
+                        f"parameter {i}'s .grad is no longer the bucket's view (zero_grad(set_to_none=True)?): "
+                        "clear gradients with GradBucket.zero_grad()")
+
+    # ---------------------------------------------------------------- grads
+    def zero_grad(self) -> None:
+        """Bound mode: zero every gradient with one fill of the buffer."""
+        if self.bound:
+            n = sum(self._param_numel)
+            self.flat[:n].zero_()
+        else:
+            for p in self.params:
+                p.grad = None
 
     def resync(self) -> None:
         """Record the extras' current values as the common starting point of
         the next step (they must be identical on every rank)."""
+        self.check_live()
         self._base = {k: t.detach().clone() for k, t in self.extras.items()}
 
     def pack(self):
         o = 0
-        for p in self.params:
+        for p, v in zip(self.params, self._views):
             n = p.numel()
-            if p.grad is None:
-                self.flat[o:o + n].zero_()
-            else:
-                self.flat[o:o + n].copy_(p.grad.reshape(-1))
+            if not self.bound:
+                if p.grad is None:
+                    v.zero_()
+                else:
+                    v.copy_(p.grad)
             o += n
         for k, t in self.extras.items():
             n = t.numel()
@@ -71,11 +158,12 @@ class GradBucket:
 
     def unpack(self):
         o = 0
-        for p in self.params:
+        for p, v in zip(self.params, self._views):
             n = p.numel()
-            if p.grad is None:
-                p.grad = torch.empty_like(p)
-            p.grad.reshape(-1).copy_(self.flat[o:o + n])
+            if not self.bound:
+                if p.grad is None:
+                    p.grad = torch.empty_like(p)
+                p.grad.copy_(v)
             o += n
         for k, t in self.extras.items():
             n = t.numel()
@@ -86,6 +174,7 @@ class GradBucket:
     def all_reduce(self, group=None):
         """pack -> one all_reduce(SUM) -> unpack.  Without a process group
         (or with one rank) the values stay as they are."""
+        self.check_live()
         if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
             self.resync()
             return

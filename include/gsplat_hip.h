@@ -244,6 +244,30 @@ int gs_debug_export(int64_t P, int32_t W, int32_t H, const void *geom_buffer,
                     uint32_t *point_list, uint32_t *ranges, uint32_t *n_contrib,
                     gs_stream_t stream);
 
+/* ---- debug-mode state validation (host functions, no device access)
+ *
+ * With `debug` set the forward checks the state it built before the blend
+ * kernels dereference it (the reference's debug mode only synchronises and
+ * reports launch errors, CR/auxiliary.h:172-179): the plan header after the
+ * one host read of the forward, then the per-tile ranges and the tile lists
+ * after the sort.  A violation returns a negative status with the message in
+ * gs_last_error() (GsplatError in Python) instead of launching.  Exported so
+ * the checks themselves are testable on the host with corrupted inputs.
+ *
+ * gs_check_plan_header: hdr = the 8-word plan header of one camera
+ *   {list instances L, longest tile, reference num_rendered, status, sort-class
+ *   prefixes p1, q1, p2, -}; tiles = the camera's tile count.  Requires
+ *   L <= num_rendered, longest tile <= L, status bits <= 3 and
+ *   q1 <= p1, p2 <= p1 <= tiles.
+ * gs_check_ranges: ranges = tiles x [begin, end) of one camera's lists;
+ *   every range in [0, L], begin <= end, the non-empty ranges contiguous in
+ *   tile order and covering exactly [0, L); longest range <= max_len (< 0: no
+ *   bound).
+ * gs_check_point_list: every id of a camera's L list entries < P. */
+int gs_check_plan_header(const uint32_t *hdr, int64_t tiles);
+int gs_check_ranges(const uint32_t *ranges, int64_t tiles, int64_t L, int64_t max_len);
+int gs_check_point_list(const uint32_t *ids, int64_t L, int64_t P);
+
 /* Stable LSD radix sort of (u64 key, u32 value) pairs on bits [0, end_bit)
  * -- the standalone form of the binning sort (cub::DeviceRadixSort::SortPairs
  * at CR/rasterizer_impl.cu:309).  keys/vals are sorted in place; scratch is

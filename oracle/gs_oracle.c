@@ -393,6 +393,18 @@ void or_render_fwd(int W, int H, const uint32_t *ranges,
   free(sf);
 }
 
+/* Pixel visiting order of or_render_bwd (NULL: tile by tile, row-major inside
+ * a tile).  The per-Gaussian gradient sums are fp32 additions in pixel order,
+ * as the reference's atomicAdd calls are in arrival order; a permuted order
+ * measures how far fp32 summation order alone moves them (the envelope the
+ * GPU's differences are judged against, tests/test_gpu_envelope.py). */
+static const uint32_t *g_pix_order = NULL;
+static int64_t g_pix_order_n = 0;
+void or_set_pixel_order(const uint32_t *order, int64_t n) {
+  g_pix_order = order;
+  g_pix_order_n = order ? n : 0;
+}
+
 /* renderCUDA<3> (backward), CR/backward.cu:432-652.  Per-pixel reverse walk.
  * Gradients are accumulated (+=) into caller-zeroed arrays:
  *   dmean2D P x 3 (x,y), dconic P x 4 (x,y,w), dopacity P, dcolors P x 3,
@@ -414,13 +426,20 @@ void or_render_bwd(int W, int H, const uint32_t *ranges,
   float *acc_f = (float *)malloc(sizeof(float) * Fa);
   float *last_f = (float *)malloc(sizeof(float) * Fa);
   float *dlf = (float *)malloc(sizeof(float) * Fa);
+  const int permuted = g_pix_order != NULL && g_pix_order_n == (int64_t)HW;
   for (int ty = 0; ty < gy; ++ty)
     for (int tx = 0; tx < gx; ++tx) {
-      const uint32_t r0 = ranges[2 * (ty * gx + tx)], r1 = ranges[2 * (ty * gx + tx) + 1];
       for (int ly = 0; ly < TILE; ++ly)
         for (int lx = 0; lx < TILE; ++lx) {
-          const int px = tx * TILE + lx, py = ty * TILE + ly;
+          int px = tx * TILE + lx, py = ty * TILE + ly;
           if (px >= W || py >= H) continue;
+          if (permuted) { /* visit the pixels in the caller's order instead */
+            const size_t q = g_pix_order[(size_t)py * W + px];
+            px = (int)(q % (size_t)W);
+            py = (int)(q / (size_t)W);
+          }
+          const int tile = (py / TILE) * gx + px / TILE;
+          const uint32_t r0 = ranges[2 * tile], r1 = ranges[2 * tile + 1];
           const size_t pix = (size_t)py * W + px;
           const float pfx = (float)px, pfy = (float)py;
           const float T_final = 1 - alphas[pix];

@@ -63,6 +63,8 @@ def lib():
         L.or_render_bwd.argtypes = [_I, _I, _u32, _u32, _f, _f, _f, _f, _f, _I, _f, _f, _u32,
                                     _f, _f, _f, _f, _I, _f, _f, _f, _f, _f, _f]
         L.or_render_bwd.restype = None
+        L.or_set_pixel_order.argtypes = [_u32, ctypes.c_int64]
+        L.or_set_pixel_order.restype = None
         L.or_preprocess_bwd.argtypes = [_I, _I, _I, _f, _i, _f, _u8, _f, _f, _F, _f, _f, _f,
                                         _I, _I, _F, _F, _F, _F, _f, _f, _f, _f, _f, _I,
                                         _f, _f, _f, _f, _f]
@@ -194,13 +196,19 @@ def rasterize_gaussians_backward(bg, means3D, radii, colors, semantic_feature, s
                                  tan_fovx, tan_fovy, dL_dout_color, dL_dout_feature,
                                  dL_dout_depth, dL_dout_alpha, sh, degree, campos, state, R,
                                  binning_unused, image_unused, alpha, debug=False,
-                                 compat="reference"):
+                                 compat="reference", pixel_order=None):
     """Positional mirror of RasterizeGaussiansBackwardCUDA (DGR/rasterize_points.cu:128-225).
 
     Camera scalars are taken in C++ positional order (c_x, c_y, tan_fovx, tan_fovy),
     exactly as the reference binding receives them.  Returns
     (dL_dmeans2D, dL_dcolors, dL_dsemantic, dL_dopacity, dL_dmeans3D, dL_dcov3D,
      dL_dsh, dL_dscales, dL_drotations).
+
+    `pixel_order` (optional, a permutation of the H*W pixel indices) changes
+    the order in which the blend backward visits pixels, hence the fp32
+    summation order of every per-Gaussian gradient sum (the reference sums
+    with atomicAdd in arrival order): the spread it causes is the fp32
+    envelope the GPU's differences are compared with.
     """
     L_ = lib()
     cm = COMPAT[compat]
@@ -231,12 +239,19 @@ def rasterize_gaussians_backward(bg, means3D, radii, colors, semantic_feature, s
         dLf = np.zeros((F, H, W), np.float32)
     feat_colors = colors if colors is not None else st.rgb
     radii_np = _np(radii, np.int32)
+    order = None
+    if pixel_order is not None:
+        order = np.ascontiguousarray(pixel_order, np.uint32)
+        assert order.size == H * W
+        L_.or_set_pixel_order(_p(order, _u32), ctypes.c_int64(order.size))
     L_.or_render_bwd(W, H, _p(st.ranges, _u32), _p(st.point_list, _u32), _p(_np(bg)),
                      _p(st.means2D), _p(st.conic_opacity), _p(feat_colors), _p(sem), F,
                      _p(st.depths), _p(_np(alpha)), _p(st.n_contrib, _u32), _p(dLc), _p(dLf),
                      _p(_np(dL_dout_depth)), _p(_np(dL_dout_alpha)), cm, _p(out["dmean2D"]),
                      _p(dconic), _p(out["dopacity"]), _p(out["dcolors"]), _p(out["dsem"]),
                      _p(ddepth))
+    if order is not None:
+        L_.or_set_pixel_order(None, ctypes.c_int64(0))
     cov_pre = _np(cov3D_precomp)
     cov = cov_pre if cov_pre is not None else st.cov3D
     L_.or_preprocess_bwd(P, int(degree), M, _p(means3D), _p(radii_np, _i), _p(sh),

@@ -121,10 +121,13 @@ def preprocess(means3D, scales, rotations, view, proj, tanfovx, tanfovy, cx, cy,
 
 
 def render(means3D, colors, opacity, scales, rotations, view, proj, tanfovx, tanfovy, cx, cy, W, H, bg,
-           features=None, means2D=None, scale_modifier=1.0):
+           features=None, means2D=None, scale_modifier=1.0, tiles=None):
     """-> (color [3,H,W], depth [1,H,W], features [F,H,W] or None,
-    alpha = 1 - T_final [1,H,W]), float64, differentiable in every float
-    input (means2D: the NDC offset leaf)."""
+    alpha = 1 - T_final [1,H,W]) in the inputs' float dtype (float64 for the
+    gradient checks, float32 for bench.py's CPU baseline), differentiable in
+    every float input (means2D: the NDC offset leaf).  `tiles` (an iterable
+    of (tx, ty)) renders only those 16x16 tiles; the rest of the image stays
+    zero (a bounded sample of a large render)."""
     pre = preprocess(means3D, scales, rotations, view, proj, tanfovx, tanfovy, cx, cy, W, H, scale_modifier,
                      means2D)
     vis = pre["visible"]
@@ -143,42 +146,44 @@ def render(means3D, colors, opacity, scales, rotations, view, proj, tanfovx, tan
     Fd = feat.shape[1] if feat is not None else 0
     fmap = None
     rows_c, rows_d, rows_a, rows_f, where = [], [], [], [], []
-    for ty in range(gy):
-        for tx in range(gx):
-            x0, y0 = tx * TILE, ty * TILE
-            x1, y1 = min(x0 + TILE, W), min(y0 + TILE, H)
-            ys, xs = torch.meshgrid(torch.arange(y0, y1, dtype=torch.float64),
-                                    torch.arange(x0, x1, dtype=torch.float64), indexing="ij")
-            qx, qy = xs.reshape(-1, 1), ys.reshape(-1, 1)
-            m = torch.nonzero((tx >= rmin_x) & (tx < rmax_x) & (ty >= rmin_y) & (ty < rmax_y)).squeeze(1)
-            if m.numel() == 0:
-                c = bg[None].expand(qx.shape[0], 3)
-                rows_c.append(c); rows_d.append(torch.zeros(qx.shape[0], dtype=means3D.dtype))
-                rows_a.append(torch.zeros(qx.shape[0], dtype=means3D.dtype))
-                if feat is not None:
-                    rows_f.append(torch.zeros(qx.shape[0], Fd, dtype=means3D.dtype))
-                where.append((x0, y0, x1, y1))
-                continue
-            dx, dy = px[m][None] - qx, py[m][None] - qy
-            cm = con[m]
-            power = -0.5 * (cm[:, 0] * dx * dx + cm[:, 2] * dy * dy) - cm[:, 1] * dx * dy
-            alpha = torch.clamp(op[m][None] * torch.exp(power), max=0.99)
-            with torch.no_grad():
-                valid = (power <= 0) & (alpha >= 1.0 / 255.0)
-            a = torch.where(valid, alpha, torch.zeros_like(alpha))
-            one_m = 1.0 - a
-            T_excl = torch.cumprod(torch.cat([torch.ones_like(one_m[:, :1]), one_m[:, :-1]], 1), 1)
-            with torch.no_grad():
-                stop = valid & (T_excl * one_m < 1e-4)
-                keep = torch.cumsum(stop.int(), 1) == 0
-            w = a * T_excl * keep
-            T_final = torch.prod(torch.where(keep, one_m, torch.ones_like(one_m)), 1)
-            rows_c.append(w @ col[m] + T_final[:, None] * bg[None])
-            rows_d.append(w @ z[m])
-            rows_a.append(1.0 - T_final)
+    dt = means3D.dtype
+    bg = bg.to(dt)
+    tile_iter = tiles if tiles is not None else [(tx, ty) for ty in range(gy) for tx in range(gx)]
+    for tx, ty in tile_iter:
+        x0, y0 = tx * TILE, ty * TILE
+        x1, y1 = min(x0 + TILE, W), min(y0 + TILE, H)
+        ys, xs = torch.meshgrid(torch.arange(y0, y1, dtype=dt),
+                                torch.arange(x0, x1, dtype=dt), indexing="ij")
+        qx, qy = xs.reshape(-1, 1), ys.reshape(-1, 1)
+        m = torch.nonzero((tx >= rmin_x) & (tx < rmax_x) & (ty >= rmin_y) & (ty < rmax_y)).squeeze(1)
+        if m.numel() == 0:
+            c = bg[None].expand(qx.shape[0], 3)
+            rows_c.append(c); rows_d.append(torch.zeros(qx.shape[0], dtype=means3D.dtype))
+            rows_a.append(torch.zeros(qx.shape[0], dtype=means3D.dtype))
             if feat is not None:
-                rows_f.append(w @ feat[m])
+                rows_f.append(torch.zeros(qx.shape[0], Fd, dtype=means3D.dtype))
             where.append((x0, y0, x1, y1))
+            continue
+        dx, dy = px[m][None] - qx, py[m][None] - qy
+        cm = con[m]
+        power = -0.5 * (cm[:, 0] * dx * dx + cm[:, 2] * dy * dy) - cm[:, 1] * dx * dy
+        alpha = torch.clamp(op[m][None] * torch.exp(power), max=0.99)
+        with torch.no_grad():
+            valid = (power <= 0) & (alpha >= 1.0 / 255.0)
+        a = torch.where(valid, alpha, torch.zeros_like(alpha))
+        one_m = 1.0 - a
+        T_excl = torch.cumprod(torch.cat([torch.ones_like(one_m[:, :1]), one_m[:, :-1]], 1), 1)
+        with torch.no_grad():
+            stop = valid & (T_excl * one_m < 1e-4)
+            keep = torch.cumsum(stop.int(), 1) == 0
+        w = a * T_excl * keep
+        T_final = torch.prod(torch.where(keep, one_m, torch.ones_like(one_m)), 1)
+        rows_c.append(w @ col[m] + T_final[:, None] * bg[None])
+        rows_d.append(w @ z[m])
+        rows_a.append(1.0 - T_final)
+        if feat is not None:
+            rows_f.append(w @ feat[m])
+        where.append((x0, y0, x1, y1))
     # assemble (index_put keeps the graph)
     pix = torch.cat([(torch.arange(y0, y1)[:, None] * W + torch.arange(x0, x1)[None]).reshape(-1)
                      for (x0, y0, x1, y1) in where])

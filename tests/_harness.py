@@ -117,7 +117,7 @@ def gpu_backward(inp, fwd, grads, compat="reference", swap=None):
     return [t.cpu().numpy() for t in out]
 
 
-def oracle_backward(inp, ofwd, grads, compat="reference", swap=None):
+def oracle_backward(inp, ofwd, grads, compat="reference", swap=None, pixel_order=None):
     if swap is None:
         swap = compat == "reference"
     L, color, feat, depth, alpha, radii, st = ofwd
@@ -126,7 +126,7 @@ def oracle_backward(inp, ofwd, grads, compat="reference", swap=None):
         inp["bg"], inp["means3D"], radii, inp["colors"], inp["semantic_feature"], inp["scales"],
         inp["rotations"], inp["scale_modifier"], inp["cov3D_precomp"], inp["viewmatrix"],
         inp["projmatrix"], *bwd_cam4(inp, swap), dc, df, dd, da, inp["sh"], inp["degree"],
-        inp["campos"], st, L, None, None, alpha, compat=compat)
+        inp["campos"], st, L, None, None, alpha, compat=compat, pixel_order=pixel_order)
 
 
 def export_state(P, W, H, fwd):

@@ -5,6 +5,7 @@
   * the caller-generation arity dispatch (G1..G4) and the settings superset;
   * no CPU fallback: host tensors are rejected loudly.
 """
+import ctypes
 import json
 import os
 import re
@@ -67,6 +68,44 @@ def test_invalid_arguments_report_errors_without_gpu():
     code = L.gs_forward_plan(ctypes.byref(g), ctypes.byref(c), 0, 0, 0, None, None, None,
                              ctypes.byref(n), None, None)
     assert code < 0 and b"feature width" in L.gs_last_error()
+
+
+def test_debug_checks_reject_corrupted_state_without_gpu():
+    """debug=True validates the forward's state on the host before the blend
+    kernels dereference it (gsplat_hip.h, gs_check_*): a corrupted plan
+    header, non-contiguous or out-of-bound ranges and out-of-range Gaussian
+    ids must be refused with a message, valid ones accepted.  Host
+    functions: no GPU needed, no GPU fault provoked."""
+    import numpy as np
+    L = _lib.load()
+    p = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    # {L, longest, num_rendered, status, p1, q1, p2, -}
+    good = np.array([500, 120, 640, 0, 3, 2, 1, 0], np.uint32)
+    assert L.gs_check_plan_header(p(good), 50) == 0
+    for i, v, msg in [(0, 700, b"exceed"), (1, 501, b"longest tile"), (3, 8, b"status"),
+                      (4, 51, b"sort-class"), (5, 4, b"sort-class"), (6, 4, b"sort-class")]:
+        bad = good.copy()
+        bad[i] = v
+        assert L.gs_check_plan_header(p(bad), 50) < 0, (i, v)
+        assert msg in L.gs_last_error(), (i, L.gs_last_error())
+    # 4 tiles, 10 instances: [0,4) [4,4) [4,9) [9,10)
+    rg = np.array([0, 4, 4, 4, 4, 9, 9, 10], np.uint32)
+    assert L.gs_check_ranges(p(rg), 4, 10, 5) == 0
+    assert L.gs_check_ranges(p(rg), 4, 10, -1) == 0
+    assert L.gs_check_ranges(p(rg), 4, 10, 4) < 0 and b"planned longest" in L.gs_last_error()
+    gap = rg.copy(); gap[4] = 5                     # [5,9): a hole at 4
+    assert L.gs_check_ranges(p(gap), 4, 10, -1) < 0 and b"contiguous" in L.gs_last_error()
+    over = rg.copy(); over[7] = 11                  # past L
+    assert L.gs_check_ranges(p(over), 4, 10, -1) < 0 and b"outside" in L.gs_last_error()
+    short = rg.copy(); short[7] = 9; short[6] = 9   # covers 9 of 10
+    assert L.gs_check_ranges(p(short), 4, 10, -1) < 0 and b"cover" in L.gs_last_error()
+    neg = rg.copy(); neg[2], neg[3] = 6, 5          # end < begin
+    assert L.gs_check_ranges(p(neg), 4, 10, -1) < 0
+    ids = np.array([0, 5, 99, 3], np.uint32)
+    assert L.gs_check_point_list(p(ids), 4, 100) == 0
+    ids[2] = 100
+    assert L.gs_check_point_list(p(ids), 4, 100) < 0 and b"id 100" in L.gs_last_error()
+    assert L.gs_check_point_list(p(ids), 2, 100) == 0  # only the first L entries count
 
 
 def test_conventions_match_reference_wrapper(monkeypatch):

@@ -164,3 +164,103 @@ def test_batch_densify_stats_match_reference_bookkeeping(P=12000, W=144, H=112, 
     torch.testing.assert_close(st["denom"], den, rtol=0, atol=0)
     torch.testing.assert_close(st["max_2D_radius"], mx, rtol=0, atol=0)
     torch.testing.assert_close(st["means2D_gradient_accum"], acc, rtol=1e-5, atol=1e-6)
+
+
+def _batch_grads(src, sets, ups, label):
+    """Gradients of one GaussianRasterizerBatch step over `sets` (G3 call)."""
+    leaves = {k: v.clone().requires_grad_(True) for k, v in src.items()}
+    im, radius, feat, depth, alpha = GaussianRasterizerBatch(sets)(
+        means2D=torch.zeros(src["means3D"].shape[0], 3, device=DEV), label=label, **leaves)
+    torch.autograd.backward([im, depth, feat], list(ups))
+    return {k: leaves[k].grad for k in leaves}
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_camera_shards_sum_to_the_full_batch(world, P=15000, W=128, H=96, C=27):
+    """BASELINE configs[3]: the 27-camera step split over N ranks (camera c
+    on rank c mod N, distributed.shard_cameras).  The per-shard batch
+    gradients summed over the shards equal the 27-camera batch's (fp32
+    summation order only), and a bound GradBucket accumulating the shards'
+    backward passes in place holds that same sum."""
+    from dynamic3dgaussians_amd.distributed import GradBucket, shard_cameras
+    src = _scene(P, 32, False, seed=9)
+    rig = camera_rig(C, W, H)
+    sets = _settings(rig, W, H, "reference")
+    gen = torch.Generator(device=DEV).manual_seed(21)
+    up_c = torch.randn(C, 3, H, W, device=DEV, generator=gen)
+    up_d = torch.randn(C, 1, H, W, device=DEV, generator=gen)
+    up_f = torch.randn(C, 32, H, W, device=DEV, generator=gen)
+    label = torch.ones(P, device=DEV)
+    full = _batch_grads(src, sets, (up_c, up_d, up_f), label)
+    shards = [shard_cameras(C, r, world) for r in range(world)]
+    assert sorted(c for s in shards for c in s) == list(range(C))
+    total = {k: torch.zeros_like(v) for k, v in full.items()}
+    for cams in shards:
+        g = _batch_grads(src, [sets[c] for c in cams], (up_c[cams], up_d[cams], up_f[cams]), label)
+        for k in total:
+            total[k] += g[k]
+    for k in full:
+        assert _rel(total[k], full[k]) <= 1e-5, (k, _rel(total[k], full[k]))
+    # the bench's path: leaves whose .grad are views into one bucket, every
+    # shard's backward accumulating into it
+    leaves = {k: v.clone().requires_grad_(True) for k, v in src.items()}
+    bucket = GradBucket(leaves, bind_grads=True)
+    bucket.zero_grad()
+    for cams in shards:
+        out = GaussianRasterizerBatch([sets[c] for c in cams])(
+            means2D=torch.zeros(P, 3, device=DEV), label=label, **leaves)
+        torch.autograd.backward([out[0], out[3], out[2]], [up_c[cams], up_d[cams], up_f[cams]])
+    bucket.all_reduce()  # no process group: a no-op that checks the views
+    for k in full:
+        assert leaves[k].grad.data_ptr() == bucket._views[list(leaves).index(k)].data_ptr()
+        assert _rel(leaves[k].grad, full[k]) <= 1e-5, (k, _rel(leaves[k].grad, full[k]))
+
+
+def test_batch_sort_classes_with_long_and_short_cameras(P=20000, W=160, H=128):
+    """The batch merges the cameras' tile-sort class extents (gs_api.hip: max
+    of the long-class prefixes, min of the short-class one): a camera with
+    tiles longer than GS_SORT_SMALL (1024) and TS_CAP (3584) next to cameras
+    whose tiles are all short must still sort every list.  A dense cluster of
+    Gaussians just in front of camera 0 makes its long tiles; the batch's
+    outputs must be bit-identical to the per-camera calls."""
+    from tests import _harness as Hh
+    rig = camera_rig(27, W, H)
+    cams = [rig[0], rig[9], rig[18]]
+    sets = _settings(cams, W, H, "reference")
+    src = _scene(P, 8, False, seed=12)
+    c0 = cams[0]
+    fwd0 = torch.from_numpy(c0.viewmatrix[:3, 2].copy()).float().to(DEV)  # camera 0's viewing axis (w2c row 2)
+    pos0 = torch.from_numpy(c0.campos.copy()).float().to(DEV)
+    gen = torch.Generator(device=DEV).manual_seed(5)
+    n_cl = 12000
+    cl = pos0 + 0.6 * fwd0 + 0.01 * torch.randn(n_cl, 3, device=DEV, generator=gen)
+    means = src["means3D"].clone()
+    means[:n_cl] = cl
+    src["means3D"] = means
+    src["scales"] = src["scales"].clone()
+    src["scales"][:n_cl] = 0.004
+    label = torch.ones(P, device=DEV)
+    per = [GaussianRasterizer(s)(means2D=torch.zeros(P, 3, device=DEV), label=label, **src) for s in sets]
+    # precondition: camera 0 has tiles past both class limits, another camera has only short tiles
+    maxlen = []
+    for s in sets:
+        out = _C_forward(src, s)
+        st = Hh.export_state(P, W, H, out)
+        rg = st["ranges"].reshape(-1, 2).astype(np.int64)
+        maxlen.append(int((rg[:, 1] - rg[:, 0]).max()))
+    assert maxlen[0] > 3584, maxlen
+    assert min(maxlen[1:]) <= 1024, maxlen
+    bat = GaussianRasterizerBatch(sets)(means2D=torch.zeros(P, 3, device=DEV), label=label, **src)
+    for c in range(len(sets)):
+        for x, y in zip(per[c], bat):
+            assert torch.equal(x, y[c]), (c, maxlen)
+
+
+def _C_forward(src, s):
+    from dynamic3dgaussians_amd import _C
+    out = _C.rasterize_gaussians(
+        s.bg, src["means3D"], src["colors_precomp"], src.get("semantic_feature"), src["opacities"],
+        src["scales"], src["rotations"], 1.0, torch.Tensor([]), s.viewmatrix, s.projmatrix, s.c_x, s.c_y,
+        s.tanfovx, s.tanfovy, s.image_height, s.image_width, torch.Tensor([]), 0, s.campos, False, False)
+    torch.cuda.synchronize()
+    return out
