@@ -10,7 +10,7 @@ a missing library raise.
 
 Superset behaviour (documented in DESIGN.md "Boundary"):
   * semantic_feature may be None/empty (F = 0), [P, F] or [P, 1, F]; any F is
-    accepted and zero-padded to the next compiled width (0, 4, 8, 16, 32, 64).
+    accepted and zero-padded to the next compiled width (0, 4, 8, 16, 32, 36, 64).
   * keyword-only `compat` selects "reference" (as-shipped numerics, default)
     or "fixed" numerics; see DESIGN.md "Quirks".
 """

@@ -21,7 +21,7 @@ GS_FLAG_ACCUMULATE = 1  # include/gsplat_hip.h
 c_int32, c_int64, c_float, c_size_t = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_size_t
 
 GS_COMPAT = {"reference": 0, "fixed": 1}
-SUPPORTED_F = (0, 4, 8, 16, 32, 64)
+SUPPORTED_F = (0, 4, 8, 16, 32, 36, 64)
 
 
 class GsGaussians(ctypes.Structure):

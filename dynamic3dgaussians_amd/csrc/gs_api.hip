@@ -61,7 +61,7 @@ T* at(void* base, size_t off) { return reinterpret_cast<T*>(static_cast<char*>(b
 template <class T>
 const T* at(const void* base, size_t off) { return reinterpret_cast<const T*>(static_cast<const char*>(base) + off); }
 
-bool feature_supported(int F) { return F == 0 || F == 4 || F == 8 || F == 16 || F == 32 || F == 64; }
+bool feature_supported(int F) { return F == 0 || F == 4 || F == 8 || F == 16 || F == 32 || F == 36 || F == 64; }
 
 int check_gaussians(const gs_gaussians* g, const gs_camera* c, bool forward) {
   if (!g || !c) return fail(-1, "null argument block");
@@ -69,7 +69,7 @@ int check_gaussians(const gs_gaussians* g, const gs_camera* c, bool forward) {
   if (c->image_width <= 0 || c->image_height <= 0)
     return fail(-1, "image size must be positive (got %dx%d)", c->image_width, c->image_height);
   if (!feature_supported(g->F))
-    return fail(-1, "semantic feature width %d not instantiated (0, 4, 8, 16, 32, 64)", g->F);
+    return fail(-1, "semantic feature width %d not instantiated (0, 4, 8, 16, 32, 36, 64)", g->F);
   if (g->P > 0) {
     if (!g->means3D || (forward && !g->opacities)) return fail(-1, "means3D and opacities are required");
     if (!c->viewmatrix || !c->projmatrix || !c->campos || !c->background)
@@ -236,6 +236,17 @@ static int64_t batch_bin_offsets(int C, const int64_t* L, CamBatch* cb) {
     o += (int64_t)BinLayout(l).total;
   }
   return o;
+}
+
+// backward scratch: the per-camera accumulation records, then (feature widths
+// whose gradient rows are not 64-B multiples, F = 36) a padded-stride feature
+// gradient area
+static size_t acc_bytes(int64_t P, int32_t C) {
+  return align_up(sizeof(float) * (size_t)ACC_STRIDE * (size_t)(P > 0 ? P : 0) * (C > 0 ? C : 0), 256);
+}
+static size_t feat_pad_bytes(int64_t P, int32_t F) {
+  const int FS = feature_grad_stride(F);
+  return FS == F ? 0 : align_up(sizeof(float) * (size_t)FS * (size_t)(P > 0 ? P : 0), 256);
 }
 
 // ---------------------------------------------------------------- debug checks
@@ -408,7 +419,12 @@ static int render_impl(const gs_gaussians* g, const gs_camera* cams, int C, int 
   const float* rec = at<float>(geom, gl.rec);
   TileArgs ta = tile_args(P, W, H, geom, image);
   ta.binning = total > 0 ? binning : nullptr;
-  launch_tile_order(ta, cb, s);
+  {
+    // the dispatch order (longest list first) from the ranges: the stage the
+    // reference's identifyTileRanges occupies
+    StageTimer t(s, GS_STAGE_RANGES);
+    launch_tile_order(ta, cb, s);
+  }
   if (total > 0) {
     {
       StageTimer t(s, GS_STAGE_DUPLICATE);
@@ -468,8 +484,14 @@ static int backward_impl(const gs_gaussians* g, const gs_camera* cams, int C, co
   (void)hipMemsetAsync(acc, 0, sizeof(float) * (size_t)ACC_STRIDE * P * C, s);
   const bool accumulate = (g->flags & GS_FLAG_ACCUMULATE) != 0;
   // the blend kernel adds the feature gradients atomically: zero first unless
-  // the output already holds the sums to add to
-  if (g->F > 0 && !accumulate) (void)hipMemsetAsync(dL_dsemantic, 0, sizeof(float) * (size_t)g->F * P, s);
+  // the output already holds the sums to add to; a padded-stride width adds
+  // into a zeroed scratch, copied (added) into the output after the blend
+  float* dsem_pad = feat_pad_bytes(P, g->F) ? reinterpret_cast<float*>(static_cast<char*>(scratch) + acc_bytes(P, C))
+                                            : nullptr;
+  if (dsem_pad)
+    (void)hipMemsetAsync(dsem_pad, 0, feat_pad_bytes(P, g->F), s);
+  else if (g->F > 0 && !accumulate)
+    (void)hipMemsetAsync(dL_dsemantic, 0, sizeof(float) * (size_t)g->F * P, s);
   RenderBwdArgs ra{};
   ra.W = W; ra.H = H; ra.grid_x = gx; ra.num_tiles = gx * gy; ra.F = g->F; ra.compat = compat; ra.P = P;
   ra.order = at<uint4>(image, il.order);
@@ -482,10 +504,11 @@ static int backward_impl(const gs_gaussians* g, const gs_camera* cams, int C, co
   ra.alphas = alphas;
   ra.n_contrib = at<uint32_t>(image, il.n_contrib);
   ra.dL_dpix = dL_dout_color; ra.dL_dfeat = dL_dout_feature; ra.dL_ddepth = dL_dout_depth;
-  ra.dL_dalpha = dL_dout_alpha; ra.acc = acc; ra.dsem = dL_dsemantic;
+  ra.dL_dalpha = dL_dout_alpha; ra.acc = acc; ra.dsem = dsem_pad ? dsem_pad : dL_dsemantic;
   {
     StageTimer t(s, GS_STAGE_RENDER_BWD);
     if (!launch_render_bwd(ra, cb, s)) return fail(-1, "unsupported feature width %d", g->F);
+    if (dsem_pad) launch_feature_grad_rows(dsem_pad, dL_dsemantic, P, g->F, accumulate ? 1 : 0, s);
   }
   if (int e = check("render backward", debug, s)) return e;
   PreprocessBwdArgs b{};
@@ -549,8 +572,7 @@ size_t gs_batch_binning_buffer_bytes(int32_t C, const int64_t* num_instances) {
   return (size_t)batch_bin_offsets(C, num_instances, nullptr);
 }
 size_t gs_batch_backward_scratch_bytes(int64_t P, int32_t F, int32_t C) {
-  (void)F;
-  return align_up(sizeof(float) * (size_t)ACC_STRIDE * (size_t)(P > 0 ? P : 0) * (C > 0 ? C : 0), 256) + 256;
+  return acc_bytes(P, C) + feat_pad_bytes(P, F) + 256;
 }
 
 int gs_forward_plan_batch(const gs_gaussians* g, const gs_camera* cams, int32_t C, int prefiltered, int debug,

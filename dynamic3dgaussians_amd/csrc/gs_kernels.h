@@ -80,6 +80,16 @@ struct RenderArgs {
   uint32_t* n_contrib;
 };
 
+// Row stride (floats) of the feature gradients the backward blend adds into:
+// F when its 16-channel blocks are 64-B aligned (F % 16 == 0 or F < 16),
+// else F rounded up to 16 (F = 36 -> 48, through a scratch copy) -- float
+// atomics execute per 64-B segment, and a straddling 16-channel block costs
+// two requests.
+__host__ __device__ constexpr int feature_grad_stride(int F) {
+  return (F < 16 || F % 16 == 0) ? F : (F + 15) / 16 * 16;
+}
+void launch_feature_grad_rows(const float* pad, float* out, int64_t P, int F, int accumulate, hipStream_t s);
+
 struct RenderBwdArgs {
   int W, H, grid_x, num_tiles, F, compat, P;
   const uint4* order;  // num_tiles: dispatch records {tile, range.x, range.y, 0}, longest list first

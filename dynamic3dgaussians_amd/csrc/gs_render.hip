@@ -4,25 +4,33 @@
 // backward.cu:432-652 (renderCUDA backward).
 //
 // MI355X design:
-//  * A 16x16 binning tile is one 256-thread workgroup; each of its 4 waves
-//    owns a 16x4 pixel strip and walks the tile's depth-sorted list on its
-//    own -- no block barriers, every wave exits when its own pixels are done.
-//  * The list is consumed in chunks of 64: lane j gathers the 48-B render
-//    record of the chunk's j-th Gaussian (prefetched one chunk ahead), tests
-//    it against the wave's strip (the Gaussian's alpha >= 1/255 extent) and
-//    parks it in a wave-private LDS slot.  A ballot leaves the Gaussians the
-//    strip can see; the inner loop visits only those, reading each record
-//    back with broadcast ds_read_b128.  Culled Gaussians are exactly the ones
-//    every pixel of the strip skips in the reference loop.
-//  * Semantic features (F = 32/64) are a dense contraction and go to the fp32
-//    matrix cores (v_mfma_f32_32x32x2_f32, an exact k-ordered fma chain):
-//      forward   out_feat^T[ch][pix] += f[g][ch] * w[g][pix]  over Gaussian pairs
-//      backward  dL/df[g][ch]        += w[g][pix] * dL/dfeat[pix][ch] over 32-Gaussian batches
-//    Colour, depth and the geometric gradients stay on the VALU.
-//  * Backward per-Gaussian sums (mean2D, conic, opacity, colour, depth) are
-//    reduced over the wave with permlane32/16 swaps + DPP and committed with
-//    ONE atomic wave-instruction; feature gradients leave the MFMA
-//    accumulator as 2 x 128-B rows per atomic instruction.
+//  * A 16x16 binning tile is four 8x8 pixel strips (STRIP_W x STRIP_H,
+//    gs_common.h); one wave64 owns a strip (lane = pixel) and walks the
+//    tile's depth-sorted list on its own -- no block barriers, every wave
+//    exits when its own pixels are done.  The forward packs a tile's 4 waves
+//    into one workgroup (GS_WPB_FWD), the backward runs a wave per workgroup.
+//  * The list is consumed in chunks of 64: lane j gathers the 64-B render
+//    record (gs_common.h R_*) of the chunk's j-th Gaussian (prefetched one
+//    chunk ahead, ids two chunks ahead), tests it against the wave's strip
+//    (the Gaussian's alpha >= 1/255 extent) and parks it in a wave-private
+//    LDS slot.  A ballot leaves the Gaussians the strip can see; the inner
+//    loop visits only those, reading each record back with broadcast LDS
+//    reads.  Culled Gaussians are exactly the ones every pixel of the strip
+//    skips in the reference loop.
+//  * Colour, depth, transmittance and the blend decisions are fp32 on the
+//    VALU.  The dense per-Gaussian contractions go to the bf16 matrix cores
+//    with every fp32 operand split into 3 bf16 pieces (split_bf16: 6 piece
+//    products per product, <= 2^-26 relative, fp32 accumulation -- as exact
+//    as the reference's fp32 fma / atomicAdd, tests/test_gpu_envelope.py):
+//      forward   out_feat^T[ch][pix] += f[g][ch] * w[g][pix] over 16-Gaussian
+//                batches (v_mfma_f32_32x32x16_bf16), F = 32 k (+ a 4-channel
+//                VALU tail at F = 36);
+//      backward  per 16-Gaussian batch, contractions over the strip's 64
+//                pixels (v_mfma_f32_16x16x32_bf16): w = alpha T against
+//                dL/dC, dL/dD, dL/dF and u = G dL/dopacity against the pixel
+//                monomials {1, X, Y, X^2, XY, Y^2} (dL/dmean2D, dL/dconic).
+//  * Backward per-Gaussian sums are committed with float atomics per 64-B
+//    accumulation record (10 components) and per feature channel.
 #include "gs_common.h"
 #include "gs_kernels.h"
 
@@ -306,7 +314,7 @@ constexpr int fwd_waves_per_simd() {
 #ifdef GS_FWD_WPE
   return GS_FWD_WPE;
 #else
-  return F == 32 ? 4 : 1;
+  return (F == 32 || F == 36) ? 4 : 1;
 #endif
 }
 template <int F, int COMPAT>
@@ -328,16 +336,21 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
   float* __restrict__ out_depth = ca.out_depth;
   float* __restrict__ out_alpha = ca.out_alpha;
   uint32_t* __restrict__ n_contrib = ca.n_contrib;
-  // Features: 8 / 16 channels on the VALU (v_pk_fma_f32 with the Gaussian's
-  // row in SGPRs, requested at the top of the iteration); 32 / 64 channels on
+  // Features: 4 / 8 / 16 channels on the VALU (fma with the Gaussian's row
+  // in SGPRs, requested at the top of the iteration); 32-channel blocks on
   // the matrix cores: a wave parks the weights w = alpha T of 16 blending
   // Gaussians in LDS and contracts the batch as out_feature^T[ch][pix] +=
   // sum_g feat[g][ch] w[g][pix] (v_mfma_f32_32x32x16_bf16, K = Gaussians,
-  // bf16-split operands: 6 matrix instructions per 16 Gaussians and 32
-  // channels instead of 16 fp32 v_mfma_f32_32x32x2_f32).
-  constexpr bool MF = (F == 32 || F == 64);
+  // 3-piece bf16 split operands: 6 matrix instructions per 16 Gaussians and
+  // 32 channels, fp32-equivalent, instead of 8 fp32 v_mfma_f32_32x32x2_f32 at
+  // 64 cycles each).  F = 36 (32 + a 4-channel tail, e.g. the fused colour +
+  // seg pass's 3 seg channels next to 32 user channels) runs the tail on the
+  // VALU next to the one matrix block instead of padding to 64.
+  constexpr bool MF = (F >= 32);
   constexpr int FB = MF ? F / 32 : 1;        // 32-channel blocks
-  constexpr int NSF = (!MF && F > 0) ? F : 1;
+  constexpr int FT = MF ? F - 32 * FB : 0;   // VALU tail of a matrix-core width
+  static_assert(FT == 0 || FT == 4, "matrix-core feature widths: 32 k or 32 k + 4");
+  constexpr int NSF = (!MF && F > 0) ? F : (FT > 0 ? FT : 1);
   constexpr int WBF = 16;                    // Gaussians per matrix batch
   // per record: (x, y, -a/2, -b) (-c/2, opacity, r, g) (b, depth, -, -)
 #ifdef GS_FWD_DUMMY
@@ -472,7 +485,8 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
       // Two survivors per iteration: their exponents are evaluated side by
       // side (independent work for the issue slots), then blended in order.
       // A missing second survivor gets power = +1 (never blends).
-      auto blend_step = [&](int j, const float4& r1, const float4& r2, float power, float alpha) {
+      auto blend_step = [&](int j, const float4& r1, const float4& r2, float power, float alpha,
+                            const float4& ft) {
         const float test_T = T * (1 - alpha);
         const bool cand = live != 0u && !(power > 0.0f) && !(alpha < ALPHA_MIN);
         const bool fin = cand && test_T < 0.0001f;  // saturated: not blended, lane done
@@ -483,6 +497,12 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
         C1 = fmaf(r1.w, w, C1);
         C2 = fmaf(r2.x, w, C2);
         Dp = fmaf(r2.y, w, Dp);
+        if constexpr (FT > 0) {
+          SF[0] = fmaf(ft.x, w, SF[0]);
+          SF[1] = fmaf(ft.y, w, SF[1]);
+          SF[2] = fmaf(ft.z, w, SF[2]);
+          SF[3] = fmaf(ft.w, w, SF[3]);
+        }
         T = blend ? test_T : T;
         last = blend ? lbase + (uint32_t)j : last;
         if constexpr (MF) {
@@ -504,6 +524,15 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
 #endif
         if (two) mask &= mask - 1;
         STAT(3, two ? 2 : 1);
+        // the survivors' tail feature rows (scalar loads), requested before
+        // their alphas are computed
+        float4 fta = make_float4(0.f, 0.f, 0.f, 0.f), ftb = fta;
+        if constexpr (FT > 0) {
+          const uint32_t ga = __builtin_amdgcn_readlane(chunk_gid, ja);
+          const uint32_t gb = __builtin_amdgcn_readlane(chunk_gid, jb < CHUNK ? jb : ja);
+          fta = *reinterpret_cast<const float4*>(feats + (size_t)ga * F + 32 * FB);
+          ftb = *reinterpret_cast<const float4*>(feats + (size_t)gb * F + 32 * FB);
+        }
         const float4 a0 = s_rec[lw][ja][0], a1 = s_rec[lw][ja][1], a2 = s_rec[lw][ja][2];
         const float4 b0 = s_rec[lw][jb][0], b1 = s_rec[lw][jb][1], b2 = s_rec[lw][jb][2];
         const float pa = gauss_power(a0.x - pfx, a0.y - pfy, make_float4(a0.z, a0.w, a1.x, 0.f));
@@ -513,8 +542,8 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
 #endif
         const float ala = fminf(0.99f, a1.y * gauss_exp(pa));
         const float alb = fminf(0.99f, b1.y * gauss_exp(pb));
-        blend_step(ja, a1, a2, pa, ala);
-        blend_step(jb, b1, b2, pb, alb);
+        blend_step(ja, a1, a2, pa, ala, fta);
+        blend_step(jb, b1, b2, pb, alb, ftb);
         if constexpr (MF) {
           if (nb >= WBF) {  // 16 or 17 parked: contract 16, carry the 17th to slot 0
             flush(WBF);
@@ -537,10 +566,10 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
       // the survivor's feature row, requested before its alpha is computed so
       // the scalar loads overlap that work
       float fcur[NSF];
-      if constexpr (!MF && F > 0) {
+      if constexpr ((!MF && F > 0) || FT > 0) {
         const uint32_t g = __builtin_amdgcn_readlane(chunk_gid, j);
 #pragma unroll
-        for (int c = 0; c < NSF; ++c) fcur[c] = feats[(size_t)g * F + c];
+        for (int c = 0; c < NSF; ++c) fcur[c] = feats[(size_t)g * F + 32 * FB * (MF ? 1 : 0) + c];
       }
       STAT(3, 1);
       STAT_INC(st_it);
@@ -568,10 +597,14 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
       STAT(4, wave_any(blend));
       STAT(5, __builtin_popcountll(__ballot(blend)));
       STAT(18, wave_any(blend) && ((__ballot(blend) & 0xFFFFFFFFull) == 0 || (__ballot(blend) >> 32) == 0));
-      if constexpr (!MF && F > 0) {
+      if constexpr ((!MF && F > 0) || FT > 0) {
         // keep the row loads above the blend decision (issued early, used late)
 #pragma unroll
         for (int c = 0; c < NSF; ++c) asm volatile("" ::"s"(fcur[c]));
+      }
+      if constexpr (FT > 0) {
+#pragma unroll
+        for (int c = 0; c < FT; ++c) SF[c] = fmaf(fcur[c], w, SF[c]);
       }
       if (F > 0 && wave_any(blend)) {
         if constexpr (MF) {
@@ -617,6 +650,11 @@ blend_done:
         const float b = (COMPAT == COMPAT_REFERENCE && c < 3) ? bg[c] : 0.0f;
         out_feature[c * HW + pix] = SF[c] + T * b;
       }
+    }
+    if constexpr (FT > 0) {
+      // tail channels 32 FB .. (>= 3: no background in either mode)
+#pragma unroll
+      for (int c = 0; c < FT; ++c) out_feature[(size_t)(32 * FB + c) * HW + pix] = SF[c];
     }
     // Q1: the reference never writes out_alpha (torch::full -> 0 stays 0);
     // we store that 0 here instead of a separate fill launch.
@@ -693,17 +731,19 @@ blend_done:
 // A wave parks w and u of 16 contributing Gaussians in LDS and contracts the
 // batch on the matrix cores (v_mfma_f32_16x16x32_bf16, K = pixels) instead of
 // reducing each Gaussian's sums over the wave with cross-lane VALU work.
-// Operands are split into two bf16 (split_bf16; the monomials are exact, so
-// their products take two terms).
+// Operands are split into three bf16 (split_bf16: 6 piece products; the
+// monomials are exact in bf16, so their products take three).
 // Waves per SIMD the backward asks the register allocator for: 3 (<= 168
-// VGPRs) where that fits without spilling, measured 0.336 vs 0.388 ms at 2
-// waves on the bench camera (F = 32); the widest instantiations keep 2.
+// VGPRs) where that fits, measured 0.336 vs 0.388 ms at 2 waves on the bench
+// camera (F = 32); with the 3-piece split that needs the colour operand in
+// LDS and one k-step's split weights live at a time (flush), else 27-camera
+// render_bwd 6.0 ms at 2 waves vs 5.45 at 3; the widest instantiations keep 2.
 template <int F, int COMPAT>
 constexpr int bwd_waves_per_simd() {
 #ifdef GS_BWD_WPE
   return GS_BWD_WPE;
 #else
-  return (F < 32 || (F == 32 && COMPAT == COMPAT_REFERENCE)) ? 3 : 2;
+  return (F < 32 || ((F == 32 || F == 36) && COMPAT == COMPAT_REFERENCE)) ? 3 : 2;
 #endif
 }
 template <int F, int COMPAT>
@@ -731,18 +771,27 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
   constexpr int WB = 16;                      // Gaussians per matrix batch
   constexpr int CB = F >= 16 ? F / 16 : 0;    // 16-channel feature blocks with their own accumulators
   constexpr int CB1 = CB > 0 ? CB : 1;
-  constexpr int FW = F < 16 ? F : 0;          // feature rows 4.. of the colour block (F = 4, 8)
+  // feature channels 16 CB .. F as rows 4.. of the colour block (F = 4, 8,
+  // and the 4-channel tail of F = 36)
+  constexpr int FW = F - 16 * CB;
+  static_assert(FW <= 12, "the colour block holds at most 12 feature rows");
+  constexpr int NCOMP = A_FEAT + FW;  // committed components per Gaussian and batch
+  // row stride of the feature gradients the atomics add into: F, or a
+  // 64-B multiple when the 16-channel blocks would straddle segments
+  // (F = 36: the host hands a 48-wide scratch, feature_grad_rows copies out)
+  constexpr int FS = feature_grad_stride(F);
   constexpr bool FIXED_FEAT = (COMPAT != COMPAT_REFERENCE) && F > 0;
   // per record: (x, y, -a/2, -b) (-c/2, opacity, r, g) (b, depth, -, -)
   __shared__ float4 s_rec[GS_WPB_BWD][CHUNK][2];
   __shared__ float2 s_rec2[GS_WPB_BWD][CHUNK];  // (b, depth)
-  // Colour block operand rows 0..3 (dL/dC_r,g,b, dL/dD) of the strip, split,
-  // in the A layout: [k-step][piece][row][pixel group of 8].  Kept in LDS
-  // (1.5 KiB) rather than in 24 VGPRs when the colour block carries no
-  // feature rows (F = 0 or >= 16): every lane reads row (l&15)&3, so rows
-  // 4..15 of the colour sums hold copies nobody reads.
-  constexpr bool XW_LDS = (FW == 0);
-  __shared__ bf16x8 s_xw[GS_WPB_BWD][XW_LDS ? 2 : 1][NSP][4][4];
+  // Colour block operand rows 0..3 (dL/dC_r,g,b, dL/dD) and the FW <= 4
+  // feature rows after them, split, in the A layout: [k-step][piece][row]
+  // [pixel group of 8].  Kept in LDS (1.5 / 3 KiB) rather than in 24 VGPRs:
+  // every lane reads row (l&15) & (XR-1), so the rows past 4 + FW of the
+  // colour sums hold copies nobody reads.
+  constexpr bool XW_LDS = (FW <= 4);
+  constexpr int XR = FW == 0 ? 4 : 8;  // operand rows kept
+  __shared__ bf16x8 s_xw[GS_WPB_BWD][XW_LDS ? 2 : 1][NSP][XR][4];
   // batch weights [slot][pixel] (row pad 4: the operand reads are conflict-free)
   __shared__ float s_w[GS_WPB_BWD][WB][68];
   __shared__ float s_u[GS_WPB_BWD][WB][68];
@@ -808,7 +857,7 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
     if constexpr (XW_LDS) {
       bsplit t;
       split_bf16(x, t);
-      if ((lane & 15) < 4) {
+      if ((lane & 15) < XR) {
 #pragma unroll
         for (int i = 0; i < NSP; ++i) s_xw[lw][s][i][lane & 15][lane >> 4] = t.p[i];
       }
@@ -821,7 +870,7 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
     const float* src = nullptr;
     if (row < 3) src = dL_dpix ? dL_dpix + (size_t)row * HW : nullptr;
     else if (row == 3) src = dL_ddepth;
-    else if (row - 4 < FW) src = dL_dfeat ? dL_dfeat + (size_t)(row - 4) * HW : nullptr;
+    else if (row - 4 < FW) src = dL_dfeat ? dL_dfeat + (size_t)(16 * CB + row - 4) * HW : nullptr;
     // A lane's 8 pixels are one run of a strip row.  Fast path (the strip
     // lies inside the image, rows and planes 16-B aligned -- decided once per
     // wave): every operand row with two 16-B loads, all issued back to back
@@ -902,13 +951,16 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
     const int g = lane & 15;
     // every id the commits below need, read up front (independent LDS reads,
     // one wait) instead of one dependent read per atomic
-    uint32_t fgid[4], agid[(WB * A_FEAT + 63) / 64];
+    // (FW > 0: the component ids are read at the commit instead, fewer live
+    // registers)
+    constexpr int NAG = FW > 0 ? 1 : (WB * NCOMP + 63) / 64;
+    uint32_t fgid[4], agid[NAG];
 #pragma unroll
     for (int r = 0; r < 4; ++r) fgid[r] = f_bits(s_slot[lw][(lane >> 4) * 4 + r].w);
 #pragma unroll
-    for (int t = 0; t < (WB * A_FEAT + 63) / 64; ++t) {
+    for (int t = 0; t < NAG; ++t) {
       const int i = lane + 64 * t;
-      agid[t] = i < WB * A_FEAT ? f_bits(s_slot[lw][i / A_FEAT].w) : 0u;
+      agid[t] = (FW == 0 && i < WB * NCOMP) ? f_bits(s_slot[lw][i / NCOMP].w) : 0u;
     }
     // All sums of the batch first, one k-step (32 pixels) at a time, so that
     // only one k-step's split weights are live:
@@ -936,7 +988,7 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
         if constexpr (XW_LDS) {
           bsplit xw;
 #pragma unroll
-          for (int i = 0; i < NSP; ++i) xw.p[i] = s_xw[lw][s][i][lane & 3][(lane >> 4) & 3];
+          for (int i = 0; i < NSP; ++i) xw.p[i] = s_xw[lw][s][i][lane & (XR - 1)][(lane >> 4) & 3];
           cw = mfma_split(xw, Ws, cw);
         } else {
           cw = mfma_split(Xw[s], Ws, cw);
@@ -984,7 +1036,11 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
     // lanes 0..15 turn slot l's sums into its 10 accumulator components and
     // park them as [slot][component] in the batch's (consumed) u rows, so
     // that each atomic wave-instruction below adds whole 40-B component
-    // records (~7 cache lines) instead of one component of 16 Gaussians.
+    // records (~7 cache lines) instead of one component of 16 Gaussians; the
+    // FW feature rows of the colour block (lanes 16.., row (l>>4)*4 + r) ride
+    // along as components A_FEAT.. (their target is the feature gradient row,
+    // FW contiguous floats: one request per Gaussian instead of one per
+    // channel).
     float* s_out = &s_u[lw][0][0];
     if (lane < 16) {
       const float4 sl = s_slot[lw][lane];
@@ -995,7 +1051,7 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
       const float uxx = fmaf(mx, fmaf(mx, S1, -Sx), 0.25f * Sxx);
       const float uyy = fmaf(my, fmaf(my, S1, -Sy), 0.25f * s_yy);
       const float uxy = fmaf(mx, fmaf(my, S1, -0.5f * Sy), fmaf(-0.5f * my, Sx, 0.25f * s_xy));
-      float* o = s_out + A_FEAT * lane;
+      float* o = s_out + NCOMP * lane;
       o[A_MX] = op * ux;
       o[A_MY] = op * uy;
       o[A_CA] = op * uxx;
@@ -1007,31 +1063,31 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
       o[A_B] = cw[2];
       o[A_DEPTH] = cw[3];
     }
+    if constexpr (FW > 0) {
+      if (lane >= 16) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int ch = (lane >> 4) * 4 + r - 4;
+          if (ch < FW) s_out[NCOMP * g + A_FEAT + ch] = cw[r];
+        }
+      }
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
-    for (int t = 0; t < (WB * A_FEAT + 63) / 64; ++t) {
+    for (int t = 0; t < (WB * NCOMP + 63) / 64; ++t) {
       const int i = lane + 64 * t;
-      if (i >= WB * A_FEAT) break;
-      const int slot = i / A_FEAT;
-      const uint32_t gi = agid[t];
+      if (i >= WB * NCOMP) break;
+      const int slot = i / NCOMP, comp = i - NCOMP * slot;
+      const uint32_t gi = FW > 0 ? f_bits(s_slot[lw][slot].w) : agid[t < NAG ? t : 0];
+      float* dst = comp < A_FEAT ? acc + (size_t)ACC_STRIDE * gi + comp
+                                 : dsem + (size_t)gi * FS + 16 * CB + (comp - A_FEAT);
 #ifdef GS_EXP_NO_ACC_ATOMIC
-      if (slot < nb && s_out[i] == 12345.f) acc[(size_t)ACC_STRIDE * gi + (i - A_FEAT * slot)] = 0.f;
+      if (slot < nb && s_out[i] == 12345.f) *dst = 0.f;
 #else
-      if (slot < nb) atomicAdd(acc + (size_t)ACC_STRIDE * gi + (i - A_FEAT * slot), s_out[i]);
+      if (slot < nb) atomicAdd(dst, s_out[i]);
 #endif
-    }
-    if constexpr (FW > 0) {
-      // rows 4 .. 4+FW of the colour block: lanes 16..47, row (l>>4)*4 + r
-      if (lane >= 16 && g < nb) {
-        const uint32_t gid = f_bits(s_slot[lw][g].w);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int ch = (lane >> 4) * 4 + r - 4;
-          if (ch < FW) atomicAdd(dsem + (size_t)gid * F + ch, cw[r]);
-        }
-      }
     }
     // features: C[slot][ch] = sum_p w[slot][p] dL/dF[p][ch]; lane l holds
     // channel 16cb + (l&15) of slots (l>>4)*4 + r
@@ -1042,9 +1098,9 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
         const int slot = (lane >> 4) * 4 + r;
         const uint32_t gi = fgid[r];
 #ifdef GS_EXP_NO_FEAT_ATOMIC
-        if (slot < nb && cf[cb][r] == 12345.f) dsem[(size_t)gi * F + 16 * cb + g] = 0.f;
+        if (slot < nb && cf[cb][r] == 12345.f) dsem[(size_t)gi * FS + 16 * cb + g] = 0.f;
 #else
-        if (slot < nb) atomicAdd(dsem + (size_t)gi * F + 16 * cb + g, cf[cb][r]);
+        if (slot < nb) atomicAdd(dsem + (size_t)gi * FS + 16 * cb + g, cf[cb][r]);
 #endif
       }
     }
@@ -1181,6 +1237,24 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
 
 // ------------------------------------------------------------------ dispatch
 
+// Feature gradients of a padded-stride scratch (F = 36: rows of 48) into the
+// caller's P x F rows: out = (accumulate ? out : 0) + scratch, coalesced on
+// the output.
+__global__ __launch_bounds__(256) void feature_grad_rows_kernel(const float* __restrict__ pad, float* __restrict__ out,
+                                                                int64_t n, int F, int FS, int accumulate) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int64_t g = i / F, c = i - g * F;
+  const float v = pad[g * FS + c];
+  out[i] = accumulate ? out[i] + v : v;
+}
+void launch_feature_grad_rows(const float* pad, float* out, int64_t P, int F, int accumulate, hipStream_t s) {
+  const int64_t n = P * (int64_t)F;
+  if (n <= 0) return;
+  hipLaunchKernelGGL(feature_grad_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, pad, out, n, F,
+                     feature_grad_stride(F), accumulate);
+}
+
 template <int F>
 static void fwd_f(const RenderArgs& a, const CamBatch& cb, hipStream_t s) {
   dim3 grid(a.num_tiles * (4 / GS_WPB_FWD) * cb.C), block(64 * GS_WPB_FWD);
@@ -1212,6 +1286,7 @@ bool launch_render_fwd(const RenderArgs& a, const CamBatch& cb, hipStream_t s) {
     case 8: fwd_f<8>(a, cb, s); return true;
     case 16: fwd_f<16>(a, cb, s); return true;
     case 32: fwd_f<32>(a, cb, s); return true;
+    case 36: fwd_f<36>(a, cb, s); return true;
     case 64: fwd_f<64>(a, cb, s); return true;
     default: return false;
   }
@@ -1225,6 +1300,7 @@ bool launch_render_bwd(const RenderBwdArgs& a, const CamBatch& cb, hipStream_t s
     case 8: bwd_f<8>(a, cb, s); return true;
     case 16: bwd_f<16>(a, cb, s); return true;
     case 32: bwd_f<32>(a, cb, s); return true;
+    case 36: bwd_f<36>(a, cb, s); return true;
     case 64: bwd_f<64>(a, cb, s); return true;
     default: return false;
   }

@@ -12,19 +12,26 @@
 //     instances of a contiguous slice of the Gaussians over the tiles in LDS
 //     and write one row of a [block][tile] count matrix (contiguous);
 //     (tile_rowscan_kernel) turns every tile column into per-block offsets
-//     inside the tile and a tile total; (tile_offsets_kernel, one workgroup) scans
-//     the totals into ranges[tile], finds the longest tile and lists tiles
-//     too long for the LDS sort.  Its header {L, max length, #long tiles}
-//     is the one device->host read of the forward (the reference's
-//     num_rendered read, :287).
+//     inside the tile and a tile total; (tile_offsets_kernel, one workgroup)
+//     scans the totals into ranges[tile] and writes the 8-word plan header
+//     {L, longest tile, the reference's num_rendered, status, sort-class
+//     prefixes P1, Q1, P2, -} -- the one device->host read of the forward
+//     (the reference's num_rendered read, :287).
 //  2. bucket (tile_hist_kernel<WRITE>): the same walk, each instance taking
 //     a slot from an LDS cursor, writes a 64-bit (depth bits << 32 | id) key
 //     into its tile's segment -- the order inside a segment is arbitrary.
 //  3. sort   (tile_sort_kernel): one workgroup per tile sorts its segment by
-//     depth bits with an LDS radix sort (wave-owned quarters, ballot-matched
-//     stable scatter, skipped constant-digit passes) and orders equal depths
-//     by id -- exactly the reference's stable order -- then writes the ids.
-//     Tiles longer than the LDS capacity run the same sort in global memory.
+//     the full key.  Common case, an MSD bucket sort: the top bits of the
+//     tile's depth-bit span pick one of 1,024 buckets (LDS atomics give each
+//     key its slot), one scan, one scatter, then every thread insertion-sorts
+//     its contiguous run of buckets by the full key.  Tiles whose keys crowd
+//     into few buckets fall back to an LSD radix sort (wave-owned quarters,
+//     ballot-matched stable scatter, skipped constant-digit passes, equal
+//     depths ordered by id).  Keys are unique, so either way the list is
+//     exactly the reference's stable order.  Length classes (short / up to
+//     TS_CAP in LDS / up to TS_CAP_LONG in a one-per-CU launch / beyond in
+//     global memory) run as separate launches over their prefix of the
+//     longest-first dispatch order (P1, Q1, P2 in the header).
 // Integer work, HBM- and latency-bound; 5 launches instead of the
 // reference's scan + 6-pass 64-bit radix sort + ranges.
 #include "gs_common.h"

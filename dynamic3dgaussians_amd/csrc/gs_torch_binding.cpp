@@ -24,7 +24,7 @@ namespace {
 using at::Tensor;
 using OptT = c10::optional<Tensor>;
 
-const int kSupportedF[] = {0, 4, 8, 16, 32, 64};
+const int kSupportedF[] = {0, 4, 8, 16, 32, 36, 64};
 
 bool present(const OptT& t) { return t.has_value() && t->defined() && t->numel() > 0; }
 

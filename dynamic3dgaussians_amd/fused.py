@@ -7,11 +7,20 @@ The reference training step rasterizes every camera twice: once for colour
 colours ride along as 3 extra feature channels of the colour pass -- one
 projection, one binning, one blend -- and come back as the seg image.
 
-In the reference numerics (compat="reference") the feature channels receive
-the background exactly like colour (`CR/forward.cu:398-404`, Q4: bg[ch] for
-ch < 3), and the blend adds w * feature with the same fp32 fma as colour, so
-the fused seg image is bit-identical to the reference's second render
-(`tests/test_gpu_parity.py::test_fused_colour_seg_matches_two_passes`).
+Channel layout.  Without caller features the seg colours are the feature
+channels themselves (F = 3, padded to the 4-wide kernel): in reference
+numerics features 0..2 receive the background exactly like colour
+(`CR/forward.cu:398-404`, Q4: bg[ch] for ch < 3) and the blend adds
+w * feature with the same fp32 fma chain as colour, so the fused seg image is
+bit-identical to the reference's second render
+(`tests/test_gpu_fused.py::test_fused_colour_seg_matches_two_passes`).  With
+the caller's F semantic channels the layout is [features (F), seg (3), ones
+(1)]: the caller's channels keep their indices, hence the Q4 background of
+channels 0..2 exactly as the plain colour render's feature map has it, and at
+F = 32 the pass is the F = 36 instantiation (32 matrix-core channels + a
+4-channel VALU tail: seg and ones) instead of a padded 64.  The ones channel
+renders sum(w) = 1 - T, which gives the seg channels their background term
+T * bg in reference numerics (where the alpha output is never written, Q1).
 
 Gradients.  dL/dseg_colors is the same per-Gaussian sum of w * dL/dseg as
 the second pass's dL/dcolors_precomp.  Geometry: in reference numerics the
@@ -49,21 +58,29 @@ def render_colour_and_seg(raster_settings, means3D: torch.Tensor, means2D: torch
     """
     if seg_colors.dim() != 2 or seg_colors.size(1) != 3:
         raise ValueError("seg_colors must be [P, 3]")
-    F_user = 0 if semantic_feature is None else semantic_feature.reshape(means3D.size(0), -1).size(1)
+    P = means3D.size(0)
+    F_user = 0 if semantic_feature is None else semantic_feature.reshape(P, -1).size(1)
     if F_user:
-        # the seg channels go first so that they get the background (ch < 3)
-        feats = torch.cat([seg_colors, semantic_feature.reshape(means3D.size(0), -1)], dim=1)
+        # [caller's features, seg, ones]: the caller's channels keep their
+        # indices (and Q4 background); the ones channel renders 1 - T
+        ones = torch.ones(P, 1, device=seg_colors.device, dtype=seg_colors.dtype)
+        feats = torch.cat([semantic_feature.reshape(P, -1), seg_colors, ones], dim=1)
     else:
-        feats = seg_colors
+        feats = seg_colors  # channels 0..2: the reference's background (Q4)
     ras = GaussianRasterizer(raster_settings)
     lab = label if label is not None else torch.ones(means3D.size(0), device=means3D.device)
     color, radii, feature_map, depth, alpha = ras(
         means3D=means3D, means2D=means2D, opacities=opacities, shs=shs, colors_precomp=colors_precomp,
         semantic_feature=feats, scales=scales, rotations=rotations, cov3D_precomp=cov3D_precomp, label=lab)
-    seg = feature_map[:3]
     compat = getattr(raster_settings, "compat", None) or _default_compat()
-    if compat != "reference":
-        seg = seg + (1.0 - alpha) * raster_settings.bg.reshape(3, 1, 1)
+    bg = raster_settings.bg.reshape(3, 1, 1)
     if F_user:
-        return color, radii, depth, seg, feature_map[3:]
+        seg = feature_map[F_user:F_user + 3]
+        # T * bg: T = 1 - alpha (fixed numerics write alpha) or 1 - sum(w)
+        cover = alpha if compat != "reference" else feature_map[F_user + 3:F_user + 4]
+        seg = seg + (1.0 - cover) * bg
+        return color, radii, depth, seg, feature_map[:F_user]
+    seg = feature_map[:3]
+    if compat != "reference":
+        seg = seg + (1.0 - alpha) * bg
     return color, radii, depth, seg

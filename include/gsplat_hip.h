@@ -177,7 +177,15 @@ int gs_backward(const gs_gaussians *g, const gs_camera *cam, const int32_t *radi
  *    positional semantics as for the single-camera calls (Q2 included).
  *  - State buffers: gs_batch_*_bytes; radii C x P; images C x (3|F|1|1) x H x W.
  *  - num_instances[C] from the plan is passed back to the render and the
- *    backward (each camera's binning buffer has its own length). */
+ *    backward (each camera's binning buffer has its own length).
+ *  - Memory: the state scales with C.  Geometry 121 B x P per camera (the
+ *    64-B render record, 24-B covariance, rect, counts); backward scratch
+ *    64 B x P per camera (one accumulation record per Gaussian and camera,
+ *    zero-filled by every backward; + 4 B x 48 x P at F = 36); binning
+ *    24 B per tile instance.  At P = 300k, C = 27 the scratch is 518 MB and
+ *    the fill ~0.1 ms per step; at P = 1M, C = 64 it is 4.1 GB -- split
+ *    larger rigs into camera groups of one batch call each (the gradients
+ *    of successive calls add with GS_FLAG_ACCUMULATE). */
 size_t gs_batch_geom_buffer_bytes(int64_t P, int32_t C);
 size_t gs_batch_image_buffer_bytes(int32_t W, int32_t H, int32_t C);
 size_t gs_batch_binning_buffer_bytes(int32_t C, const int64_t *num_instances);

@@ -1,15 +1,19 @@
 """GPU parity: the HIP rasterizer (through the C ABI) against the CPU oracle.
 
-Tolerances (DESIGN.md "Parity"):
+Tolerances (DESIGN.md section 5 has the measured errors):
   * integer/index work (tile counts, sorted point lists, tile ranges, radii,
     the radix sort, the wave reduction on integer data): bit-exact;
   * preprocess floats (means2D, depths, conics, SH colours): bit-exact -- both
     sides are strict IEEE fp32 in the same operation order;
-  * rendered images: PSNR(HIP vs oracle) >= 80 dB, >= 99.9 % of pixels within
-    1e-4 absolute, and n_contrib identical for >= 99.9 % of pixels (the blend
-    uses FMA contraction and a different expf, so an alpha-threshold decision
-    may flip on a rare pixel);
-  * gradients: relative L2 over all Gaussians <= 1e-3 per output tensor.
+  * rendered images: PSNR(HIP vs oracle) >= 80 dB and >= 99.9 % of pixels
+    within 1e-5 absolute on colour, feature (and alpha) channels, depth within
+    1e-5 relative to the depth range; n_contrib identical for >= 99.9 % of
+    pixels (the blend's exp is v_exp_f32, not libm expf, so an
+    alpha-threshold decision may flip on a rare pixel).  Measured: colour
+    <= 4.8e-7, features <= 2.9e-6 (3-piece bf16 split contractions);
+  * gradients: relative L2 over all Gaussians <= 1e-4 per output tensor
+    (measured <= 2.1e-5, typically ~1e-6), and -- test_gpu_envelope -- within
+    10x the oracle's own fp32 summation-order spread in reference mode.
 """
 import numpy as np
 import pytest
@@ -31,12 +35,12 @@ def _cmp_forward(inp, compat, F):
     assert Lg == Lo, "num_rendered differs"
     np.testing.assert_array_equal(rg, ro)
     assert H.psnr(cg, co) >= 80.0
-    assert np.mean(np.abs(cg - co) <= 1e-4) >= 0.999
-    assert np.mean(np.abs(dg - do) <= 1e-4 * max(1.0, np.abs(do).max())) >= 0.999
+    assert np.mean(np.abs(cg - co) <= 1e-5) >= 0.999
+    assert np.mean(np.abs(dg - do) <= 1e-5 * max(1.0, np.abs(do).max())) >= 0.999
     if F:
         assert fg.shape == fo.shape
-        assert np.mean(np.abs(fg - fo) <= 1e-4 * max(1.0, np.abs(fo).max())) >= 0.999
-    assert np.mean(np.abs(ag - ao) <= 1e-4) >= 0.999
+        assert np.mean(np.abs(fg - fo) <= 1e-5) >= 0.999
+    assert np.mean(np.abs(ag - ao) <= 1e-5) >= 0.999
     return g, o
 
 
@@ -167,7 +171,7 @@ def test_forward_padded_feature_width():
     g = H.gpu_forward(inp)
     o = H.oracle_forward(inp)
     assert g[2].shape == (5, 96, 128)
-    np.testing.assert_allclose(g[2].cpu().numpy(), o[2], atol=2e-4, rtol=0)
+    np.testing.assert_allclose(g[2].cpu().numpy(), o[2], atol=1e-5, rtol=0)
 
 
 # ---------------------------------------------------------------- backward
@@ -194,7 +198,7 @@ def test_backward_parity(compat, kw):
         if b.size == 0 or not np.any(b):
             assert not np.any(a) or np.abs(a).max() < 1e-6, name
             continue
-        assert H.rel_l2(a, b) <= 1e-3, (name, H.rel_l2(a, b))
+        assert H.rel_l2(a, b) <= 1e-4, (name, H.rel_l2(a, b))
 
 
 def test_backward_reference_swap_matters():
@@ -207,7 +211,7 @@ def test_backward_reference_swap_matters():
     a = H.gpu_backward(inp, g, grads, "reference", swap=True)
     b = H.oracle_backward(inp, o, grads, "reference", swap=True)
     c = H.gpu_backward(inp, g, grads, "reference", swap=False)
-    assert H.rel_l2(a[7], b[7]) <= 1e-3
+    assert H.rel_l2(a[7], b[7]) <= 1e-4
     assert H.rel_l2(a[7], c[7]) > 0.1
 
 
@@ -349,14 +353,16 @@ def test_absent_upstream_gradients_are_zeros():
 
 
 
-def test_native_binding_matches_ctypes_binding():
+@pytest.mark.parametrize("F,Fp", [(20, 32), (35, 36)])
+def test_native_binding_matches_ctypes_binding(F, Fp):
     """The C++ fast path (lib/_gs_native.so) and the ctypes binding drive the
     same C ABI: identical forward outputs, and the same gradients (label mask,
-    padded feature width, SH, caller buffers with the accumulate flag)."""
+    padded feature width -- 35 -> 36 takes the padded-stride feature gradient
+    scratch -- SH, caller buffers with the accumulate flag)."""
     from dynamic3dgaussians_amd import _C as C
     assert C.native_loaded()
-    inp = H.scene(P=3000, F=20, sh_degree=2, use_sh=True, W=96, H=80)
-    grads = H.upstream_grads(80, 96, 20)
+    inp = H.scene(P=3000, F=F, sh_degree=2, use_sh=True, W=96, H=80)
+    grads = H.upstream_grads(80, 96, F)
     mask = torch.from_numpy((np.arange(3000) % 3 != 0).astype(np.float32)).to(H.DEV)
     res = {}
     keep = C._native
@@ -373,7 +379,7 @@ def test_native_binding_matches_ctypes_binding():
                     d("projmatrix"), *H.bwd_cam4(inp, True), dc, df, dd, da, d("sh"), inp["degree"],
                     d("campos"), geom, num_rendered, binning, img, alpha, False)
             b = C.rasterize_gaussians_backward(*args, grad_mask=mask)
-            bufs = C.backward_buffers(3000, 32, inp["sh"].shape[1], H.DEV)
+            bufs = C.backward_buffers(3000, Fp, inp["sh"].shape[1], H.DEV)
             C.rasterize_gaussians_backward(*args, grad_mask=mask, out=bufs)
             C.rasterize_gaussians_backward(*args, grad_mask=mask, out=bufs, accumulate=True)
             torch.cuda.synchronize()
@@ -391,3 +397,18 @@ def test_native_binding_matches_ctypes_binding():
         assert H.rel_l2(xa[k], xb[k]) <= 1e-5 or np.abs(xb[k]).max() == 0, k
     # the accumulated buffers hold twice the single call's gradients
     assert H.rel_l2(xa["dmeans3D"], 2 * ba[4]) <= 1e-5
+
+
+def test_debug_mode_validates_and_passes_on_a_valid_scene():
+    """debug=True: the forward checks its plan header, ranges and list ids on
+    the host (gs_check_*, gsplat_hip.h) before the blend; a valid scene
+    passes and renders exactly what the non-debug call renders."""
+    inp = H.scene(P=3000, F=8)
+    a = _C.rasterize_gaussians(*H.fwd_args(inp, H.DEV))
+    args = H.fwd_args(inp, H.DEV)
+    args[-1] = True  # debug
+    b = _C.rasterize_gaussians(*args)
+    torch.cuda.synchronize()
+    assert a[0] == b[0]
+    for x, y in zip(a[1:6], b[1:6]):
+        assert torch.equal(x, y)

@@ -1,8 +1,39 @@
+# Round evidence of the current tree on one MI355X, one command:
+#   1. PMC passes of the 27-camera batch launches (gpu_pmc.sh) -> profiles/pmc_*.json
+#      (read by bench.py's roofline.traffic / issue / atomics)
+#   2. the GPU suite and smoke()
+#   3. the default bench line (CPU baselines included)
+#   4. rocprofv3 --kernel-trace --stats of the same bench command
+#   5. a two-rank rehearsal of bench.py's distributed path on the one GPU
+#      (gloo): the weak headline + the 27-camera split step, and --cams-total 27
+# Outputs in gpurun_out/$TAG.
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd $R
-timeout -k 10 600 python -m pytest tests -m gpu -q --timeout 300 -p no:cacheprovider > gpurun_out/t2.log 2>&1; echo "tests exit $?" >> gpurun_out/t2.log
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit 1
-timeout -k 10 600 python bench.py > gpurun_out/bench1.json 2> gpurun_out/bench1.err || exit 2
+TAG=${TAG:-round}
+O=$R/gpurun_out/$TAG
+mkdir -p $O
+if [ "${SKIP_PMC:-0}" != "1" ]; then
+timeout -k 10 600 bash tools/gpu_pmc.sh > $O/pmc.log 2>&1 || { echo "pmc failed"; tail -20 $O/pmc.log; exit 1; }
+cp profiles/pmc_traffic.json profiles/pmc_valu.json profiles/pmc_atomic.json $O/
+tail -3 $O/pmc.log
+fi
+cd $R
+if [ "${SKIP_TESTS:-0}" != "1" ]; then
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/tests.log 2>&1 || { echo "tests failed"; tail -40 $O/tests.log; exit 2; }
+tail -2 $O/tests.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { cat $O/smoke.log; exit 3; }
+tail -1 $O/smoke.log
+fi
+timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err || { tail $O/bench.err; exit 4; }
+cat $O/bench.json
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof1 -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --steps 3 --warmup 1 > $R/gpurun_out/bench_prof.json 2> $R/gpurun_out/bench_prof.err || exit 3
+rm -rf $O/bprof
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/bprof -o bench --output-format csv -- python3 $R/bench.py --no-cpu-baseline > $O/bench_under_rocprof.json 2> $O/bprof.err || exit 5
+cat $O/bench_under_rocprof.json
+cd $R
+if [ "${SKIP_DIST:-0}" != "1" ]; then
+GS_BENCH_BACKEND=gloo GS_BENCH_SHARE_GPU=1 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 > $O/dist2_weak.json 2> $O/dist2_weak.err || { tail $O/dist2_weak.err; exit 6; }
+GS_BENCH_BACKEND=gloo GS_BENCH_SHARE_GPU=1 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 2 --steps 3 --warmup 1 --cams-total 27 > $O/dist2_strong.json 2> $O/dist2_strong.err || { tail $O/dist2_strong.err; exit 7; }
+cat $O/dist2_weak.json $O/dist2_strong.json
+fi
