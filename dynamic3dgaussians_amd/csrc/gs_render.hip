@@ -314,7 +314,7 @@ constexpr int fwd_waves_per_simd() {
 #ifdef GS_FWD_WPE
   return GS_FWD_WPE;
 #else
-  return (F == 32 || F == 36) ? 4 : 1;
+  return F == 32 ? 4 : F == 36 ? 3 : 1;  // F = 36: 0.188 vs 0.205 ms per camera at 4 (spills)
 #endif
 }
 template <int F, int COMPAT>
@@ -717,6 +717,10 @@ blend_done:
 }
 
 // ------------------------------------------------------------------ backward
+
+// s_w / s_u element (row r, column c) of a 64-float row: the 16-B group index
+// XOR-swizzled by the row
+__device__ inline int sw_idx(int r, int c) { return r * 64 + ((((c >> 2) ^ r) & 15) << 2) + (c & 3); }
 //
 // Every per-Gaussian sum of the backward is a contraction over the wave's 64
 // pixels of one of two per-(Gaussian, pixel) weights with per-pixel
@@ -743,7 +747,7 @@ constexpr int bwd_waves_per_simd() {
 #ifdef GS_BWD_WPE
   return GS_BWD_WPE;
 #else
-  return (F < 32 || ((F == 32 || F == 36) && COMPAT == COMPAT_REFERENCE)) ? 3 : 2;
+  return (F < 32 || (F == 32 && COMPAT == COMPAT_REFERENCE)) ? 3 : 2;
 #endif
 }
 template <int F, int COMPAT>
@@ -792,9 +796,11 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
   constexpr bool XW_LDS = (FW <= 4);
   constexpr int XR = FW == 0 ? 4 : 8;  // operand rows kept
   __shared__ bf16x8 s_xw[GS_WPB_BWD][XW_LDS ? 2 : 1][NSP][XR][4];
-  // batch weights [slot][pixel] (row pad 4: the operand reads are conflict-free)
-  __shared__ float s_w[GS_WPB_BWD][WB][68];
-  __shared__ float s_u[GS_WPB_BWD][WB][68];
+  // batch weights [slot][pixel]: 64-float rows, 16-B groups XOR-swizzled by
+  // the row (sw_idx) so that the flush's 16-row operand reads and the
+  // per-lane writes are both conflict-free without padding
+  __shared__ float s_w[GS_WPB_BWD][WB * 64];
+  __shared__ float s_u[GS_WPB_BWD][WB * 64];
   __shared__ float4 s_slot[GS_WPB_BWD][WB];  // (mean x - cx, mean y - cy, opacity, id bits)
 
   // strip item = tile * 4 + wave (dispatch order, see strip_item)
@@ -980,8 +986,8 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
         bsplit Ws;
         {
           float x[8];
-          const float4 a0 = *reinterpret_cast<const float4*>(&s_w[lw][g][p0]);
-          const float4 a1 = *reinterpret_cast<const float4*>(&s_w[lw][g][p0 + 4]);
+          const float4 a0 = *reinterpret_cast<const float4*>(&s_w[lw][sw_idx(g, p0)]);
+          const float4 a1 = *reinterpret_cast<const float4*>(&s_w[lw][sw_idx(g, p0 + 4)]);
           x[0] = a0.x; x[1] = a0.y; x[2] = a0.z; x[3] = a0.w; x[4] = a1.x; x[5] = a1.y; x[6] = a1.z; x[7] = a1.w;
           split_bf16(x, Ws);
         }
@@ -1002,8 +1008,8 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
       bsplit Us;
       {
         float y[8];
-        const float4 b0 = *reinterpret_cast<const float4*>(&s_u[lw][g][p0]);
-        const float4 b1 = *reinterpret_cast<const float4*>(&s_u[lw][g][p0 + 4]);
+        const float4 b0 = *reinterpret_cast<const float4*>(&s_u[lw][sw_idx(g, p0)]);
+        const float4 b1 = *reinterpret_cast<const float4*>(&s_u[lw][sw_idx(g, p0 + 4)]);
         y[0] = b0.x; y[1] = b0.y; y[2] = b0.z; y[3] = b0.w; y[4] = b1.x; y[5] = b1.y; y[6] = b1.z; y[7] = b1.w;
         split_bf16(y, Us);
       }
@@ -1041,7 +1047,7 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
     // along as components A_FEAT.. (their target is the feature gradient row,
     // FW contiguous floats: one request per Gaussian instead of one per
     // channel).
-    float* s_out = &s_u[lw][0][0];
+    float* s_out = &s_u[lw][0];
     if (lane < 16) {
       const float4 sl = s_slot[lw][lane];
       const float mx = sl.x, my = sl.y, op = sl.z;
@@ -1212,8 +1218,8 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
         la = alpha;
         u = G * dL_dopa;
       }
-      s_w[lw][nb][lane] = w;
-      s_u[lw][nb][lane] = u;
+      s_w[lw][sw_idx(nb, lane)] = w;
+      s_u[lw][sw_idx(nb, lane)] = u;
       if (lane == 0)
         s_slot[lw][nb] = make_float4(r0.x - cx, r0.y - cy, op, bits_f(__builtin_amdgcn_readlane(chunk_gid, j)));
       if (++nb == WB) {
