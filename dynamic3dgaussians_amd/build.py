@@ -47,7 +47,10 @@ VARIANT_FLAGS = {"": [], "stats": ["-DGS_STATS"], "stamps": ["-DGS_STAMPS"], "st
                  "exp_fdummy": ["-DGS_FWD_DUMMY"], "exp_fdummy_ulw": ["-DGS_FWD_DUMMY", "-DGS_FWD_ULW", "-DGS_FWD_SLAST"],
                  "exp_pb1": ["-DGS_PBWD_GROUP=1"], "exp_pb3": ["-DGS_PBWD_GROUP=3"],
                  "exp_mid512": ["-DGS_SORT_MID512"], "exp_rs256": ["-DGS_RS_THREADS=256"],
-                 "exp_split2": ["-DGS_SPLIT_PIECES=2"], "exp_bwd_wpe2": ["-DGS_BWD_WPE=2"], "exp_fwd_wpe3": ["-DGS_FWD_WPE=3"]}
+                 "exp_split2": ["-DGS_SPLIT_PIECES=2"], "exp_bwd_wpe2": ["-DGS_BWD_WPE=2"], "exp_fwd_wpe3": ["-DGS_FWD_WPE=3"],
+                 "exp_fwd_noflush": ["-DGS_EXP_FWD_NO_FLUSH"], "exp_bwd_nomfma": ["-DGS_EXP_BWD_NO_MFMA"],
+                 "exp_noatomic_nomfma": ["-DGS_EXP_NO_FEAT_ATOMIC", "-DGS_EXP_NO_ACC_ATOMIC", "-DGS_EXP_BWD_NO_MFMA"],
+                 "exp_fwd_dma": ["-DGS_FWD_DMA"]}
 ARCH = os.environ.get("GSPLAT_OFFLOAD_ARCH", "gfx950")
 
 # Per-file flags.  The preprocess kernels are compiled without FMA

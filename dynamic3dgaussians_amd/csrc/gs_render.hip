@@ -362,6 +362,16 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
 #endif
   // batch weights [slot][pixel] (row pad 4: conflict-free writes and reads)
   __shared__ float s_fw[GS_WPB_FWD][MF ? WBF + 1 : 1][68];  // +1: a pair may overfill by one
+#ifdef GS_FWD_DMA
+  // Experiment (measured, not kept: render_fwd 3.50 vs 3.42 ms per 27-camera
+  // launch, profiles/r03m_ab_fwd_dma.log): the batch Gaussians' feature rows
+  // copied global -> LDS by an LDS-DMA (global_load_lds_dword) the moment a
+  // Gaussian is parked, instead of the gather at the flush.
+  constexpr bool FDMA = MF;
+#else
+  constexpr bool FDMA = false;
+#endif
+  __shared__ float s_ff[GS_WPB_FWD][FDMA ? WBF + 1 : 1][FDMA ? 32 * FB : 1];
 
   // strip item = tile * 4 + wave (dispatch order, see strip_item)
 #ifdef GS_FWD_ULW
@@ -404,7 +414,24 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
   // Contract the batch's nb Gaussians.  A[ch][k] = feat[gid_k][32 fb + ch]
   // (lane l: channel l&31, k = 8(l>>5) + j), B[k][pix] = w[k][pix] (lane l:
   // pixel (l&31) + 32 blk); slots k >= nb are zeroed on both sides.
+  // Park Gaussian g's feature rows as batch slot k: LDS-DMA into s_ff[k]
+  // (lane l copies channel l of the matrix blocks), or remember the id for
+  // the flush's gather.
+  auto park_row = [&](uint32_t g, int k) {
+    if constexpr (FDMA) {
+      if (lane < 32 * FB)
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void*)(feats + (size_t)g * F + lane),
+            (__attribute__((address_space(3))) void*)&s_ff[lw][k][0], 4, 0, 0);
+    } else {
+      gidv = lane == k ? g : gidv;
+    }
+  };
   auto flush = [&](int n) {
+#ifdef GS_EXP_FWD_NO_FLUSH
+    // timing only (results wrong): the batch is dropped uncontracted
+    if (n >= 0) return;
+#endif
     // an opaque copy of the lane index keeps the compiler from hoisting the
     // flush's address arithmetic into loop-long registers
     int ln = lane;
@@ -418,11 +445,21 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
       bsplit A;
       {
         float fa[8];
+        if constexpr (FDMA) {
+          // the parked rows' DMAs have landed (issued at park time)
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int k = 8 * h + j;
-          const uint32_t g = (uint32_t)__shfl((int)gidv, k, 64);
-          fa[j] = k < n ? feats[(size_t)g * F + fb * 32 + (ln & 31)] : 0.f;
+          for (int j = 0; j < 8; ++j) {
+            const int k = 8 * h + j;
+            fa[j] = k < n ? s_ff[lw][k][fb * 32 + (ln & 31)] : 0.f;
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int k = 8 * h + j;
+            const uint32_t g = (uint32_t)__shfl((int)gidv, k, 64);
+            fa[j] = k < n ? feats[(size_t)g * F + fb * 32 + (ln & 31)] : 0.f;
+          }
         }
         split_bf16(fa, A);
       }
@@ -508,7 +545,7 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
         if constexpr (MF) {
           if (wave_any(blend)) {  // park it; the batch is flushed after the pair
             s_fw[lw][nb][lane] = w;  // 0 on non-blending lanes
-            gidv = lane == nb ? __builtin_amdgcn_readlane(chunk_gid, j) : gidv;
+            park_row(__builtin_amdgcn_readlane(chunk_gid, j), nb);
             ++nb;
           }
         }
@@ -549,8 +586,13 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
             flush(WBF);
             if (nb > WBF) {
               s_fw[lw][0][lane] = s_fw[lw][WBF][lane];
-              const uint32_t g16 = __builtin_amdgcn_readlane(gidv, WBF);
-              gidv = lane == 0 ? g16 : gidv;
+              if constexpr (FDMA) {
+                // the 17th row (landed: the flush waited) moves to slot 0
+                if (lane < 32 * FB) s_ff[lw][0][lane] = s_ff[lw][WBF][lane];
+              } else {
+                const uint32_t g16 = __builtin_amdgcn_readlane(gidv, WBF);
+                gidv = lane == 0 ? g16 : gidv;
+              }
             }
             nb -= WBF;
           }
@@ -609,7 +651,7 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
       if (F > 0 && wave_any(blend)) {
         if constexpr (MF) {
           s_fw[lw][nb][lane] = w;  // 0 on non-blending lanes
-          gidv = lane == nb ? __builtin_amdgcn_readlane(chunk_gid, j) : gidv;
+          park_row(__builtin_amdgcn_readlane(chunk_gid, j), nb);
           if (++nb == WBF) {
             flush(WBF);
             nb = 0;
@@ -978,8 +1020,14 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
     float4_t cf[CB1];
 #pragma unroll
     for (int cb = 0; cb < CB1; ++cb) cf[cb] = float4_t{0.f, 0.f, 0.f, 0.f};
+#ifdef GS_EXP_BWD_NO_MFMA
+    // timing only (results wrong): no splits, no matrix contractions
+    constexpr int NKS = 0;
+#else
+    constexpr int NKS = 2;
+#endif
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < NKS; ++s) {
       const int p0 = 32 * s + 8 * (lane >> 4);
       {
         // the weights w: colour block and features
