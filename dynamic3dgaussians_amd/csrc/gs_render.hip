@@ -55,15 +55,23 @@ typedef float float4_t __attribute__((ext_vector_type(4)));
 
 __device__ inline bool wave_any(bool p) { return __ballot(p) != 0ull; }
 
-// Workgroup -> (camera, slot) of a batch launch: camera-minor -- block b is
-// camera b % C, tile slot b / C, so every camera's longest tiles start first
-// and the work in flight spans all cameras.  Measured against camera-major
-// (all of camera 0's workgroups, then camera 1's, ...; GS_CAM_MAJOR):
-// render_bwd 5.23 vs 5.55 ms per 27-camera step -- in camera-major order
-// every strip in flight adds into the same camera's accumulation records,
-// and the contended float atomics cost more than the cache locality gains.
+// Workgroup -> (camera, slot) of a batch launch: groups of 8 cameras one
+// after the other, camera-minor inside a group -- block b of a group is
+// camera g0 + b % 8, tile slot b / 8.  Workgroups are dealt to the 8 XCDs
+// round-robin (b % 8), so while a group runs each XCD renders ONE camera:
+// the 4 strip workgroups of a backward tile (slots 4t .. 4t+3, blocks 8 apart)
+// and the neighbouring tiles of the camera share that XCD's L2, and every
+// camera's longest tiles still start first.  Measured at the 27-camera batch
+// (profiles/r03n_*): render_bwd HBM reads 6.3 vs 20.1 GB per launch against
+// all 27 cameras interleaved (each tile's strips then sat on 4 different XCDs
+// and fetched the tile's records 4 times), 5.26-5.39 vs 5.30-5.45 ms.
+// Camera-major order (GS_CAM_MAJOR: all of camera 0's workgroups, then
+// camera 1's, ...) measured 5.55 vs 5.23 ms: every strip in flight adds into
+// the same camera's accumulation records and the contended float atomics
+// cost more than the locality gains.  A final group of C % 8 cameras is
+// interleaved the same way without the one-camera-per-XCD property.
 #ifndef GS_CAM_GROUP
-#define GS_CAM_GROUP 64  // cameras interleaved at a time (>= the batch: all of them)
+#define GS_CAM_GROUP 8  // cameras interleaved at a time (8 = one per XCD)
 #endif
 __device__ inline void cam_slot(int bid, int C, int per_cam, int& cam, int& slot) {
 #ifdef GS_CAM_MAJOR
