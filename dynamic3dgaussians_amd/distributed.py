@@ -53,6 +53,8 @@ class GradBucket:
     the caller rebinds: `params` may be a dict (name -> Parameter, e.g. the
     params dict the optimizer groups are built from) and `extras_from` a
     (dict, keys) pair (e.g. (variables, ["means2D_gradient_accum", "denom"])).
+    `keys` restricts a dict of parameters to the trainable entries (e.g.
+    without the reference's constant seg_colors).
 
     bind_grads=True makes every parameter's .grad a view into the flat
     buffer: the backward accumulates straight into the bucket, so
@@ -64,9 +66,9 @@ class GradBucket:
     def __init__(self, params: Iterable[torch.Tensor] | Mapping[str, torch.Tensor],
                  extras: Dict[str, torch.Tensor] | None = None,
                  extras_from: tuple[Mapping[str, torch.Tensor], Sequence[str]] | None = None,
-                 bind_grads: bool = False):
+                 bind_grads: bool = False, keys: Sequence[str] | None = None):
         if isinstance(params, Mapping):
-            self._param_src, self._param_keys = params, list(params.keys())
+            self._param_src, self._param_keys = params, list(keys if keys is not None else params.keys())
             self.params = [params[k] for k in self._param_keys]
         else:
             self._param_src, self._param_keys = None, None

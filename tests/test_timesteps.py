@@ -1,0 +1,240 @@
+"""The per-timestep driver (dynamic3dgaussians_amd/timesteps.py) on the CPU:
+the reference's timestep initialisation and optimizer-state surgery
+(train.py:294-314, external.py:143-155) restated independently here, and
+the camera-sharded loop over two gloo ranks against one process rendering
+the whole rig.  The renders come from the dense PyTorch splat
+(oracle/torch_splat.py, test infrastructure) standing in for the HIP batch
+renderer, which needs a GPU (tests/test_gpu_timesteps.py runs that one)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from dynamic3dgaussians_amd.camera import camera_rig
+from dynamic3dgaussians_amd.scene import camera_tensors, make_gaussians
+from dynamic3dgaussians_amd.timesteps import (TimestepDriver, initialize_post_first_timestep,
+                                              initialize_per_timestep, update_params_and_optimizer)
+from oracle import torch_splat as TS
+
+N_CAMS, W, H, P = 4, 32, 32, 80
+LRS = {"means3D": 1.6e-4, "rgb_colors": 2.5e-3, "unnorm_rotations": 1e-3, "logit_opacities": 0.05,
+       "log_scales": 1e-3}
+
+
+def _params(seed=0):
+    g = make_gaussians(P, seed=seed, extent=0.6)
+    seg = torch.zeros(P, 3)
+    seg[: P // 2, 0] = 1.0  # first half foreground
+    return {"means3D": g["means3D"], "rgb_colors": g["colors"], "unnorm_rotations": g["rotations"],
+            "logit_opacities": torch.logit(g["opacities"].clamp(0.05, 0.9)), "log_scales": torch.log(g["scales"] * 6),
+            "seg_colors": seg}
+
+
+def _optimizer(params, cls=torch.optim.Adam):
+    return cls([{"params": [params[k]], "name": k, "lr": lr} for k, lr in LRS.items()], lr=0.0, eps=1e-15)
+
+
+def _leaf(params):
+    return {k: torch.nn.Parameter(v.clone()) if k != "seg_colors" else v.clone() for k, v in params.items()}
+
+
+# ------------------------------------------------------------ initialisation
+
+def test_update_params_and_optimizer_resets_moments_keeps_step():
+    params = _leaf(_params())
+    opt = _optimizer(params)
+    for p in (params[k] for k in LRS):
+        p.grad = torch.randn_like(p)
+    opt.step()
+    old = params["means3D"]
+    step_before = opt.state[old]["step"].clone()
+    new = torch.randn_like(old)
+    update_params_and_optimizer({"means3D": new}, params, opt)
+    p = params["means3D"]
+    assert p is not old and isinstance(p, torch.nn.Parameter) and p.requires_grad
+    group = [g for g in opt.param_groups if g["name"] == "means3D"][0]
+    assert group["params"][0] is p
+    assert old not in opt.state
+    st = opt.state[p]
+    assert torch.equal(st["exp_avg"], torch.zeros_like(new)) and torch.equal(st["exp_avg_sq"], torch.zeros_like(new))
+    assert torch.equal(st["step"], step_before)
+    assert torch.equal(p.data, new)
+    # the untouched groups keep their state
+    assert opt.state[params["rgb_colors"]]["exp_avg"].abs().sum() > 0
+
+
+def test_initialize_per_timestep_constant_velocity():
+    params = _leaf(_params())
+    opt = _optimizer(params)
+    for p in (params[k] for k in LRS):
+        p.grad = torch.randn_like(p)
+    opt.step()
+    prev_pts = params["means3D"].detach().clone() - 0.01
+    prev_rot = torch.nn.functional.normalize(params["unnorm_rotations"].detach().clone() + 0.05)
+    variables = {"prev_pts": prev_pts, "prev_rot": prev_rot,
+                 "neighbor_indices": torch.randint(0, P // 2, (P // 2, 5))}
+    pts0 = params["means3D"].detach().clone()
+    rot0 = torch.nn.functional.normalize(params["unnorm_rotations"].detach().clone())
+    col0 = params["rgb_colors"].detach().clone()
+    params, variables = initialize_per_timestep(params, variables, opt)
+    # train.py:297-298
+    np.testing.assert_allclose(params["means3D"].detach(), pts0 + (pts0 - prev_pts), rtol=0, atol=1e-7)
+    want_rot = torch.nn.functional.normalize(rot0 + (rot0 - prev_rot))
+    np.testing.assert_allclose(params["unnorm_rotations"].detach(), want_rot, rtol=0, atol=1e-7)
+    # train.py:300-309
+    fg = params["seg_colors"][:, 0] > 0.5
+    inv = rot0[fg].clone()
+    inv[:, 1:] *= -1
+    assert torch.equal(variables["prev_inv_rot_fg"], inv)
+    fg_pts = pts0[fg]
+    assert torch.equal(variables["prev_offset"], fg_pts[variables["neighbor_indices"]] - fg_pts[:, None])
+    assert torch.equal(variables["prev_pts"], pts0) and torch.equal(variables["prev_rot"], rot0)
+    assert torch.equal(variables["prev_col"], col0)
+    # the two replaced groups start from zero moments
+    assert opt.state[params["means3D"]]["exp_avg"].abs().sum() == 0
+
+
+def test_initialize_post_first_timestep_graph():
+    params = _leaf(_params())
+    opt = _optimizer(params)
+
+    def brute_knn(pts, k):  # squared distances, excluding the point itself (o3d_knn semantics)
+        d = ((pts[:, None] - pts[None]) ** 2).sum(-1)
+        d.fill_diagonal_(float("inf"))
+        sq, idx = torch.topk(d, k, largest=False)
+        return sq, idx
+
+    v = initialize_post_first_timestep(params, {}, opt, num_knn=4, knn_fn=brute_knn)
+    fg = params["seg_colors"][:, 0] > 0.5
+    sq, idx = brute_knn(params["means3D"][fg].detach(), 4)
+    assert torch.equal(v["neighbor_indices"], idx)
+    np.testing.assert_allclose(v["neighbor_weight"], torch.exp(-2000 * sq), rtol=1e-6)
+    np.testing.assert_allclose(v["neighbor_dist"], torch.sqrt(sq), rtol=1e-6)
+    assert torch.equal(v["init_bg_pts"], params["means3D"][~fg].detach())
+    for g in opt.param_groups:
+        assert (g["lr"] == 0.0) == (g["name"] in ("logit_opacities", "log_scales"))
+
+
+# ------------------------------------------------------------ sharded loop
+
+def _rig():
+    return [camera_tensors(c) for c in camera_rig(N_CAMS, W, H, radius=2.0)]
+
+
+def _splat_render(rig):
+    """render(rendervar, cams) through the dense PyTorch splat (float32)."""
+    def render(rv, cams):
+        ims = []
+        for c in cams:
+            ct = rig[c]
+            col, _, _, _ = TS.render(rv["means3D"], rv["colors_precomp"], rv["opacities"], rv["scales"],
+                                     rv["rotations"], ct["viewmatrix"], ct["projmatrix"], ct["tanfovx"],
+                                     ct["tanfovy"], ct["c_x"], ct["c_y"], W, H, ct["bg"])
+            ims.append(col)
+        return torch.stack(ims), None
+    return render
+
+
+def _targets(t):
+    return torch.rand(N_CAMS, 3, H, W, generator=torch.Generator().manual_seed(100 + t))
+
+
+class _RecordingAdam(torch.optim.Adam):
+    """torch.optim.Adam that records the gradients it is handed."""
+
+    def __init__(self, *a, **k):
+        super().__init__(*a, **k)
+        self.seen = []
+
+    def step(self, closure=None):
+        self.seen.append({g["name"]: g["params"][0].grad.detach().clone() for g in self.param_groups
+                          if g["params"][0].grad is not None})
+        return super().step(closure)
+
+
+def _run(rank, world):
+    torch.manual_seed(0)
+    params = _leaf(_params())
+    opt = _optimizer(params, _RecordingAdam)
+    drv = TimestepDriver(params, {}, opt, N_CAMS, _splat_render(_rig()), rank=rank, world=world)
+    losses = drv.run(2, lambda t: 2, _targets)
+    return ({k: v.detach().clone() for k, v in drv.params.items()}, opt.seen, losses)
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        params, grads, losses = _run(rank, world)
+        # numpy through the queue (tensors would be shared by file descriptor,
+        # which dies with the process)
+        q.put((rank, ({k: v.numpy() for k, v in params.items()},
+                      [{k: v.numpy() for k, v in g.items()} for g in grads], losses)))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_driver_two_ranks_match_whole_rig():
+    single_params, single_grads, single_losses = _run(0, 1)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    (p0, g0, l0), (p1, g1, l1) = res[0], res[1]
+    # the ranks hold identical parameters after every all-reduced step
+    for k in p0:
+        assert np.array_equal(p0[k], p1[k]), k
+    # 2 timesteps x 2 iterations, each step's all-reduced gradient = the
+    # whole rig's gradient in one process (fp32 summation order)
+    assert len(g0) == len(single_grads) == 4
+    for gs, gd in zip(single_grads, g0):
+        for k in gs:
+            a, b = gs[k].numpy(), gd[k]
+            rel = float(np.linalg.norm(a - b) / max(float(np.linalg.norm(a)), 1e-30))
+            assert rel < 1e-5, (k, rel)
+    # the ranks' loss shares add up to the rig's loss
+    for ls, a, b in zip(single_losses, l0, l1):
+        np.testing.assert_allclose(np.add(a, b), ls, rtol=1e-5)
+    # timestep 1 started from the constant-velocity initialisation
+    for k in single_params:
+        np.testing.assert_allclose(p0[k], single_params[k], rtol=0, atol=5e-4)
+
+
+def test_driver_loss_decreases_on_fit():
+    """Fitting the rig's renders of a perturbed scene: the timestep-0 loss
+    falls over the iterations (the loop trains)."""
+    torch.manual_seed(0)
+    rig = _rig()
+    render = _splat_render(rig)
+    target_params = _params(seed=0)
+    with torch.no_grad():
+        from dynamic3dgaussians_amd.timesteps import params2rendervar
+        tg, _ = render(params2rendervar(target_params), list(range(N_CAMS)))
+    params = _leaf(_params(seed=0))
+    with torch.no_grad():
+        params["rgb_colors"].add_(0.2 * torch.randn_like(params["rgb_colors"])).clamp_(0, 1)
+    opt = _optimizer(params)
+    for g in opt.param_groups:
+        g["lr"] = g["lr"] * 4
+    drv = TimestepDriver(params, {}, opt, N_CAMS, render)
+    losses = drv.timestep(0, 8, tg)
+    assert losses[-1] < 0.8 * losses[0], losses

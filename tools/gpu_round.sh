@@ -5,7 +5,8 @@
 #   3. the default bench line (CPU baselines included)
 #   4. rocprofv3 --kernel-trace --stats of the same bench command
 #   5. a two-rank rehearsal of bench.py's distributed path on the one GPU
-#      (gloo): the weak headline + the 27-camera split step, and --cams-total 27
+#      (gloo): the weak headline + the 27-camera split step, and --cams-total 27;
+#      tools/timesteps_run.py (configs[3] shape) on one rank and on two
 # Outputs in gpurun_out/$TAG.
 set -o pipefail
 R=$GRAFT_REPO_ROOT
@@ -36,4 +37,8 @@ if [ "${SKIP_DIST:-0}" != "1" ]; then
 GS_BENCH_BACKEND=gloo GS_BENCH_SHARE_GPU=1 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 > $O/dist2_weak.json 2> $O/dist2_weak.err || { tail $O/dist2_weak.err; exit 6; }
 GS_BENCH_BACKEND=gloo GS_BENCH_SHARE_GPU=1 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 2 --steps 3 --warmup 1 --cams-total 27 > $O/dist2_strong.json 2> $O/dist2_strong.err || { tail $O/dist2_strong.err; exit 7; }
 cat $O/dist2_weak.json $O/dist2_strong.json
+# configs[3] shape: the timestep driver, one rank and two ranks (gloo, one GPU)
+timeout -k 10 300 python tools/timesteps_run.py > $O/ts1.json 2> $O/ts1.err || { tail $O/ts1.err; exit 8; }
+GS_BENCH_BACKEND=gloo GS_BENCH_SHARE_GPU=1 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29541 tools/timesteps_run.py > $O/ts2.json 2> $O/ts2.err || { tail $O/ts2.err; exit 9; }
+cat $O/ts1.json $O/ts2.json
 fi
