@@ -263,7 +263,38 @@ __device__ inline float4_t mfma_bf16(const bf16x8& a, const bf16x8& b, float4_t 
 __device__ inline f32x16 mfma_bf16(const bf16x8& a, const bf16x8& b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
+// Two operands at a time: one v_cvt_pk_bf16_f32 rounds both (RNE, as the
+// scalar conversion), and each piece is read back to fp32 from the packed
+// word by a shift (low half) or a mask (high half) -- 5.5 vector
+// instructions per operand for 3 pieces instead of the 7.5 the compiler
+// emits for the per-element form (a one-element conversion plus a shift per
+// piece and operand).  Bit-identical pieces.  The remainders are single
+// v_sub_f32 (inline asm, so the compiler does not pair them into
+// v_pk_add_f32, which issues beside the matrix instructions at a higher
+// price and cost registers: F = 32 forward 126 VGPRs and no scratch vs 128
+// and 24 B).  27-camera step (profiles/r03q_ab_split.log): render_fwd
+// 3.21-3.30 vs 3.44-3.48 ms per-element, render_bwd 5.02-5.06 vs 5.24-5.35;
+// the v_pk_add_f32 pairing (GS_SPLIT_PK) 3.37-3.40 / 5.04-5.11.
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ inline uint32_t cvt_pk_bf16(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, bf16x2));
+}
+__device__ inline float bf16_lo(uint32_t u) { return __uint_as_float(u << 16); }
+__device__ inline float bf16_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
+#ifndef GS_SPLIT_PK
+// the remainders with one v_sub_f32 each (no packed fp32 pairing)
+__device__ inline float split_sub(float a, float h) {
+  float r;
+  asm("v_sub_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(h));
+  return r;
+}
+#else
+__device__ inline float split_sub(float a, float h) { return a - h; }
+#endif
 __device__ inline void split_bf16(const float (&x)[8], bsplit& s) {
+#ifdef GS_OLD_SPLIT
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     float r = x[j];
@@ -274,6 +305,24 @@ __device__ inline void split_bf16(const float (&x)[8], bsplit& s) {
       if (i + 1 < NSP) r -= (float)h;
     }
   }
+#else
+  u32x4 w[NSP];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float a = x[2 * j], b = x[2 * j + 1];
+#pragma unroll
+    for (int i = 0; i < NSP; ++i) {
+      const uint32_t u = cvt_pk_bf16(a, b);
+      w[i][j] = u;
+      if (i + 1 < NSP) {
+        a = split_sub(a, bf16_lo(u));
+        b = split_sub(b, bf16_hi(u));
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NSP; ++i) s.p[i] = __builtin_bit_cast(bf16x8, w[i]);
+#endif
 }
 // c += a * b over the split pieces (i + j < NSP), the smallest products first
 template <class Acc>
@@ -294,11 +343,25 @@ __device__ inline Acc mfma_split_x(const bsplit& a, const float (&x)[8], Acc c) 
 #pragma unroll
   for (int j = 0; j < NSP; ++j) {
     bf16x8 b;
+#ifdef GS_OLD_SPLIT
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       b[e] = (__bf16)r[e];
       if (j + 1 < NSP) r[e] -= (float)b[e];
     }
+#else
+    u32x4 w;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const uint32_t u = cvt_pk_bf16(r[2 * e], r[2 * e + 1]);
+      w[e] = u;
+      if (j + 1 < NSP) {
+        r[2 * e] = split_sub(r[2 * e], bf16_lo(u));
+        r[2 * e + 1] = split_sub(r[2 * e + 1], bf16_hi(u));
+      }
+    }
+    b = __builtin_bit_cast(bf16x8, w);
+#endif
 #pragma unroll
     for (int i = 0; i + j < NSP; ++i) c = mfma_bf16(a.p[i], b, c);
   }
