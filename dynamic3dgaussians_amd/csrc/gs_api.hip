@@ -442,7 +442,10 @@ static int render_impl(const gs_gaussians* g, const gs_camera* cams, int C, int 
         return e;
   }
   RenderArgs ra{};
-  ra.W = W; ra.H = H; ra.grid_x = gx; ra.num_tiles = gx * gy; ra.F = g->F; ra.compat = compat;
+  // the matrix-core feature widths gather rows by 32-bit byte offsets
+  if (g->F >= 32 && (uint64_t)g->P * (uint64_t)g->F * 4u > 0xFFFFFFFFull)
+    return fail(-1, "semantic feature table of %lld x %d floats exceeds 4 GiB", (long long)g->P, g->F);
+  ra.W = W; ra.H = H; ra.grid_x = gx; ra.num_tiles = gx * gy; ra.F = g->F; ra.compat = compat; ra.P = g->P;
   ra.order = ta.order;
   ra.smax = at<uint32_t>(image, il.smax);
   ra.ranges = ta.ranges; ra.point_list = total > 0 ? static_cast<const uint32_t*>(binning) : nullptr;

@@ -65,7 +65,7 @@ struct PreprocessBwdArgs {
 };
 
 struct RenderArgs {
-  int W, H, grid_x, num_tiles, F, compat;
+  int W, H, grid_x, num_tiles, F, compat, P;
   const uint4* order;  // num_tiles: dispatch records {tile, range.x, range.y, 0}, longest list first
   const uint2* ranges;
   const uint32_t* point_list;

@@ -498,6 +498,19 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
       gidv = lane == k ? g : gidv;
     }
   };
+  // feature rows addressed by unsigned 32-bit byte offsets through a buffer
+  // resource over the P x F table (the host refuses tables over 4 GiB);
+  // GS_FWD_GATHER64: 64-bit pointer arithmetic per row (3 more vector
+  // instructions per row and spilled registers at the 128-VGPR cap)
+#ifdef GS_FWD_GATHER64
+  constexpr bool fbuf = false;
+#else
+  constexpr bool fbuf = MF;
+#endif
+  const uint64_t fbytes = (uint64_t)ca.P * F * 4u;
+  const auto frsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(feats), (short)0,
+                                                       (int)(uint32_t)(fbytes < 0xFFFFFFFFull ? fbytes : 0xFFFFFFFFull),
+                                                       0x00020000);
   auto flush = [&](int n) {
 #ifdef GS_EXP_FWD_NO_FLUSH
     // timing only (results wrong): the batch is dropped uncontracted
@@ -523,6 +536,17 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
           for (int j = 0; j < 8; ++j) {
             const int k = 8 * h + j;
             fa[j] = k < n ? s_ff[lw][k][fb * 32 + (ln & 31)] : 0.f;
+          }
+        } else if (fbuf) {
+          // 32-bit row offsets through a buffer resource: one address
+          // instruction per row instead of 64-bit pointer arithmetic
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int k = 8 * h + j;
+            const uint32_t g = (uint32_t)__shfl((int)gidv, k, 64);
+            const uint32_t off = (g * (uint32_t)F + (uint32_t)(fb * 32 + (ln & 31))) * 4u;
+            const float v = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(frsrc, (int)off, 0, 0));
+            fa[j] = k < n ? v : 0.f;
           }
         } else {
 #pragma unroll
@@ -1147,11 +1171,13 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
         const float cb = row == 1 ? 1.f : row == 4 ? Y : 0.f;
         const float cc = row == 3 ? 1.f : 0.f;
         const float X0 = (float)(2 * (p8 % STRIP_W) - (STRIP_W - 1));
+        u32x4 xw;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float X = X0 + (float)(2 * j);
-          xu[j] = (__bf16)fmaf(X, fmaf(cc, X, cb), ca);
+        for (int e = 0; e < 4; ++e) {
+          const float Xa = X0 + (float)(4 * e), Xb = Xa + 2.f;
+          xw[e] = cvt_pk_bf16(fmaf(Xa, fmaf(cc, Xa, cb), ca), fmaf(Xb, fmaf(cc, Xb, cb), ca));
         }
+        xu = __builtin_bit_cast(bf16x8, xw);
       }
       cu = mfma_exact_split(xu, Us, cu);
     }
