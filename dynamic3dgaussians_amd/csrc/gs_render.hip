@@ -54,6 +54,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float float4_t __attribute__((ext_vector_type(4)));
 
 __device__ inline bool wave_any(bool p) { return __ballot(p) != 0ull; }
+__device__ inline uint64_t clamp_u32(uint64_t v) { return v < 0xFFFFFFFFull ? v : 0xFFFFFFFFull; }
 
 // Workgroup -> (camera, slot) of a batch launch: groups of 8 cameras one
 // after the other, camera-minor inside a group -- block b of a group is
@@ -509,8 +510,7 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
 #endif
   const uint64_t fbytes = (uint64_t)ca.P * F * 4u;
   const auto frsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(feats), (short)0,
-                                                       (int)(uint32_t)(fbytes < 0xFFFFFFFFull ? fbytes : 0xFFFFFFFFull),
-                                                       0x00020000);
+                                                       (int)(uint32_t)clamp_u32(fbytes), 0x00020000);
   auto flush = [&](int n) {
 #ifdef GS_EXP_FWD_NO_FLUSH
     // timing only (results wrong): the batch is dropped uncontracted
@@ -909,6 +909,15 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
   const float* __restrict__ dL_dalpha = ca.dL_dalpha;
   float* __restrict__ acc = ca.acc;
   float* __restrict__ dsem = ca.dsem;
+#ifdef GS_BWD_BUFFER_ATOMIC
+  // buffer resources over the camera's accumulation records and the feature
+  // gradient rows: the commits' atomics take 32-bit byte offsets (the host
+  // refuses tables over 4 GiB)
+  const auto acc_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      acc, (short)0, (int)(uint32_t)clamp_u32((uint64_t)ca.P * ACC_STRIDE * 4u), 0x00020000);
+  const auto dsem_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      dsem, (short)0, (int)(uint32_t)clamp_u32((uint64_t)ca.P * feature_grad_stride(F) * 4u), 0x00020000);
+#endif
   constexpr int WB = 16;                      // Gaussians per matrix batch
   constexpr int CB = F >= 16 ? F / 16 : 0;    // 16-channel feature blocks with their own accumulators
   constexpr int CB1 = CB > 0 ? CB : 1;
@@ -1232,12 +1241,24 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
       if (i >= WB * NCOMP) break;
       const int slot = i / NCOMP, comp = i - NCOMP * slot;
       const uint32_t gi = FW > 0 ? f_bits(s_slot[lw][slot].w) : agid[t < NAG ? t : 0];
+#ifndef GS_BWD_BUFFER_ATOMIC
       float* dst = comp < A_FEAT ? acc + (size_t)ACC_STRIDE * gi + comp
                                  : dsem + (size_t)gi * FS + 16 * CB + (comp - A_FEAT);
 #ifdef GS_EXP_NO_ACC_ATOMIC
       if (slot < nb && s_out[i] == 12345.f) *dst = 0.f;
 #else
       if (slot < nb) atomicAdd(dst, s_out[i]);
+#endif
+#else
+      // experiment: no-return buffer atomics at 32-bit byte offsets (5.07-5.11
+      // vs 5.06-5.08 ms with global atomics, profiles/r03s_ab_bwd_buffer_atomic.log)
+      if (slot < nb) {
+        if (comp < A_FEAT)
+          (void)__builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(s_out[i], acc_rsrc, (int)((ACC_STRIDE * gi + comp) * 4u), 0, 0);
+        else
+          (void)__builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(
+              s_out[i], dsem_rsrc, (int)((gi * (uint32_t)FS + (uint32_t)(16 * CB + comp - A_FEAT)) * 4u), 0, 0);
+      }
 #endif
     }
     // features: C[slot][ch] = sum_p w[slot][p] dL/dF[p][ch]; lane l holds
@@ -1250,8 +1271,12 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
         const uint32_t gi = fgid[r];
 #ifdef GS_EXP_NO_FEAT_ATOMIC
         if (slot < nb && cf[cb][r] == 12345.f) dsem[(size_t)gi * FS + 16 * cb + g] = 0.f;
-#else
+#elif !defined(GS_BWD_BUFFER_ATOMIC)
         if (slot < nb) atomicAdd(dsem + (size_t)gi * FS + 16 * cb + g, cf[cb][r]);
+#else
+        if (slot < nb)
+          (void)__builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(
+              cf[cb][r], dsem_rsrc, (int)((gi * (uint32_t)FS + (uint32_t)(16 * cb + g)) * 4u), 0, 0);
 #endif
       }
     }
