@@ -156,21 +156,64 @@ class _RecordingAdam(torch.optim.Adam):
         return super().step(closure)
 
 
-def _run(rank, world):
+def _toy_densify(params, variables, optimizer, i):
+    """At iteration 1: remove Gaussian 3 and clone Gaussian 0, with the
+    reference's optimizer-state surgery (external.py:157-205 restated:
+    rows dropped from / zero rows appended to the Adam moments, new
+    Parameters, the statistics tensors rebound)."""
+    if i != 1:
+        return params, variables
+    trainable = [g["name"] for g in optimizer.param_groups]
+    keep = torch.ones(params["means3D"].shape[0], dtype=torch.bool)
+    keep[3] = False
+    for k in list(params):
+        if k in trainable:
+            g = [x for x in optimizer.param_groups if x["name"] == k][0]
+            st = optimizer.state.pop(g["params"][0], None)
+            p = torch.nn.Parameter(g["params"][0][keep].detach().requires_grad_(True))
+            if st is not None:
+                st["exp_avg"], st["exp_avg_sq"] = st["exp_avg"][keep], st["exp_avg_sq"][keep]
+                optimizer.state[p] = st
+            g["params"][0] = p
+            params[k] = p
+        else:
+            params[k] = params[k][keep]
+    for k in ("means2D_gradient_accum", "denom", "max_2D_radius"):
+        variables[k] = variables[k][keep]
+    for k in list(params):
+        v = params[k][:1].detach()
+        if k in trainable:
+            g = [x for x in optimizer.param_groups if x["name"] == k][0]
+            st = optimizer.state.pop(g["params"][0], None)
+            p = torch.nn.Parameter(torch.cat((g["params"][0].detach(), v), 0).requires_grad_(True))
+            if st is not None:
+                st["exp_avg"] = torch.cat((st["exp_avg"], torch.zeros_like(v)), 0)
+                st["exp_avg_sq"] = torch.cat((st["exp_avg_sq"], torch.zeros_like(v)), 0)
+                optimizer.state[p] = st
+            g["params"][0] = p
+            params[k] = p
+        else:
+            params[k] = torch.cat((params[k], v), 0)
+    for k in ("means2D_gradient_accum", "denom", "max_2D_radius"):
+        variables[k] = torch.cat((variables[k], torch.zeros(1)), 0)
+    return params, variables
+
+
+def _run(rank, world, densify=None):
     torch.manual_seed(0)
     params = _leaf(_params())
     opt = _optimizer(params, _RecordingAdam)
-    drv = TimestepDriver(params, {}, opt, N_CAMS, _splat_render(_rig()), rank=rank, world=world)
-    losses = drv.run(2, lambda t: 2, _targets)
+    drv = TimestepDriver(params, {}, opt, N_CAMS, _splat_render(_rig()), rank=rank, world=world, densify=densify)
+    losses = drv.run(2, lambda t: 2 if densify is None else 3, _targets)
     return ({k: v.detach().clone() for k, v in drv.params.items()}, opt.seen, losses)
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, densify=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        params, grads, losses = _run(rank, world)
+        params, grads, losses = _run(rank, world, _toy_densify if densify else None)
         # numpy through the queue (tensors would be shared by file descriptor,
         # which dies with the process)
         q.put((rank, ({k: v.numpy() for k, v in params.items()},
@@ -187,12 +230,19 @@ def _free_port():
     return p
 
 
-def test_driver_two_ranks_match_whole_rig():
-    single_params, single_grads, single_losses = _run(0, 1)
+@pytest.mark.parametrize("densify", [False, True])
+def test_driver_two_ranks_match_whole_rig(densify):
+    """densify=True: a densification at timestep 0 replaces every tensor;
+    the driver builds a new bucket at the next step, the replaced
+    Parameters skip that iteration's optimizer step (no .grad), as in the
+    reference, and the ranks stay identical."""
+    single_params, single_grads, single_losses = _run(0, 1, _toy_densify if densify else None)
+    if densify:
+        assert single_params["means3D"].shape[0] == P  # one removed, one cloned
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, densify)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=300) for _ in procs)
@@ -203,9 +253,9 @@ def test_driver_two_ranks_match_whole_rig():
     # the ranks hold identical parameters after every all-reduced step
     for k in p0:
         assert np.array_equal(p0[k], p1[k]), k
-    # 2 timesteps x 2 iterations, each step's all-reduced gradient = the
+    # 2 timesteps x 2 (3) iterations, each step's all-reduced gradient = the
     # whole rig's gradient in one process (fp32 summation order)
-    assert len(g0) == len(single_grads) == 4
+    assert len(g0) == len(single_grads) == (6 if densify else 4)
     for gs, gd in zip(single_grads, g0):
         for k in gs:
             a, b = gs[k].numpy(), gd[k]
