@@ -111,6 +111,14 @@ def test_batch_matches_per_camera(F, use_sh, compat, P=15000, W=176, H=144, C=5)
     assert torch.all(leaves_b["means3D"].grad[off] == 0)
 
 
+def test_batch_of_two_camera_groups_matches_per_camera():
+    """11 cameras: the blend launches deal the first 8 one per XCD and the
+    last 3 as a smaller group (cam_slot, GS_CAM_GROUP = 8); every camera's
+    outputs stay bit-identical to its per-camera render and the gradients
+    the per-camera sum."""
+    test_batch_matches_per_camera(32, False, "reference", P=9000, W=112, H=96, C=11)
+
+
 def test_batch_of_one_is_the_single_camera_call(P=12000, W=128, H=96):
     src = _scene(P, 32, False, seed=2)
     rig = camera_rig(3, W, H)
