@@ -50,7 +50,7 @@ VARIANT_FLAGS = {"": [], "stats": ["-DGS_STATS"], "stamps": ["-DGS_STAMPS"], "st
                  "exp_split2": ["-DGS_SPLIT_PIECES=2"], "exp_bwd_wpe2": ["-DGS_BWD_WPE=2"], "exp_fwd_wpe3": ["-DGS_FWD_WPE=3"],
                  "exp_fwd_noflush": ["-DGS_EXP_FWD_NO_FLUSH"], "exp_bwd_nomfma": ["-DGS_EXP_BWD_NO_MFMA"],
                  "exp_noatomic_nomfma": ["-DGS_EXP_NO_FEAT_ATOMIC", "-DGS_EXP_NO_ACC_ATOMIC", "-DGS_EXP_BWD_NO_MFMA"],
-                 "exp_fwd_dma": ["-DGS_FWD_DMA"], "exp_camgrp_all": ["-DGS_CAM_GROUP=64"], "exp_oldsplit": ["-DGS_OLD_SPLIT"], "exp_split_pk": ["-DGS_SPLIT_PK"], "exp_fwd_gather64": ["-DGS_FWD_GATHER64"], "exp_bwd_buffer_atomic": ["-DGS_BWD_BUFFER_ATOMIC"]}
+                 "exp_fwd_dma": ["-DGS_FWD_DMA"], "exp_camgrp_all": ["-DGS_CAM_GROUP=64"], "exp_oldsplit": ["-DGS_OLD_SPLIT"], "exp_split_pk": ["-DGS_SPLIT_PK"], "exp_fwd_gather64": ["-DGS_FWD_GATHER64"], "exp_bwd_buffer_atomic": ["-DGS_BWD_BUFFER_ATOMIC"], "exp_bucket_store2": ["-DGS_EXP_BUCKET_STORE2"], "exp_bucket_direct": ["-DGS_BUCKET_DIRECT"]}
 ARCH = os.environ.get("GSPLAT_OFFLOAD_ARCH", "gfx950")
 
 # Per-file flags.  The preprocess kernels are compiled without FMA

@@ -87,7 +87,16 @@ __global__ __launch_bounds__(TB_THREADS) void tile_hist_kernel(TileArgs a0, CamB
     auto emit = [&](int x, int y, uint64_t k) {
       const uint32_t u = (uint32_t)(y * gx + x - t0);
       if (u < (uint32_t)nt) {
+#ifdef GS_EXP_BUCKET_STORE2
+        // timing only: every key stored twice (same address, same value)
+        if (WRITE) {
+          const uint32_t sl = atomicAdd(&s_bin[u], 1u);
+          *(volatile uint64_t*)&a.keys[sl] = k;
+          *(volatile uint64_t*)&a.keys[sl] = k;
+        }
+#else
         if (WRITE) a.keys[atomicAdd(&s_bin[u], 1u)] = k;
+#endif
         else atomicAdd(&s_bin[u], 1u);
       }
     };
@@ -143,6 +152,133 @@ __global__ __launch_bounds__(TB_THREADS) void tile_hist_kernel(TileArgs a0, CamB
       for (int w2 = 0; w2 < TB_THREADS / 64; ++w2) sum += s_rect[w2];
       a.bsum[b] = sum;
     }
+  }
+}
+
+// Bucket pass with the block's keys staged in LDS (GS_BUCKET_DIRECT: the
+// tile_hist_kernel<true> walk above, every key stored where its slot lands).
+// Consecutive lanes of that walk hold unrelated Gaussians, so each key store
+// is its own 8-B request to a different line; storing every key twice cost
+// +0.7 ms per 27-camera step (profiles/r03u_ab_bucket_store2.log), i.e. the
+// stores, not the walk, bound the pass.  Here the block first lays out its
+// own per-tile runs in LDS (the count pass's per-block counts, scanned), the
+// walk drops each key into its run there, and the block then copies the runs
+// out in order: consecutive lanes store consecutive keys of a run.  A block
+// with more keys than the LDS holds (cap) stores directly, as before.
+__global__ __launch_bounds__(TB_THREADS) void tile_bucket_kernel(TileArgs a0, CamBatch cb, int t0, int nt, int cap) {
+  const TileArgs a = cam_tile_args(a0, cb, blockIdx.y);
+  extern __shared__ uint64_t s_dyn64[];
+  uint64_t* s_key = s_dyn64;                                  // cap keys
+  uint32_t* s_pos = reinterpret_cast<uint32_t*>(s_key + cap); // cap global slots
+  uint32_t* s_cur = s_pos + cap;                              // nt run cursors (local, or global if direct)
+  uint32_t* s_dlt = s_cur + nt;                               // nt: global slot - local slot of the tile's run
+  __shared__ uint32_t s_wsum[TB_THREADS / 64];
+  __shared__ uint32_t s_total;
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int per = (a.P + TB_BLOCKS - 1) / TB_BLOCKS;
+  const int g0 = b * per, g1 = min(a.P, g0 + per);
+  const int T = a.num_tiles;
+  uint4 rnext = g0 + tid < g1 ? a.rect[g0 + tid] : make_uint4(0u, 0u, 0u, 0u);
+  // this block's run length in every tile: the column scan left each block's
+  // offset inside the tile in thist (the next block's offset, or the tile
+  // total, ends the run)
+  constexpr int KT = 16;  // tiles per thread in the local scan (TB_THREADS * KT >= nt)
+  const int i0 = tid * ((nt + TB_THREADS - 1) / TB_THREADS);
+  const int i1 = min(nt, i0 + (nt + TB_THREADS - 1) / TB_THREADS);
+  uint32_t cnt[KT];
+  uint32_t run = 0;
+#pragma unroll
+  for (int k = 0; k < KT; ++k) {
+    const int i = i0 + k;
+    cnt[k] = 0;
+    if (i < i1) {
+      const size_t t = (size_t)t0 + i;
+      const uint32_t beg = a.thist[(size_t)b * T + t];
+      const uint32_t end = b + 1 < TB_BLOCKS ? a.thist[(size_t)(b + 1) * T + t] : a.ttotal[t];
+      cnt[k] = end - beg;
+      run += cnt[k];
+    }
+  }
+  // exclusive scan of the per-thread sums over the block
+  uint32_t incl = run;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) s_wsum[wv] = incl;
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t acc = 0;
+    for (int w = 0; w < TB_THREADS / 64; ++w) {
+      const uint32_t v = s_wsum[w];
+      s_wsum[w] = acc;
+      acc += v;
+    }
+    s_total = acc;
+  }
+  __syncthreads();
+  const uint32_t total = s_total;
+  const bool staged = total <= (uint32_t)cap;
+  {
+    uint32_t lo = s_wsum[wv] + incl - run;  // local start of this thread's first tile
+#pragma unroll
+    for (int k = 0; k < KT; ++k) {
+      const int i = i0 + k;
+      if (i < i1) {
+        const size_t t = (size_t)t0 + i;
+        const uint32_t gbeg = a.ranges[t].x + a.thist[(size_t)b * T + t];
+        s_cur[i] = staged ? lo : gbeg;
+        s_dlt[i] = gbeg - lo;
+        lo += cnt[k];
+      }
+    }
+  }
+  __syncthreads();
+  const int gx = a.grid_x;
+  for (int base = g0; base < g1; base += TB_THREADS) {
+    const int g = base + tid;
+    int x0 = 0, y0 = 0, w = 0, n = 0;
+    uint64_t key = 0;
+    const uint4 r = rnext;  // {x0 | y0 << 16, x1 | y1 << 16, depth bits, tiles_touched}
+    if (base + TB_THREADS < g1 && g + TB_THREADS < g1) rnext = a.rect[g + TB_THREADS];
+    if (g < g1) {
+      x0 = (int)(r.x & 0xFFFFu);
+      y0 = (int)(r.x >> 16);
+      w = (int)(r.y & 0xFFFFu) - x0;
+      n = w * ((int)(r.y >> 16) - y0);
+      if (n > 0) key = ((uint64_t)r.z << 32) | (uint32_t)g;
+    }
+    auto emit = [&](int x, int y, uint64_t k) {
+      const uint32_t u = (uint32_t)(y * gx + x - t0);
+      if (u < (uint32_t)nt) {
+        const uint32_t sl = atomicAdd(&s_cur[u], 1u);
+        if (staged) {
+          s_key[sl] = k;
+          s_pos[sl] = s_dlt[u] + sl;
+        } else {
+          a.keys[sl] = k;
+        }
+      }
+    };
+    if (n > 0 && n <= LANE_TILES) {
+      const int h = n / w;
+      for (int y = y0; y < y0 + h; ++y)
+        for (int x = x0; x < x0 + w; ++x) emit(x, y, key);
+    }
+    uint64_t big = __ballot(n > LANE_TILES);
+    while (big) {
+      const int j = __builtin_ctzll(big);
+      big &= big - 1;
+      const int bx0 = __shfl(x0, j, 64), by0 = __shfl(y0, j, 64), bw = __shfl(w, j, 64);
+      const int bn = __shfl(n, j, 64);
+      const uint64_t bk = (uint64_t)__shfl((long long)key, j, 64);
+      for (int i = lane; i < bn; i += 64) emit(bx0 + i % bw, by0 + i / bw, bk);
+    }
+  }
+  if (staged) {
+    __syncthreads();
+    for (uint32_t i = tid; i < total; i += TB_THREADS) a.keys[s_pos[i]] = s_key[i];
   }
 }
 
@@ -681,6 +817,17 @@ void launch_tile_bucket(const TileArgs& a, const CamBatch& cb, hipStream_t s) {
   const int T = a.num_tiles;
   for (int t0 = 0; t0 < T; t0 += TB_BINS) {
     const int nt = min(TB_BINS, T - t0);
+#ifndef GS_BUCKET_DIRECT
+    // staged: the whole LDS of a CU (one workgroup) for the cursors, the run
+    // offsets and as many keys as fit (12 B each)
+    constexpr int kLds = 160 * 1024 - 1024;  // minus the static arrays
+    const int cap = (kLds - 8 * nt) / 12;
+    if (nt <= TB_THREADS * 16 && cap >= 2048) {
+      hipLaunchKernelGGL(tile_bucket_kernel, dim3(TB_BLOCKS, cb.C), dim3(TB_THREADS),
+                         (size_t)12 * cap + (size_t)8 * nt, s, a, cb, t0, nt, cap);
+      continue;
+    }
+#endif
     hipLaunchKernelGGL(tile_hist_kernel<true>, dim3(TB_BLOCKS, cb.C), dim3(TB_THREADS), sizeof(uint32_t) * nt, s,
                        a, cb, t0, nt);
   }
