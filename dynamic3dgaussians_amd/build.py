@@ -40,7 +40,7 @@ VARIANT_FLAGS = {"": [], "stats": ["-DGS_STATS"], "stamps": ["-DGS_STAMPS"], "st
                  "exp_ssmall512": ["-DGS_SORT_SMALL=512"], "exp_ssmall768": ["-DGS_SORT_SMALL=768"],
                  "exp_ssmall1536": ["-DGS_SORT_SMALL=1536"], "exp_cammajor": ["-DGS_CAM_MAJOR"], "exp_camg4": ["-DGS_CAM_GROUP=4"], "exp_camg9": ["-DGS_CAM_GROUP=9"], "exp_camg2": ["-DGS_CAM_GROUP=2"],
                  "exp_kpt16": ["-DGS_BS_KPT=16"], "exp_bsl10": ["-DGS_BS_BITS_LONG=10"], "exp_bsl12": ["-DGS_BS_BITS_LONG=12"],
-                 "exp_tbb64": ["-DGS_TB_BLOCKS=64"], "exp_tbb128": ["-DGS_TB_BLOCKS=128"],
+                 "exp_tbb64": ["-DGS_TB_BLOCKS=64"], "exp_tbb128": ["-DGS_TB_BLOCKS=128"], "exp_tbb256": ["-DGS_TB_BLOCKS=256"],
                  "exp_fulw": ["-DGS_FWD_ULW", "-DGS_FWD_SLAST"],
                  "exp_ulw": ["-DGS_FWD_ULW", "-DGS_FWD_SLAST", "-DGS_BWD_ULW"],
                  "exp_bkt_batch": ["-DGS_BUCKET_BATCH"],

@@ -81,9 +81,13 @@ __host__ __device__ inline int64_t sort_blocks(int64_t n) {
 }
 // Tile bucketing geometry (gs_tiles.hip): TB_BLOCKS workgroups each own a
 // contiguous slice of the Gaussians and histogram their instances over (a
-// range of at most TB_BINS) tiles in LDS.
+// range of at most TB_BINS) tiles in LDS.  128 per camera: with the bucket
+// pass staging a workgroup's keys in LDS (tile_bucket_kernel), longer per-tile
+// runs make longer coalesced stores -- bench step duplicate 0.253-0.260 vs
+// 0.341-0.343 ms and scan 0.091 vs 0.121 at 256 (profiles/r03w_ab_tbb128.log);
+// the bench camera's ~13 k keys per workgroup fit the LDS.
 #ifndef GS_TB_BLOCKS
-#define GS_TB_BLOCKS 256
+#define GS_TB_BLOCKS 128
 #endif
 constexpr int TB_BLOCKS = GS_TB_BLOCKS;  // per camera; a multiple of 64 (tile_rowscan_kernel, tile_offsets_kernel)
 #ifndef GS_TB_THREADS

@@ -164,14 +164,15 @@ __global__ __launch_bounds__(TB_THREADS) void tile_hist_kernel(TileArgs a0, CamB
 // own per-tile runs in LDS (the count pass's per-block counts, scanned), the
 // walk drops each key into its run there, and the block then copies the runs
 // out in order: consecutive lanes store consecutive keys of a run.  A block
-// with more keys than the LDS holds (cap) stores directly, as before.
+// with more keys than the LDS holds (cap, 10 B per key) stores directly, as
+// before.
 __global__ __launch_bounds__(TB_THREADS) void tile_bucket_kernel(TileArgs a0, CamBatch cb, int t0, int nt, int cap) {
   const TileArgs a = cam_tile_args(a0, cb, blockIdx.y);
   extern __shared__ uint64_t s_dyn64[];
-  uint64_t* s_key = s_dyn64;                                  // cap keys
-  uint32_t* s_pos = reinterpret_cast<uint32_t*>(s_key + cap); // cap global slots
-  uint32_t* s_cur = s_pos + cap;                              // nt run cursors (local, or global if direct)
-  uint32_t* s_dlt = s_cur + nt;                               // nt: global slot - local slot of the tile's run
+  uint64_t* s_key = s_dyn64;                                    // cap keys
+  uint32_t* s_cur = reinterpret_cast<uint32_t*>(s_key + cap);   // nt run cursors (local, or global if direct)
+  uint32_t* s_dlt = s_cur + nt;                                 // nt: global slot - local slot of the tile's run
+  uint16_t* s_til = reinterpret_cast<uint16_t*>(s_dlt + nt);    // cap: the key's tile (nt <= 65536)
   __shared__ uint32_t s_wsum[TB_THREADS / 64];
   __shared__ uint32_t s_total;
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -255,7 +256,7 @@ __global__ __launch_bounds__(TB_THREADS) void tile_bucket_kernel(TileArgs a0, Ca
         const uint32_t sl = atomicAdd(&s_cur[u], 1u);
         if (staged) {
           s_key[sl] = k;
-          s_pos[sl] = s_dlt[u] + sl;
+          s_til[sl] = (uint16_t)u;
         } else {
           a.keys[sl] = k;
         }
@@ -278,7 +279,7 @@ __global__ __launch_bounds__(TB_THREADS) void tile_bucket_kernel(TileArgs a0, Ca
   }
   if (staged) {
     __syncthreads();
-    for (uint32_t i = tid; i < total; i += TB_THREADS) a.keys[s_pos[i]] = s_key[i];
+    for (uint32_t i = tid; i < total; i += TB_THREADS) a.keys[s_dlt[s_til[i]] + i] = s_key[i];
   }
 }
 
@@ -819,12 +820,12 @@ void launch_tile_bucket(const TileArgs& a, const CamBatch& cb, hipStream_t s) {
     const int nt = min(TB_BINS, T - t0);
 #ifndef GS_BUCKET_DIRECT
     // staged: the whole LDS of a CU (one workgroup) for the cursors, the run
-    // offsets and as many keys as fit (12 B each)
+    // offsets and as many keys as fit (10 B each: the key and its tile)
     constexpr int kLds = 160 * 1024 - 1024;  // minus the static arrays
-    const int cap = (kLds - 8 * nt) / 12;
+    const int cap = ((kLds - 8 * nt) / 10) & ~3;
     if (nt <= TB_THREADS * 16 && cap >= 2048) {
       hipLaunchKernelGGL(tile_bucket_kernel, dim3(TB_BLOCKS, cb.C), dim3(TB_THREADS),
-                         (size_t)12 * cap + (size_t)8 * nt, s, a, cb, t0, nt, cap);
+                         (size_t)10 * cap + (size_t)8 * nt, s, a, cb, t0, nt, cap);
       continue;
     }
 #endif
