@@ -194,9 +194,12 @@ __global__ __launch_bounds__(256) void preprocess_fwd_kernel(PreprocessArgs a0, 
   const int g = blockIdx.x * 256 + threadIdx.x;
   if (g >= a0.P) return;
   const PreprocessArgs a = cam_args(a0, batch, blockIdx.y);
-  a.radii[g] = 0;
-  a.tiles[g] = 0;
-  a.rect[g] = make_uint4(0u, 0u, 0u, 0u);
+  // a culled Gaussian's outputs (a visible one's are written once, at the end)
+  auto culled = [&]() {
+    a.radii[g] = 0;
+    a.tiles[g] = 0;
+    a.rect[g] = make_uint4(0u, 0u, 0u, 0u);
+  };
   const V3 p = ld3(a.means3D + 3 * g);
   // The 3D covariance does not depend on the camera: the batch's camera 0
   // stores it for every Gaussian (before the frustum test, so a Gaussian
@@ -227,6 +230,7 @@ __global__ __launch_bounds__(256) void preprocess_fwd_kernel(PreprocessArgs a0, 
   const V3 pv = xf43(a.view, p);
   if (pv.z <= 0.0f) {  // in_frustum, Q8
     if (a.prefiltered) atomicOr(a.status, 1);
+    culled();
     return;
   }
   const float4 ph = xf44(a.proj, p);
@@ -237,7 +241,10 @@ __global__ __launch_bounds__(256) void preprocess_fwd_kernel(PreprocessArgs a0, 
   float cov[3];
   ewa_cov2d(e, c3, cov);
   const float det = cov[0] * cov[2] - cov[1] * cov[1];
-  if (det == 0.0f) return;
+  if (det == 0.0f) {
+    culled();
+    return;
+  }
   const float det_inv = 1.f / det;
   const float ca = cov[2] * det_inv, cb = -cov[1] * det_inv, cc = cov[0] * det_inv;
   const float mid = 0.5f * (cov[0] + cov[2]);
@@ -247,7 +254,10 @@ __global__ __launch_bounds__(256) void preprocess_fwd_kernel(PreprocessArgs a0, 
   const float px = ndc_to_pix(ppx, a.W), py = ndc_to_pix(ppy, a.H);
   int2 rmin, rmax;
   tile_rect(px, py, (int)rad, a.grid_x, a.grid_y, rmin, rmax);
-  if ((rmax.x - rmin.x) * (rmax.y - rmin.y) == 0) return;
+  if ((rmax.x - rmin.x) * (rmax.y - rmin.y) == 0) {
+    culled();
+    return;
+  }
 
   float rgb[3];
   if (a.colors_precomp) {
