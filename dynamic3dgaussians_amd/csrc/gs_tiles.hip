@@ -528,6 +528,8 @@ struct RadixSmem {
 
 template <class KP, int TS_THREADS, int BINS>
 __device__ __attribute__((always_inline)) KP tile_radix_sort(KP A, KP B, int n, RadixSmem<TS_THREADS, BINS>& sm) {
+  // one thread per 8-bit digit in the count scans below
+  static_assert(TS_THREADS >= 256, "tile_radix_sort needs >= 256 threads per workgroup");
   constexpr int TS_WAVES = TS_THREADS / 64;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint64_t lt = (1ull << lane) - 1ull;
