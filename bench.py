@@ -414,10 +414,12 @@ def main():
         opt = FusedAdam(groups, lr=0.0, eps=1e-15)
     else:
         opt = torch.optim.Adam(groups, lr=0.0, eps=1e-15, fused=optim_kind == "torch_fused")
-    # Every parameter's .grad is a view into the all-reduce bucket: the
-    # backward accumulates straight into it (no pack/unpack copies at N > 1);
-    # gradients are cleared by one fill of the bucket.
-    bucket = GradBucket(params, bind_grads=True)
+    # N > 1: every parameter's .grad is a view into the all-reduce bucket, so
+    # the backward accumulates straight into it (no pack/unpack copies) and
+    # one fill clears it.  N = 1 has no exchange: gradients stay unbound, so
+    # autograd hands the backward's tensors to the leaves without the six
+    # accumulate kernels and the fill (-0.06 ms per step).
+    bucket = GradBucket(params, bind_grads=world > 1)
     g = torch.Generator(device=dev).manual_seed(1 + rank)
     H_, W_ = args.height, args.width
     up_color = torch.randn(3, H_, W_, device=dev, generator=g)

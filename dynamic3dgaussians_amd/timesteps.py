@@ -192,7 +192,10 @@ class TimestepDriver:
         # the optimizer's parameters (seg_colors and other constants stay out)
         names = {g.get("name") for g in self.optimizer.param_groups}
         keys = [k for k in self.params if k in names]
-        self.bucket = GradBucket(self.params, extras_from=(self.variables, list(STATS[:2])), bind_grads=True,
+        # bound .grad views only when there is an exchange (N = 1: autograd
+        # hands the backward's tensors to the leaves, no accumulate kernels)
+        self.bucket = GradBucket(self.params, extras_from=(self.variables, list(STATS[:2])),
+                                 bind_grads=self.world > 1,
                                  keys=keys)
 
     def _live_bucket(self):
