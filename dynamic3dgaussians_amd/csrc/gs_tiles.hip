@@ -17,9 +17,13 @@
 //     {L, longest tile, the reference's num_rendered, status, sort-class
 //     prefixes P1, Q1, P2, -} -- the one device->host read of the forward
 //     (the reference's num_rendered read, :287).
-//  2. bucket (tile_hist_kernel<WRITE>): the same walk, each instance taking
-//     a slot from an LDS cursor, writes a 64-bit (depth bits << 32 | id) key
-//     into its tile's segment -- the order inside a segment is arbitrary.
+//  2. bucket (tile_bucket_kernel): the same walk, each instance taking a slot
+//     from an LDS cursor in its workgroup's run of its tile (the plan's
+//     per-block counts, scanned), its 64-bit (depth bits << 32 | id) key
+//     staged in LDS; the runs are then copied to their tiles' segments in
+//     order, so consecutive lanes store consecutive keys (a workgroup with
+//     more keys than the LDS holds stores each key where its slot lands,
+//     tile_hist_kernel<true>) -- the order inside a segment is arbitrary.
 //  3. sort   (tile_sort_kernel): one workgroup per tile sorts its segment by
 //     the full key.  Common case, an MSD bucket sort: the top bits of the
 //     tile's depth-bit span pick one of 1,024 buckets (LDS atomics give each
