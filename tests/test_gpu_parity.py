@@ -88,7 +88,11 @@ def test_radix_sort_stable(n, end_bit):
     dict(use_sh=True, sh_degree=3), dict(use_cov=True), dict(W=100, H=75, cam_index=5),
     dict(cx=40.0, cy=70.0, W=128, H=96),
     # tiles longer than the LDS sort (> 8192 instances): the global-memory path
-    dict(P=20000, W=48, H=32), dict(P=30000, W=48, H=32), dict(P=60000, W=80, H=48)])
+    dict(P=20000, W=48, H=32), dict(P=30000, W=48, H=32), dict(P=60000, W=80, H=48),
+    # more tiles than one binning pass holds (TB_BINS = 16384): the count and
+    # bucket passes run per tile range; workgroups above and below the staged
+    # bucket's LDS capacity (direct and staged stores)
+    dict(P=20000, W=2112, H=2080)])
 def test_preprocess_and_binning_bitexact(kw):
     inp = H.scene(**{"P": 3000, **kw})
     g = H.gpu_forward(inp)
