@@ -31,6 +31,8 @@
 //                monomials {1, X, Y, X^2, XY, Y^2} (dL/dmean2D, dL/dconic).
 //  * Backward per-Gaussian sums are committed with float atomics per 64-B
 //    accumulation record (10 components) and per feature channel.
+//  * A batch launch deals its cameras to the XCDs in groups of 8 (cam_slot),
+//    so a backward tile's 4 strip workgroups share one XCD's L2.
 #include "gs_common.h"
 #include "gs_kernels.h"
 
@@ -38,7 +40,7 @@ namespace gs {
 
 constexpr float ALPHA_MIN = 1.0f / 255.0f;
 constexpr int CHUNK = 64;
-// Waves per workgroup in the blend kernels.  Each wave owns one 16x4 strip
+// Waves per workgroup in the blend kernels.  Each wave owns one strip
 // and never synchronises with the others.  Measured (bench camera, F = 32):
 // the forward is faster with a tile per workgroup (its 4 waves gather the
 // same records through one CU's L1: 0.202 vs 0.223 ms), the backward with a
