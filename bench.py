@@ -102,7 +102,9 @@ def setup_dist(args):
     # cuda:0 and exchanges the gradient bucket over gloo.
     backend = os.environ.get("GS_BENCH_BACKEND", "nccl")
     dev_index = 0 if os.environ.get("GS_BENCH_SHARE_GPU") == "1" else local
-    if world > 1:
+    # GS_BENCH_FORCE_DIST=1 (one-GPU rehearsal of the RCCL calls: RCCL refuses
+    # two ranks on one device): a process group even at WORLD_SIZE 1
+    if world > 1 or os.environ.get("GS_BENCH_FORCE_DIST") == "1":
         torch.cuda.set_device(dev_index)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
@@ -373,7 +375,15 @@ def cpu_baseline(args, params, label, cam, settings, dev):
 
 def main():
     args = parse()
+    # The bench line is the only output on stdout: native libraries may print
+    # there (RCCL writes a version banner on rank 0 when the communicator
+    # comes up), so fd 1 goes to stderr for the run and the line is written
+    # to the saved descriptor.
+    sys.stdout.flush()
+    line_fd = os.dup(1)
+    os.dup2(2, 1)
     world, rank, dev = setup_dist(args)
+    dist_on = dist.is_initialized()
     _lib.load()
     torch.manual_seed(args.seed)
 
@@ -419,7 +429,7 @@ def main():
     # one fill clears it.  N = 1 has no exchange: gradients stay unbound, so
     # autograd hands the backward's tensors to the leaves without the six
     # accumulate kernels and the fill (-0.06 ms per step).
-    bucket = GradBucket(params, bind_grads=world > 1)
+    bucket = GradBucket(params, bind_grads=dist_on)
     g = torch.Generator(device=dev).manual_seed(1 + rank)
     H_, W_ = args.height, args.width
     up_color = torch.randn(3, H_, W_, device=dev, generator=g)
@@ -527,7 +537,7 @@ def main():
     stage_ms = {k: v[0] for k, v in all_stages.items()}
     dom = max(stage_ms, key=stage_ms.get)
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     _lib.timing_enable(True, stages=[dom])
@@ -537,13 +547,13 @@ def main():
         step()
         host_marks.append(time.perf_counter())
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     stages = _lib.timing_read()
     _lib.timing_enable(False)
-    if world > 1:
+    if dist_on:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -554,17 +564,17 @@ def main():
     for _ in range(args.warmup):
         step(other)
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     t1 = time.perf_counter()
     for _ in range(args.steps):
         step(other)
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     other_elapsed = time.perf_counter() - t1
-    if world > 1:
+    if dist_on:
         t = torch.tensor([other_elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         other_elapsed = float(t.item())
@@ -573,18 +583,18 @@ def main():
         for _ in range(args.warmup):
             fn()
         torch.cuda.synchronize()
-        if world > 1:
+        if dist_on:
             dist.barrier()
         torch.cuda.synchronize()
         ta = time.perf_counter()
         for _ in range(args.steps):
             fn()
         torch.cuda.synchronize()
-        if world > 1:
+        if dist_on:
             dist.barrier()
         torch.cuda.synchronize()
         el = time.perf_counter() - ta
-        if world > 1:
+        if dist_on:
             t = torch.tensor([el], device=dev, dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el = float(t.item())
@@ -671,8 +681,9 @@ def main():
         result["psnr_vs_oracle_db"] = round(psnr, 2) if np.isfinite(psnr) else "inf"
         result["psnr_vs_gt_db"] = psnr_gt
     if rank == 0:
-        print(json.dumps(result), flush=True)
-    if world > 1:
+        sys.stdout.flush()
+        os.write(line_fd, (json.dumps(result) + "\n").encode())
+    if dist_on:
         dist.barrier()
         dist.destroy_process_group()
 
