@@ -43,7 +43,7 @@ class GradBucket:
     construction, every all_reduce(), and resync() -- call it after changing
     the extras' VALUES identically on every rank outside a step.
 
-    Densification (external.py:202-204, 237-240, 273-275) does not change
+    Densification (external.py:202-204, 273-275) does not change
     values in place: it binds NEW tensors into the variables dict and NEW
     Parameters into the optimizer, with a different Gaussian count.  A bucket
     cannot follow that; all_reduce() and resync() therefore check that every

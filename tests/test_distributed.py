@@ -212,7 +212,7 @@ def test_bucket_detects_replaced_parameter():
 
 def test_bucket_detects_replaced_statistics():
     """The densification reset binds new zero tensors into variables
-    (external.py:237-240 via update_params_and_optimizer / remove_points):
+    (external.py:273-275; remove_points at :202-204):
     a bucket tracking the old statistics must raise."""
     P = 10
     p = torch.zeros(P, requires_grad=True)
