@@ -24,33 +24,21 @@ INCLUDE = os.path.join(REPO, "include")
 OUT_DIR = os.path.join(PKG, "lib")
 BUILD_DIR = os.path.join(OUT_DIR, "obj")
 LIB = os.path.join(OUT_DIR, "libgsplat_hip.so")
-# Build variants: "" = the product library; "stats" adds the blend kernels'
-# work counters (-DGS_STATS, tools/render_stats.py only).
+# Build variants ("" = the product library): see VARIANT_FLAGS.
 VARIANT = os.environ.get("GSPLAT_VARIANT", "")
 if VARIANT:
     LIB = os.path.join(OUT_DIR, f"libgsplat_hip_{VARIANT}.so")
     BUILD_DIR = os.path.join(OUT_DIR, f"obj_{VARIANT}")
-VARIANT_FLAGS = {"": [], "stats": ["-DGS_STATS"], "stamps": ["-DGS_STAMPS"], "stamps_fine": ["-DGS_STAMPS", "-DGS_STAMPS_FINE"],
-                 # timing experiments only (results are wrong by construction)
-                 "exp_nofeat": ["-DGS_EXP_NO_FEAT_ATOMIC"], "exp_noacc": ["-DGS_EXP_NO_ACC_ATOMIC"],
-                 "exp_noatomic": ["-DGS_EXP_NO_FEAT_ATOMIC", "-DGS_EXP_NO_ACC_ATOMIC"],
-                 "exp_occ5": ["-DGS_EXP_FWD_LDS_PAD=18000"], "exp_occ3": ["-DGS_EXP_FWD_LDS_PAD=40000"],
-                 "exp_wg1": ["-DGS_WPB_FWD=1"], "exp_tilegroup": ["-DGS_XCD_TILE_GROUP"], "exp_strip16x4": ["-DGS_STRIP_16X4"], "exp_tb512": ["-DGS_TB_THREADS=512"], "exp_fwd_nopair": ["-DGS_FWD_NO_PAIR"], "exp_acc10": ["-DGS_ACC_STRIDE=10"], "exp_wg4": ["-DGS_WPB_BWD=4"], "exp_bwd_wpe3": ["-DGS_BWD_WPE=3"],  "exp_fwd_wpe5": ["-DGS_FWD_WPE=5"], "exp_fwd_wpe6": ["-DGS_FWD_WPE=6"],
-                 "exp_oldmath": ["-DGS_OLD_MATH"], "exp_oldepi": ["-DGS_OLD_EPILOGUE"], "exp_oldpro": ["-DGS_OLD_PROLOGUE"], "exp_radixsort": ["-DGS_NO_BUCKET_SORT"], "exp_bs8": ["-DGS_BS_BITS=8"], "exp_bs9": ["-DGS_BS_BITS=9"], "exp_bs11": ["-DGS_BS_BITS=11"], "exp_bs12": ["-DGS_BS_BITS=12"],
-                 "exp_ssmall512": ["-DGS_SORT_SMALL=512"], "exp_ssmall768": ["-DGS_SORT_SMALL=768"],
-                 "exp_ssmall1536": ["-DGS_SORT_SMALL=1536"], "exp_cammajor": ["-DGS_CAM_MAJOR"], "exp_camg4": ["-DGS_CAM_GROUP=4"], "exp_camg9": ["-DGS_CAM_GROUP=9"], "exp_camg2": ["-DGS_CAM_GROUP=2"],
-                 "exp_kpt16": ["-DGS_BS_KPT=16"], "exp_bsl10": ["-DGS_BS_BITS_LONG=10"], "exp_bsl12": ["-DGS_BS_BITS_LONG=12"],
-                 "exp_tbb64": ["-DGS_TB_BLOCKS=64"], "exp_tbb128": ["-DGS_TB_BLOCKS=128"], "exp_tbb256": ["-DGS_TB_BLOCKS=256"],
-                 "exp_fulw": ["-DGS_FWD_ULW", "-DGS_FWD_SLAST"],
-                 "exp_ulw": ["-DGS_FWD_ULW", "-DGS_FWD_SLAST", "-DGS_BWD_ULW"],
-                 "exp_bkt_batch": ["-DGS_BUCKET_BATCH"],
-                 "exp_fdummy": ["-DGS_FWD_DUMMY"], "exp_fdummy_ulw": ["-DGS_FWD_DUMMY", "-DGS_FWD_ULW", "-DGS_FWD_SLAST"],
-                 "exp_pb1": ["-DGS_PBWD_GROUP=1"], "exp_pb3": ["-DGS_PBWD_GROUP=3"],
-                 "exp_mid512": ["-DGS_SORT_MID512"], "exp_rs256": ["-DGS_RS_THREADS=256"],
-                 "exp_split2": ["-DGS_SPLIT_PIECES=2"], "exp_bwd_wpe2": ["-DGS_BWD_WPE=2"], "exp_fwd_wpe3": ["-DGS_FWD_WPE=3"],
-                 "exp_fwd_noflush": ["-DGS_EXP_FWD_NO_FLUSH"], "exp_bwd_nomfma": ["-DGS_EXP_BWD_NO_MFMA"],
-                 "exp_noatomic_nomfma": ["-DGS_EXP_NO_FEAT_ATOMIC", "-DGS_EXP_NO_ACC_ATOMIC", "-DGS_EXP_BWD_NO_MFMA"],
-                 "exp_fwd_dma": ["-DGS_FWD_DMA"], "exp_camgrp_all": ["-DGS_CAM_GROUP=64"], "exp_oldsplit": ["-DGS_OLD_SPLIT"], "exp_split_pk": ["-DGS_SPLIT_PK"], "exp_fwd_gather64": ["-DGS_FWD_GATHER64"], "exp_bwd_buffer_atomic": ["-DGS_BWD_BUFFER_ATOMIC"], "exp_bucket_store2": ["-DGS_EXP_BUCKET_STORE2"], "exp_bucket_direct": ["-DGS_BUCKET_DIRECT"]}
+# Build variants: "stats" (work counters of the blend and sort kernels,
+# tools/render_stats.py), "stamps" / "stamps_fine" (per-wave lifetime stamps,
+# tools/batch_steps.py --stamps) and two timing-only removals whose results
+# are wrong by construction (the backward's atomic-free ceiling, DESIGN.md
+# section 4).  A variant name not listed here is a frozen snapshot (e.g. a
+# copy of a previous product library for A/B timing) and is never rebuilt.
+VARIANT_FLAGS = {"": [], "stats": ["-DGS_STATS"], "stamps": ["-DGS_STAMPS"],
+                 "stamps_fine": ["-DGS_STAMPS", "-DGS_STAMPS_FINE"],
+                 "exp_nofeat": ["-DGS_EXP_NO_FEAT_ATOMIC"],
+                 "exp_noatomic": ["-DGS_EXP_NO_FEAT_ATOMIC", "-DGS_EXP_NO_ACC_ATOMIC"]}
 ARCH = os.environ.get("GSPLAT_OFFLOAD_ARCH", "gfx950")
 
 # Per-file flags.  The preprocess kernels are compiled without FMA

@@ -483,13 +483,6 @@ static int backward_impl(const gs_gaussians* g, const gs_camera* cams, int C, co
   const int gx = (W + TILE - 1) / TILE, gy = (H + TILE - 1) / TILE;
   const GeomLayout gl(P);
   const ImgLayout il(W, H);
-#ifdef GS_BWD_BUFFER_ATOMIC
-  // the blend backward's commits address one camera's accumulation records
-  // and the feature gradient rows by 32-bit byte offsets
-  if ((uint64_t)P * ACC_STRIDE * 4u > 0xFFFFFFFFull ||
-      (uint64_t)P * (uint64_t)feature_grad_stride(g->F) * 4u > 0xFFFFFFFFull)
-    return fail(-1, "%lld Gaussians exceed the 4 GiB per-camera gradient tables", (long long)P);
-#endif
   float* acc = static_cast<float*>(scratch);
   (void)hipMemsetAsync(acc, 0, sizeof(float) * (size_t)ACC_STRIDE * P * C, s);
   const bool accumulate = (g->flags & GS_FLAG_ACCUMULATE) != 0;

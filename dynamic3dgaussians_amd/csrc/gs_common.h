@@ -15,15 +15,11 @@ namespace gs {
 constexpr int TILE = 16;
 constexpr int TILE_PIX = TILE * TILE;
 constexpr int WAVE = 64;
-// Strip shape: 8 x 8 (default) or 16 x 4 (-DGS_STRIP_16X4).  A square strip
-// has the shortest perimeter, so fewer Gaussians reach it: on the bench
-// camera 3.43 M (Gaussian, strip) survivors at 8 x 8 vs 3.81 M at 16 x 4 for
-// the same 115 M blended (Gaussian, pixel) pairs (tools/strip_survey.py).
-#ifdef GS_STRIP_16X4
-constexpr int STRIP_W = 16, STRIP_H = 4;
-#else
+// Strip shape: 8 x 8.  A square strip has the shortest perimeter, so fewer
+// Gaussians reach it: on the bench camera 3.43 M (Gaussian, strip) survivors
+// at 8 x 8 vs 3.81 M at 16 x 4 for the same 115 M blended (Gaussian, pixel)
+// pairs (tools/strip_survey.py; 16 x 4 strips measured slower).
 constexpr int STRIP_W = 8, STRIP_H = 8;
-#endif
 constexpr int STRIPS_X = TILE / STRIP_W;  // strips per tile row
 // top-left pixel of strip `s` (0..3) of tile (tx, ty)
 __host__ __device__ inline int strip_x0(int tx, int s) { return tx * TILE + (s % STRIPS_X) * STRIP_W; }
@@ -55,10 +51,7 @@ enum AccField {
 // A Gaussian's accumulation record occupies one aligned 64-B segment: float
 // atomics execute at the memory side per 64-B segment, so a record that
 // straddles two segments costs two requests per commit.
-#ifndef GS_ACC_STRIDE
-#define GS_ACC_STRIDE 16
-#endif
-constexpr int ACC_STRIDE = GS_ACC_STRIDE;
+constexpr int ACC_STRIDE = 16;
 
 constexpr int COMPAT_REFERENCE = 0;
 constexpr int COMPAT_FIXED = 1;
@@ -86,14 +79,8 @@ __host__ __device__ inline int64_t sort_blocks(int64_t n) {
 // runs make longer coalesced stores -- bench step duplicate 0.253-0.260 vs
 // 0.341-0.343 ms and scan 0.091 vs 0.121 at 256 (profiles/r03w_ab_tbb128.log);
 // the bench camera's ~13 k keys per workgroup fit the LDS.
-#ifndef GS_TB_BLOCKS
-#define GS_TB_BLOCKS 128
-#endif
-constexpr int TB_BLOCKS = GS_TB_BLOCKS;  // per camera; a multiple of 64 (tile_rowscan_kernel, tile_offsets_kernel)
-#ifndef GS_TB_THREADS
-#define GS_TB_THREADS 1024
-#endif
-constexpr int TB_THREADS = GS_TB_THREADS;
+constexpr int TB_BLOCKS = 128;  // per camera; a multiple of 64 (tile_rowscan_kernel, tile_offsets_kernel)
+constexpr int TB_THREADS = 1024;
 constexpr int TB_BINS = 16384;    // LDS tile bins per pass (64 KiB)
 constexpr int TS_CAP = 3584;      // per-tile LDS sort capacity (2 x 28 KiB of u64 keys)
 constexpr int TS_CAP_LONG = 9600; // long-tile launch: 2 x 75 KiB (+ 8 KiB radix state), one workgroup per CU
@@ -229,25 +216,10 @@ __device__ inline bool rect_culled(float mx, float my, float a, float b, float c
 // bwd 292 vs 274 us): it hands each XCD a horizontal band of the image, and
 // the bands through the scene centre carry most of the blend work, so the
 // XCDs owning them finish last.  Plain dispatch order interleaves tiles over
-// the XCDs (tile % 8 with a tile per workgroup) and balances the load.
-//
-// GS_XCD_TILE_GROUP (experiment): keep a tile's 4 strip workgroups on one XCD
-// (one L2 fill of the tile's records instead of up to 4) while tiles stay
-// interleaved over the XCDs.  Bijective: the tail (tiles past the last full
-// group of 8) keeps plain order.
-__device__ inline int strip_item(int bid, int num_tiles, int wpb) {
-#ifdef GS_XCD_TILE_GROUP
-  if (wpb == 1) {
-    const int full = (num_tiles / 8) * 8;
-    if (bid < full * 4) {
-      const int xcd = bid % 8, slot = bid / 8;
-      return ((slot / 4) * 8 + xcd) * 4 + (slot % 4);
-    }
-  }
-#endif
-  (void)num_tiles;
-  return bid * wpb;
-}
+// the XCDs (tile % 8 with a tile per workgroup) and balances the load.  (The
+// wave-per-workgroup backward keeps a tile's 4 strip workgroups on one XCD:
+// strip_of_block, gs_render.hip.)
+__device__ inline int strip_item(int bid, int wpb) { return bid * wpb; }
 
 __device__ inline float bits_f(uint32_t u) { return __uint_as_float(u); }
 __device__ inline uint32_t f_bits(float f) { return __float_as_uint(f); }

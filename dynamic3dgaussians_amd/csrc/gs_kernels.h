@@ -168,8 +168,8 @@ void launch_tile_order(const TileArgs& a, const CamBatch& cb, hipStream_t s);
 // max_len: the longest tile over the batch (-1: unknown); L: the batch's total instances
 // Dispatch-order extents of the sort's length classes over the batch (plan
 // header M_SORT_*: p1 / p2 = max over cameras of the prefixes holding every
-// tile longer than GS_SORT_SMALL / TS_CAP, q1 = min over cameras of the
-// prefix of tiles known to be longer than GS_SORT_SMALL); valid = false:
+// tile longer than SORT_SMALL / TS_CAP, q1 = min over cameras of the
+// prefix of tiles known to be longer than SORT_SMALL); valid = false:
 // every class launch covers all tiles.
 struct SortClasses {
   bool valid = false;

@@ -422,10 +422,7 @@ __device__ inline void cov3d_bwd(V3 scale, float mod, float4 rot, const float d[
 // per output), so a batch costs one pass over the Gaussian state instead of
 // C read-modify-write passes.  Every output element is written, so outputs
 // need no zero-fill.
-#ifndef GS_PBWD_GROUP
-#define GS_PBWD_GROUP 2
-#endif
-constexpr int PB_GROUP = GS_PBWD_GROUP;  // cameras whose operands are requested together
+constexpr int PB_GROUP = 2;  // cameras whose operands are requested together
 // SH: the SH-coefficient backward is compiled in (launched when a.shs is set);
 // the precomputed-colour instantiation carries none of its registers.
 template <bool SH>

@@ -8,7 +8,7 @@
 //    gs_common.h); one wave64 owns a strip (lane = pixel) and walks the
 //    tile's depth-sorted list on its own -- no block barriers, every wave
 //    exits when its own pixels are done.  The forward packs a tile's 4 waves
-//    into one workgroup (GS_WPB_FWD), the backward runs a wave per workgroup.
+//    into one workgroup (WPB_FWD), the backward runs a wave per workgroup.
 //  * The list is consumed in chunks of 64: lane j gathers the 64-B render
 //    record (gs_common.h R_*) of the chunk's j-th Gaussian (prefetched one
 //    chunk ahead, ids two chunks ahead), tests it against the wave's strip
@@ -46,12 +46,8 @@ constexpr int CHUNK = 64;
 // same records through one CU's L1: 0.202 vs 0.223 ms), the backward with a
 // wave per workgroup (its 12 KiB of LDS are released the moment its strip is
 // done: 0.330 vs 0.342 ms).
-#ifndef GS_WPB_FWD
-#define GS_WPB_FWD 4
-#endif
-#ifndef GS_WPB_BWD
-#define GS_WPB_BWD 1
-#endif
+constexpr int WPB_FWD = 4;
+constexpr int WPB_BWD = 1;
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float float4_t __attribute__((ext_vector_type(4)));
 
@@ -68,27 +64,44 @@ __device__ inline uint64_t clamp_u32(uint64_t v) { return v < 0xFFFFFFFFull ? v 
 // (profiles/r03n_*): render_bwd HBM reads 6.3 vs 20.1 GB per launch against
 // all 27 cameras interleaved (each tile's strips then sat on 4 different XCDs
 // and fetched the tile's records 4 times), 5.26-5.39 vs 5.30-5.45 ms.
-// Camera-major order (GS_CAM_MAJOR: all of camera 0's workgroups, then
-// camera 1's, ...) measured 5.55 vs 5.23 ms: every strip in flight adds into
+// Camera-major order (all of camera 0's workgroups, then camera 1's, ...)
+// measured 5.55 vs 5.23 ms: every strip in flight adds into
 // the same camera's accumulation records and the contended float atomics
 // cost more than the locality gains.  A final group of C % 8 cameras is
 // interleaved the same way without the one-camera-per-XCD property.
-#ifndef GS_CAM_GROUP
-#define GS_CAM_GROUP 8  // cameras interleaved at a time (8 = one per XCD)
-#endif
+constexpr int CAM_GROUP = 8;  // cameras interleaved at a time (8 = one per XCD)
 __device__ inline void cam_slot(int bid, int C, int per_cam, int& cam, int& slot) {
-#ifdef GS_CAM_MAJOR
-  (void)C;
-  cam = bid / per_cam;
-  slot = bid - cam * per_cam;
-#else
-  // groups of GS_CAM_GROUP cameras one after the other, camera-minor inside
-  const int G = GS_CAM_GROUP < C ? GS_CAM_GROUP : C;
+  // groups of CAM_GROUP cameras one after the other, camera-minor inside
+  const int G = CAM_GROUP < C ? CAM_GROUP : C;
   const int grp = bid / (G * per_cam), r = bid - grp * G * per_cam;
   const int g0 = grp * G, gn = C - g0 < G ? C - g0 : G;  // the last group may be smaller
   cam = g0 + r % gn;
   slot = r / gn;
-#endif
+}
+// Workgroup -> (camera, strip item) of the wave-per-workgroup backward.  A
+// (camera, tile) unit is 4 strip workgroups, and those 4 must sit on one XCD
+// (one L2 fill of the tile's records and feature rows).  Units are dealt
+// 8 at a time, one per XCD: the k-th group of 8 units is blocks 32k .. 32k+31,
+// unit 8k + x on XCD x (blocks 32k + 8s + x, s = strip).  Units are ordered
+// by cam_slot (groups of 8 cameras, camera-minor), so for C >= 8 this is the
+// same block order as cam_slot over strips, and for C < 8 (an 8-rank split:
+// 3-4 cameras per rank) XCD x renders camera x % C instead of every tile's
+// strips straddling 2 XCDs.  The last U % 8 units keep plain order.
+__device__ inline void strip_of_block(int bid, int C, int num_tiles, int& cam, int& item) {
+  const int U = C * num_tiles, full = U & ~7;
+  int u, s;
+  if (bid < 4 * full) {
+    const int x = bid & 7, q = bid >> 3;
+    s = q & 3;
+    u = ((q >> 2) << 3) + x;
+  } else {
+    const int r = bid - 4 * full;
+    u = full + (r >> 2);
+    s = r & 3;
+  }
+  int tslot;
+  cam_slot(u, C, num_tiles, cam, tslot);
+  item = tslot * 4 + s;
 }
 template <class A>
 __device__ inline int num_tiles_of(const A& a) { return a.num_tiles; }
@@ -167,10 +180,6 @@ extern "C" int gs_stamps_set(void* buf, long long bwd_off) {
 #define STAMP(v) ((void)0)
 #endif
 
-// exp(x) as one v_exp_f32 (2^x) on x*log2(e): ~3 ulp instead of libm's
-// correctly-rounded-ish 14-instruction sequence.  Forward and backward use
-// the same function, so their alpha decisions agree bit for bit.
-__device__ inline float fast_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
 // 1/x as one v_rcp_f32 (1 ulp).
 __device__ inline float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
 
@@ -217,14 +226,9 @@ __device__ inline RecRegs load_rec(const uint32_t* __restrict__ point_list, cons
 // backward kernel, so both make bit-identical alpha decisions.
 // The exponent is carried in base 2: the half conic is scaled by log2(e) once
 // per record, so alpha = opacity * 2^power' costs one v_exp_f32 and no
-// multiply per pixel (GS_OLD_MATH: natural-base exponent, exp(x) = 2^(x log2 e)).
-#ifdef GS_OLD_MATH
-constexpr float HC_SCALE = 1.0f;
-__device__ inline float gauss_exp(float p) { return fast_exp(p); }
-#else
+// multiply per pixel.
 constexpr float HC_SCALE = 1.4426950408889634f;
 __device__ inline float gauss_exp(float p) { return __builtin_amdgcn_exp2f(p); }
-#endif
 __device__ inline float4 half_conic(const float4& q0, const float4& q1) {
   return make_float4((-0.5f * HC_SCALE) * q0.z, -HC_SCALE * q0.w, (-0.5f * HC_SCALE) * q1.x, 0.0f);
 }
@@ -249,12 +253,9 @@ __device__ inline bool strip_culled(const RecRegs& q, float sx0, float sx1, floa
 // i + j < NSP (NSP = 3: 6 products; the dropped ones are <= 2^-26 |ab|, under
 // fp32's own 2^-24 rounding of a product), smallest first, into the fp32
 // accumulator.  Each bf16 x bf16 product is exact in fp32.
-// GS_SPLIT_PIECES=2 is the round-2 two-piece split (3 products, ~2^-17 per
-// product), kept for timing comparisons only.
-#ifndef GS_SPLIT_PIECES
-#define GS_SPLIT_PIECES 3
-#endif
-constexpr int NSP = GS_SPLIT_PIECES;
+// (Round 2 used a two-piece split: 3 products, ~2^-17 per product; DESIGN.md
+// section 4.)
+constexpr int NSP = 3;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 struct bsplit {
   bf16x8 p[NSP];
@@ -277,7 +278,7 @@ __device__ inline f32x16 mfma_bf16(const bf16x8& a, const bf16x8& b, f32x16 c) {
 // price and cost registers: F = 32 forward 126 VGPRs and no scratch vs 128
 // and 24 B).  27-camera step (profiles/r03q_ab_split.log): render_fwd
 // 3.21-3.30 vs 3.44-3.48 ms per-element, render_bwd 5.02-5.06 vs 5.24-5.35;
-// the v_pk_add_f32 pairing (GS_SPLIT_PK) 3.37-3.40 / 5.04-5.11.
+// the v_pk_add_f32 pairing 3.37-3.40 / 5.04-5.11.
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -286,29 +287,13 @@ __device__ inline uint32_t cvt_pk_bf16(float a, float b) {
 }
 __device__ inline float bf16_lo(uint32_t u) { return __uint_as_float(u << 16); }
 __device__ inline float bf16_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
-#ifndef GS_SPLIT_PK
 // the remainders with one v_sub_f32 each (no packed fp32 pairing)
 __device__ inline float split_sub(float a, float h) {
   float r;
   asm("v_sub_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(h));
   return r;
 }
-#else
-__device__ inline float split_sub(float a, float h) { return a - h; }
-#endif
 __device__ inline void split_bf16(const float (&x)[8], bsplit& s) {
-#ifdef GS_OLD_SPLIT
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    float r = x[j];
-#pragma unroll
-    for (int i = 0; i < NSP; ++i) {
-      const __bf16 h = (__bf16)r;
-      s.p[i][j] = h;
-      if (i + 1 < NSP) r -= (float)h;
-    }
-  }
-#else
   u32x4 w[NSP];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -325,7 +310,6 @@ __device__ inline void split_bf16(const float (&x)[8], bsplit& s) {
   }
 #pragma unroll
   for (int i = 0; i < NSP; ++i) s.p[i] = __builtin_bit_cast(bf16x8, w[i]);
-#endif
 }
 // c += a * b over the split pieces (i + j < NSP), the smallest products first
 template <class Acc>
@@ -345,14 +329,6 @@ __device__ inline Acc mfma_split_x(const bsplit& a, const float (&x)[8], Acc c) 
   for (int e = 0; e < 8; ++e) r[e] = x[e];
 #pragma unroll
   for (int j = 0; j < NSP; ++j) {
-    bf16x8 b;
-#ifdef GS_OLD_SPLIT
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      b[e] = (__bf16)r[e];
-      if (j + 1 < NSP) r[e] -= (float)b[e];
-    }
-#else
     u32x4 w;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -363,8 +339,7 @@ __device__ inline Acc mfma_split_x(const bsplit& a, const float (&x)[8], Acc c) 
         r[2 * e + 1] = split_sub(r[2 * e + 1], bf16_hi(u));
       }
     }
-    b = __builtin_bit_cast(bf16x8, w);
-#endif
+    const bf16x8 b = __builtin_bit_cast(bf16x8, w);
 #pragma unroll
     for (int i = 0; i + j < NSP; ++i) c = mfma_bf16(a.p[i], b, c);
   }
@@ -385,21 +360,17 @@ __device__ inline Acc mfma_exact_split(const bf16x8& a, const bsplit& b, Acc c) 
 // at 130 registers = 3 waves), else the compiler's choice.
 template <int F>
 constexpr int fwd_waves_per_simd() {
-#ifdef GS_FWD_WPE
-  return GS_FWD_WPE;
-#else
   return F == 32 ? 4 : F == 36 ? 3 : 1;  // F = 36: 0.188 vs 0.205 ms per camera at 4 (spills)
-#endif
 }
 template <int F, int COMPAT>
-__global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu(fwd_waves_per_simd<F>(), 8))) void render_fwd_kernel(
+__global__ __launch_bounds__(64 * WPB_FWD) __attribute__((amdgpu_waves_per_eu(fwd_waves_per_simd<F>(), 8))) void render_fwd_kernel(
     RenderArgs a0, CamBatch cb) {
   // camera c of the batch: workgroups are dealt camera-minor (see cam_slot)
   STAMP(ts0);
   int cam, bslot;
-  cam_slot(blockIdx.x, cb.C, num_tiles_of(a0) * 4 / GS_WPB_FWD, cam, bslot);
+  cam_slot(blockIdx.x, cb.C, num_tiles_of(a0) * 4 / WPB_FWD, cam, bslot);
   const RenderArgs ca = cam_render_args(a0, cb, cam);
-  const int W = ca.W, H = ca.H, grid_x = ca.grid_x, num_tiles = ca.num_tiles;
+  const int W = ca.W, H = ca.H, grid_x = ca.grid_x;
   const uint4* __restrict__ order = ca.order;
   const uint32_t* __restrict__ point_list = ca.point_list;
   const float* __restrict__ rec = ca.rec;
@@ -427,35 +398,13 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
   constexpr int NSF = (!MF && F > 0) ? F : (FT > 0 ? FT : 1);
   constexpr int WBF = 16;                    // Gaussians per matrix batch
   // per record: (x, y, -a/2, -b) (-c/2, opacity, r, g) (b, depth, -, -)
-#ifdef GS_FWD_DUMMY
-  // + slot CHUNK: an empty record (zero conic and opacity: power 0, alpha 0)
-  // standing in for the missing second survivor of a pair
-  __shared__ float4 s_rec[GS_WPB_FWD][CHUNK + 1][3];
-#else
-  __shared__ float4 s_rec[GS_WPB_FWD][CHUNK][3];
-#endif
+  __shared__ float4 s_rec[WPB_FWD][CHUNK][3];
   // batch weights [slot][pixel] (row pad 4: conflict-free writes and reads)
-  __shared__ float s_fw[GS_WPB_FWD][MF ? WBF + 1 : 1][68];  // +1: a pair may overfill by one
-#ifdef GS_FWD_DMA
-  // Experiment (measured, not kept: render_fwd 3.50 vs 3.42 ms per 27-camera
-  // launch, profiles/r03m_ab_fwd_dma.log): the batch Gaussians' feature rows
-  // copied global -> LDS by an LDS-DMA (global_load_lds_dword) the moment a
-  // Gaussian is parked, instead of the gather at the flush.
-  constexpr bool FDMA = MF;
-#else
-  constexpr bool FDMA = false;
-#endif
-  __shared__ float s_ff[GS_WPB_FWD][FDMA ? WBF + 1 : 1][FDMA ? 32 * FB : 1];
+  __shared__ float s_fw[WPB_FWD][MF ? WBF + 1 : 1][68];  // +1: a pair may overfill by one
 
   // strip item = tile * 4 + wave (dispatch order, see strip_item)
-#ifdef GS_FWD_ULW
-  // the wave's LDS slot as a scalar: LDS addresses of the survivors' records
-  // become scalar arithmetic
-  const int lane = threadIdx.x & 63, lw = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-#else
   const int lane = threadIdx.x & 63, lw = threadIdx.x >> 6;  // lw: LDS slot of the wave
-#endif
-  const int item = strip_item(bslot, num_tiles, GS_WPB_FWD) + lw;
+  const int item = strip_item(bslot, WPB_FWD) + lw;
   const uint4 trec = tile_rec(order, item >> 2);
   const int tile = (int)trec.x, wave = item & 3;
   const int tx = tile % grid_x, ty = tile / grid_x;
@@ -466,9 +415,6 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
   const float sx0 = (float)qx0, sx1 = sx0 + (float)(STRIP_W - 1);
   const float sy0 = (float)qy0, sy1 = sy0 + (float)(STRIP_H - 1);
   const uint2 range = make_uint2(trec.y, trec.z);
-#ifdef GS_FWD_DUMMY
-  if (lane < 3) s_rec[lw][CHUNK][lane] = make_float4(0.f, 0.f, 0.f, 0.f);
-#endif
 
   float T = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f, Dp = 0.f;
   float SF[NSF];
@@ -488,36 +434,18 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
   // Contract the batch's nb Gaussians.  A[ch][k] = feat[gid_k][32 fb + ch]
   // (lane l: channel l&31, k = 8(l>>5) + j), B[k][pix] = w[k][pix] (lane l:
   // pixel (l&31) + 32 blk); slots k >= nb are zeroed on both sides.
-  // Park Gaussian g's feature rows as batch slot k: LDS-DMA into s_ff[k]
-  // (lane l copies channel l of the matrix blocks), or remember the id for
-  // the flush's gather.
-  auto park_row = [&](uint32_t g, int k) {
-    if constexpr (FDMA) {
-      if (lane < 32 * FB)
-        __builtin_amdgcn_global_load_lds(
-            (const __attribute__((address_space(1))) void*)(feats + (size_t)g * F + lane),
-            (__attribute__((address_space(3))) void*)&s_ff[lw][k][0], 4, 0, 0);
-    } else {
-      gidv = lane == k ? g : gidv;
-    }
-  };
+  // Park Gaussian g's feature rows as batch slot k: remember the id for the
+  // flush's gather.  (Copying the rows to LDS by LDS-DMA at park time was
+  // measured slower: DESIGN.md section 4.)
+  auto park_row = [&](uint32_t g, int k) { gidv = lane == k ? g : gidv; };
   // feature rows addressed by unsigned 32-bit byte offsets through a buffer
-  // resource over the P x F table (the host refuses tables over 4 GiB);
-  // GS_FWD_GATHER64: 64-bit pointer arithmetic per row (3 more vector
-  // instructions per row and spilled registers at the 128-VGPR cap)
-#ifdef GS_FWD_GATHER64
-  constexpr bool fbuf = false;
-#else
-  constexpr bool fbuf = MF;
-#endif
+  // resource over the P x F table (the host refuses tables over 4 GiB): 64-bit
+  // pointer arithmetic per row cost 3 more vector instructions per row and
+  // spilled registers at the 128-VGPR cap
   const uint64_t fbytes = (uint64_t)ca.P * F * 4u;
   const auto frsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(feats), (short)0,
                                                        (int)(uint32_t)clamp_u32(fbytes), 0x00020000);
   auto flush = [&](int n) {
-#ifdef GS_EXP_FWD_NO_FLUSH
-    // timing only (results wrong): the batch is dropped uncontracted
-    if (n >= 0) return;
-#endif
     // an opaque copy of the lane index keeps the compiler from hoisting the
     // flush's address arithmetic into loop-long registers
     int ln = lane;
@@ -531,32 +459,15 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
       bsplit A;
       {
         float fa[8];
-        if constexpr (FDMA) {
-          // the parked rows' DMAs have landed (issued at park time)
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // 32-bit row offsets through a buffer resource: one address
+        // instruction per row instead of 64-bit pointer arithmetic
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const int k = 8 * h + j;
-            fa[j] = k < n ? s_ff[lw][k][fb * 32 + (ln & 31)] : 0.f;
-          }
-        } else if (fbuf) {
-          // 32-bit row offsets through a buffer resource: one address
-          // instruction per row instead of 64-bit pointer arithmetic
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const int k = 8 * h + j;
-            const uint32_t g = (uint32_t)__shfl((int)gidv, k, 64);
-            const uint32_t off = (g * (uint32_t)F + (uint32_t)(fb * 32 + (ln & 31))) * 4u;
-            const float v = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(frsrc, (int)off, 0, 0));
-            fa[j] = k < n ? v : 0.f;
-          }
-        } else {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const int k = 8 * h + j;
-            const uint32_t g = (uint32_t)__shfl((int)gidv, k, 64);
-            fa[j] = k < n ? feats[(size_t)g * F + fb * 32 + (ln & 31)] : 0.f;
-          }
+        for (int j = 0; j < 8; ++j) {
+          const int k = 8 * h + j;
+          const uint32_t g = (uint32_t)__shfl((int)gidv, k, 64);
+          const uint32_t off = (g * (uint32_t)F + (uint32_t)(fb * 32 + (ln & 31))) * 4u;
+          const float v = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(frsrc, (int)off, 0, 0));
+          fa[j] = k < n ? v : 0.f;
         }
         split_bf16(fa, A);
       }
@@ -602,19 +513,12 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
     }
     const uint32_t chunk_gid = q.gid;  // lane j: id of the chunk's j-th record
     uint64_t mask = __ballot(keep);
-#ifdef GS_FWD_SLAST
-    // list position (+1) of the chunk's first record as a scalar: a blending
-    // survivor's `last` is one select against an SGPR, no vector add
-    const uint32_t lbase = __builtin_amdgcn_readfirstlane(c0 - range.x + 1);
-#else
     const uint32_t lbase = c0 - range.x + 1;
-#endif
     STAT(0, 1);
     STAT(1, range.y - c0 < CHUNK ? range.y - c0 : CHUNK);
     STAT(2, __builtin_popcountll(mask));
     q = load_rec_gid(rec, gnext);                                 // next chunk (clamped)
     gnext = load_gid(point_list, c0 + 2 * CHUNK + lane, lastv);    // the one after
-#ifndef GS_FWD_NO_PAIR
     if constexpr (F == 0 || MF) {
       // Two survivors per iteration: their exponents are evaluated side by
       // side (independent work for the issue slots), then blended in order.
@@ -651,11 +555,7 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
         const int ja = __builtin_ctzll(mask);
         mask &= mask - 1;
         const bool two = mask != 0;
-#ifdef GS_FWD_DUMMY
-        const int jb = two ? __builtin_ctzll(mask) : CHUNK;
-#else
         const int jb = two ? __builtin_ctzll(mask) : ja;
-#endif
         if (two) mask &= mask - 1;
         STAT(3, two ? 2 : 1);
         // the survivors' tail feature rows (scalar loads), requested before
@@ -671,9 +571,7 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
         const float4 b0 = s_rec[lw][jb][0], b1 = s_rec[lw][jb][1], b2 = s_rec[lw][jb][2];
         const float pa = gauss_power(a0.x - pfx, a0.y - pfy, make_float4(a0.z, a0.w, a1.x, 0.f));
         float pb = gauss_power(b0.x - pfx, b0.y - pfy, make_float4(b0.z, b0.w, b1.x, 0.f));
-#ifndef GS_FWD_DUMMY
         pb = two ? pb : 1.0f;
-#endif
         const float ala = fminf(0.99f, a1.y * gauss_exp(pa));
         const float alb = fminf(0.99f, b1.y * gauss_exp(pb));
         blend_step(ja, a1, a2, pa, ala, fta);
@@ -683,22 +581,15 @@ __global__ __launch_bounds__(64 * GS_WPB_FWD) __attribute__((amdgpu_waves_per_eu
             flush(WBF);
             if (nb > WBF) {
               s_fw[lw][0][lane] = s_fw[lw][WBF][lane];
-              if constexpr (FDMA) {
-                // the 17th row (landed: the flush waited) moves to slot 0
-                if (lane < 32 * FB) s_ff[lw][0][lane] = s_ff[lw][WBF][lane];
-              } else {
-                const uint32_t g16 = __builtin_amdgcn_readlane(gidv, WBF);
-                gidv = lane == 0 ? g16 : gidv;
-              }
+              const uint32_t g16 = __builtin_amdgcn_readlane(gidv, WBF);
+              gidv = lane == 0 ? g16 : gidv;
             }
             nb -= WBF;
           }
         }
         if (!wave_any(live != 0u)) goto blend_done;
       }
-    } else
-#endif
-    {
+    } else {
     while (mask) {
       const int j = __builtin_ctzll(mask);
       mask &= ~(1ull << j);
@@ -805,14 +696,12 @@ blend_done:
     // channel fb*32 + (r&3) + 8(r>>2) + 4(l>>5), strip pixel (l&31) + 32 blk.
     float t_lo, t_hi;
     swap32(T, T, t_lo, t_hi);  // T of strip pixel (l&31) and (l&31)+32
-#ifndef GS_OLD_EPILOGUE
     // Buffer stores: one per-lane byte offset (pixel + the lane's channel
     // quarter) and the register's channel in the scalar offset, so the 16 x FB
     // stores per pixel cost no address arithmetic on the vector ALUs.
     const bool small = (uint64_t)F * HW * 4u < 0x7FFFFFFFull;
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(out_feature, (short)0,
                                                         small ? (int)((uint64_t)F * HW * 4u) : 0, 0x00020000);
-#endif
 #pragma unroll
     for (int blk = 0; blk < 2; ++blk) {
       const int p = (lane & 31) + 32 * blk;
@@ -820,7 +709,6 @@ blend_done:
       if (qx < W && qy < H) {
         const size_t pix = (size_t)qy * W + qx;
         const float Tp = blk ? t_hi : t_lo;
-#ifndef GS_OLD_EPILOGUE
         if (small) {
           const uint32_t voff = (uint32_t)(pix + (size_t)(4 * (lane >> 5)) * HW) * 4u;
 #pragma unroll
@@ -835,7 +723,7 @@ blend_done:
             }
           continue;
         }
-#endif
+        // images over 2 GiB of features: 64-bit addresses
 #pragma unroll
         for (int fb = 0; fb < FB; ++fb)
 #pragma unroll
@@ -851,7 +739,7 @@ blend_done:
   STAMP(ts3);
   __builtin_amdgcn_s_waitcnt(0);
   STAMP(ts4);
-  stamp_store((long long)blockIdx.x * GS_WPB_FWD + lw, ts1 - ts0, ts2 - ts0, ts3 - ts0, ts4 - ts0);
+  stamp_store((long long)blockIdx.x * WPB_FWD + lw, ts1 - ts0, ts2 - ts0, ts3 - ts0, ts4 - ts0);
 #endif
 }
 
@@ -883,21 +771,18 @@ __device__ inline int sw_idx(int r, int c) { return r * 64 + ((((c >> 2) ^ r) & 
 // render_bwd 6.0 ms at 2 waves vs 5.45 at 3; the widest instantiations keep 2.
 template <int F, int COMPAT>
 constexpr int bwd_waves_per_simd() {
-#ifdef GS_BWD_WPE
-  return GS_BWD_WPE;
-#else
   return (F < 32 || (F == 32 && COMPAT == COMPAT_REFERENCE)) ? 3 : 2;
-#endif
 }
 template <int F, int COMPAT>
-__global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu(bwd_waves_per_simd<F, COMPAT>(), 8))) void render_bwd_kernel(
+__global__ __launch_bounds__(64 * WPB_BWD) __attribute__((amdgpu_waves_per_eu(bwd_waves_per_simd<F, COMPAT>(), 8))) void render_bwd_kernel(
     RenderBwdArgs a0, CamBatch cb) {
   // camera c of the batch: workgroups are dealt camera-minor (see cam_slot)
   STAMP(ts0);
+  static_assert(WPB_BWD == 1, "strip_of_block maps one strip per workgroup");
   int cam, bslot;
-  cam_slot(blockIdx.x, cb.C, num_tiles_of(a0) * 4 / GS_WPB_BWD, cam, bslot);
+  strip_of_block(blockIdx.x, cb.C, num_tiles_of(a0), cam, bslot);
   const RenderBwdArgs ca = cam_render_bwd_args(a0, cb, cam);
-  const int W = ca.W, H = ca.H, grid_x = ca.grid_x, num_tiles = ca.num_tiles;
+  const int W = ca.W, H = ca.H, grid_x = ca.grid_x;
   const uint4* __restrict__ order = ca.order;
   const uint32_t* __restrict__ point_list = ca.point_list;
   const float* __restrict__ rec = ca.rec;
@@ -911,15 +796,6 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
   const float* __restrict__ dL_dalpha = ca.dL_dalpha;
   float* __restrict__ acc = ca.acc;
   float* __restrict__ dsem = ca.dsem;
-#ifdef GS_BWD_BUFFER_ATOMIC
-  // buffer resources over the camera's accumulation records and the feature
-  // gradient rows: the commits' atomics take 32-bit byte offsets (the host
-  // refuses tables over 4 GiB)
-  const auto acc_rsrc = __builtin_amdgcn_make_buffer_rsrc(
-      acc, (short)0, (int)(uint32_t)clamp_u32((uint64_t)ca.P * ACC_STRIDE * 4u), 0x00020000);
-  const auto dsem_rsrc = __builtin_amdgcn_make_buffer_rsrc(
-      dsem, (short)0, (int)(uint32_t)clamp_u32((uint64_t)ca.P * feature_grad_stride(F) * 4u), 0x00020000);
-#endif
   constexpr int WB = 16;                      // Gaussians per matrix batch
   constexpr int CB = F >= 16 ? F / 16 : 0;    // 16-channel feature blocks with their own accumulators
   constexpr int CB1 = CB > 0 ? CB : 1;
@@ -934,8 +810,8 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
   constexpr int FS = feature_grad_stride(F);
   constexpr bool FIXED_FEAT = (COMPAT != COMPAT_REFERENCE) && F > 0;
   // per record: (x, y, -a/2, -b) (-c/2, opacity, r, g) (b, depth, -, -)
-  __shared__ float4 s_rec[GS_WPB_BWD][CHUNK][2];
-  __shared__ float2 s_rec2[GS_WPB_BWD][CHUNK];  // (b, depth)
+  __shared__ float4 s_rec[WPB_BWD][CHUNK][2];
+  __shared__ float2 s_rec2[WPB_BWD][CHUNK];  // (b, depth)
   // Colour block operand rows 0..3 (dL/dC_r,g,b, dL/dD) and the FW <= 4
   // feature rows after them, split, in the A layout: [k-step][piece][row]
   // [pixel group of 8].  Kept in LDS (1.5 / 3 KiB) rather than in 24 VGPRs:
@@ -943,21 +819,17 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
   // colour sums hold copies nobody reads.
   constexpr bool XW_LDS = (FW <= 4);
   constexpr int XR = FW == 0 ? 4 : 8;  // operand rows kept
-  __shared__ bf16x8 s_xw[GS_WPB_BWD][XW_LDS ? 2 : 1][NSP][XR][4];
+  __shared__ bf16x8 s_xw[WPB_BWD][XW_LDS ? 2 : 1][NSP][XR][4];
   // batch weights [slot][pixel]: 64-float rows, 16-B groups XOR-swizzled by
   // the row (sw_idx) so that the flush's 16-row operand reads and the
   // per-lane writes are both conflict-free without padding
-  __shared__ float s_w[GS_WPB_BWD][WB * 64];
-  __shared__ float s_u[GS_WPB_BWD][WB * 64];
-  __shared__ float4 s_slot[GS_WPB_BWD][WB];  // (mean x - cx, mean y - cy, opacity, id bits)
+  __shared__ float s_w[WPB_BWD][WB * 64];
+  __shared__ float s_u[WPB_BWD][WB * 64];
+  __shared__ float4 s_slot[WPB_BWD][WB];  // (mean x - cx, mean y - cy, opacity, id bits)
 
   // strip item = tile * 4 + wave (dispatch order, see strip_item)
-#ifdef GS_BWD_ULW
-  const int lane = threadIdx.x & 63, lw = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-#else
   const int lane = threadIdx.x & 63, lw = threadIdx.x >> 6;  // lw: LDS slot of the wave
-#endif
-  const int item = strip_item(bslot, num_tiles, GS_WPB_BWD) + lw;
+  const int item = strip_item(bslot, WPB_BWD) + lw;
   const uint4 trec = tile_rec(order, item >> 2);
   const int tile = (int)trec.x, wave = item & 3;
   const int tx = tile % grid_x, ty = tile / grid_x;
@@ -985,9 +857,7 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
   const float dLd = inside && dL_ddepth ? dL_ddepth[pix] : 0.f;
   const float dLa = inside && dL_dalpha ? dL_dalpha[pix] : 0.f;
   const float bg_dot = bg[0] * dLp[0] + bg[1] * dLp[1] + bg[2] * dLp[2];
-#ifndef GS_OLD_MATH
   const float tf_bg = T_final * bg_dot;  // the background term's per-pixel factor (exact in reference mode: T_final = 1)
-#endif
   float dLf_own[FIXED_FEAT ? F : 1];  // fixed mode: f . dL/dF feeds dL/dalpha
   if constexpr (FIXED_FEAT) {
 #pragma unroll
@@ -1036,11 +906,7 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
                            reinterpret_cast<uintptr_t>(alphas)) & 15) == 0;
     const bool fast = (W & 3) == 0 && (HW & 3) == 0 && qx0 + STRIP_W <= W && qy0 + STRIP_H <= H &&
                       __ballot(!lane_ok) == 0ull;
-#ifdef GS_OLD_PROLOGUE
-    if (false) {
-#else
     if (fast) {
-#endif
       const float* sp = src ? src : alphas;
       float4 rw[2][2], rf[CB1][2][2];
 #pragma unroll
@@ -1126,12 +992,7 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
     float4_t cf[CB1];
 #pragma unroll
     for (int cb = 0; cb < CB1; ++cb) cf[cb] = float4_t{0.f, 0.f, 0.f, 0.f};
-#ifdef GS_EXP_BWD_NO_MFMA
-    // timing only (results wrong): no splits, no matrix contractions
-    constexpr int NKS = 0;
-#else
-    constexpr int NKS = 2;
-#endif
+    constexpr int NKS = 2;  // k-steps of 32 pixels
 #pragma unroll
     for (int s = 0; s < NKS; ++s) {
       const int p0 = 32 * s + 8 * (lane >> 4);
@@ -1243,24 +1104,13 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
       if (i >= WB * NCOMP) break;
       const int slot = i / NCOMP, comp = i - NCOMP * slot;
       const uint32_t gi = FW > 0 ? f_bits(s_slot[lw][slot].w) : agid[t < NAG ? t : 0];
-#ifndef GS_BWD_BUFFER_ATOMIC
       float* dst = comp < A_FEAT ? acc + (size_t)ACC_STRIDE * gi + comp
                                  : dsem + (size_t)gi * FS + 16 * CB + (comp - A_FEAT);
 #ifdef GS_EXP_NO_ACC_ATOMIC
+      // timing only (results wrong): the atomic-free ceiling
       if (slot < nb && s_out[i] == 12345.f) *dst = 0.f;
 #else
       if (slot < nb) atomicAdd(dst, s_out[i]);
-#endif
-#else
-      // experiment: no-return buffer atomics at 32-bit byte offsets (5.07-5.11
-      // vs 5.06-5.08 ms with global atomics, profiles/r03s_ab_bwd_buffer_atomic.log)
-      if (slot < nb) {
-        if (comp < A_FEAT)
-          (void)__builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(s_out[i], acc_rsrc, (int)((ACC_STRIDE * gi + comp) * 4u), 0, 0);
-        else
-          (void)__builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(
-              s_out[i], dsem_rsrc, (int)((gi * (uint32_t)FS + (uint32_t)(16 * CB + comp - A_FEAT)) * 4u), 0, 0);
-      }
 #endif
     }
     // features: C[slot][ch] = sum_p w[slot][p] dL/dF[p][ch]; lane l holds
@@ -1273,12 +1123,8 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
         const uint32_t gi = fgid[r];
 #ifdef GS_EXP_NO_FEAT_ATOMIC
         if (slot < nb && cf[cb][r] == 12345.f) dsem[(size_t)gi * FS + 16 * cb + g] = 0.f;
-#elif !defined(GS_BWD_BUFFER_ATOMIC)
-        if (slot < nb) atomicAdd(dsem + (size_t)gi * FS + 16 * cb + g, cf[cb][r]);
 #else
-        if (slot < nb)
-          (void)__builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(
-              cf[cb][r], dsem_rsrc, (int)((gi * (uint32_t)FS + (uint32_t)(16 * cb + g)) * 4u), 0, 0);
+        if (slot < nb) atomicAdd(dsem + (size_t)gi * FS + 16 * cb + g, cf[cb][r]);
 #endif
       }
     }
@@ -1327,10 +1173,8 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
       s_rec2[lw][lane] = q.q2;
     }
     const uint32_t chunk_gid = q.gid;  // lane j: id of the chunk's j-th record
-#ifndef GS_OLD_MATH
     // chunk entry j is in front of this pixel's last contributor iff j < lrel
     const int lrel = (int)last - (int)(c0 - range.x);
-#endif
     uint64_t mask = __ballot(keep);
     STAT(8, 1);
     STAT(9, hi - c0);
@@ -1344,7 +1188,6 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
     while (mask) {
       const int j = 63 - __builtin_clzll(mask);
       mask &= ~(1ull << j);
-      const uint32_t k = c0 + j - range.x;  // position in the tile list
       const float4 r0 = s_rec[lw][j][0];
       const float4 r1 = s_rec[lw][j][1];
       const float2 r2 = s_rec2[lw][j];
@@ -1353,12 +1196,7 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
       const float power = gauss_power(dx, dy, make_float4(r0.z, r0.w, r1.x, 0.f));
       const float G = gauss_exp(power);
       const float alpha = fminf(0.99f, op * G);
-#ifdef GS_OLD_MATH
-      const bool valid = (k < last) && !(power > 0.0f) && !(alpha < ALPHA_MIN);
-#else
-      (void)k;
       const bool valid = (j < lrel) && !(power > 0.0f) && !(alpha < ALPHA_MIN);
-#endif
       STAT(11, 1);
       STAT_INC(st_it);
       STAT(12, wave_any(valid));
@@ -1381,11 +1219,7 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
           cdot += fd;
         }
         Q = fmaf(la, lcd - Q, Q);
-#ifdef GS_OLD_MATH
-        const float dL_dopa = fmaf(-T_final * rinv, bg_dot, (cdot - Q) * T);
-#else
         const float dL_dopa = fmaf(-tf_bg, rinv, (cdot - Q) * T);
-#endif
         lcd = cdot;
         la = alpha;
         u = G * dL_dopa;
@@ -1408,7 +1242,7 @@ __global__ __launch_bounds__(64 * GS_WPB_BWD) __attribute__((amdgpu_waves_per_eu
   STAMP(ts3);
   __builtin_amdgcn_s_waitcnt(0);
   STAMP(ts4);
-  stamp_store(g_stamp_bwd_off + (long long)blockIdx.x * GS_WPB_BWD + lw, ts1 - ts0, ts2 - ts0, ts3 - ts0, ts4 - ts0,
+  stamp_store(g_stamp_bwd_off + (long long)blockIdx.x * WPB_BWD + lw, ts1 - ts0, ts2 - ts0, ts3 - ts0, ts4 - ts0,
               tA ? tA - ts0 : 0, tB ? tB - ts0 : 0, tC ? tC - ts0 : 0, tD ? tD - ts0 : 0);
 #endif
 }
@@ -1435,21 +1269,16 @@ void launch_feature_grad_rows(const float* pad, float* out, int64_t P, int F, in
 
 template <int F>
 static void fwd_f(const RenderArgs& a, const CamBatch& cb, hipStream_t s) {
-  dim3 grid(a.num_tiles * (4 / GS_WPB_FWD) * cb.C), block(64 * GS_WPB_FWD);
-#ifdef GS_EXP_FWD_LDS_PAD
-  const size_t pad = GS_EXP_FWD_LDS_PAD;  // occupancy experiment: unused dynamic LDS
-#else
-  const size_t pad = 0;
-#endif
+  dim3 grid(a.num_tiles * (4 / WPB_FWD) * cb.C), block(64 * WPB_FWD);
   if (a.compat == COMPAT_REFERENCE)
-    hipLaunchKernelGGL((render_fwd_kernel<F, COMPAT_REFERENCE>), grid, block, pad, s, a, cb);
+    hipLaunchKernelGGL((render_fwd_kernel<F, COMPAT_REFERENCE>), grid, block, 0, s, a, cb);
   else
     hipLaunchKernelGGL((render_fwd_kernel<F, COMPAT_FIXED>), grid, block, 0, s, a, cb);
 }
 
 template <int F>
 static void bwd_f(const RenderBwdArgs& a, const CamBatch& cb, hipStream_t s) {
-  dim3 grid(a.num_tiles * (4 / GS_WPB_BWD) * cb.C), block(64 * GS_WPB_BWD);
+  dim3 grid(a.num_tiles * (4 / WPB_BWD) * cb.C), block(64 * WPB_BWD);
   if (a.compat == COMPAT_REFERENCE)
     hipLaunchKernelGGL((render_bwd_kernel<F, COMPAT_REFERENCE>), grid, block, 0, s, a, cb);
   else

@@ -44,9 +44,7 @@
 namespace gs {
 
 // tile length up to which the tile sort runs in its short (small-LDS) class
-#ifndef GS_SORT_SMALL
-#define GS_SORT_SMALL 1024
-#endif
+constexpr int SORT_SMALL = 1024;
 
 // Instances of one rect handled by one lane; larger rects are spread over the
 // wave (a full-screen Gaussian must not serialize its wave for 2,500 tiles).
@@ -91,43 +89,10 @@ __global__ __launch_bounds__(TB_THREADS) void tile_hist_kernel(TileArgs a0, CamB
     auto emit = [&](int x, int y, uint64_t k) {
       const uint32_t u = (uint32_t)(y * gx + x - t0);
       if (u < (uint32_t)nt) {
-#ifdef GS_EXP_BUCKET_STORE2
-        // timing only: every key stored twice (same address, same value)
-        if (WRITE) {
-          const uint32_t sl = atomicAdd(&s_bin[u], 1u);
-          *(volatile uint64_t*)&a.keys[sl] = k;
-          *(volatile uint64_t*)&a.keys[sl] = k;
-        }
-#else
         if (WRITE) a.keys[atomicAdd(&s_bin[u], 1u)] = k;
-#endif
         else atomicAdd(&s_bin[u], 1u);
       }
     };
-#ifdef GS_BUCKET_BATCH
-    if (WRITE) {
-      // All of the lane's slot claims first, then all of its key stores: the
-      // returning LDS atomics issue back to back instead of each waiting for
-      // the previous instance's store (one LDS round trip per rect instead of
-      // one per instance).  The wave's longest small rect bounds the unroll.
-      const int nl = (n > 0 && n <= LANE_TILES) ? n : 0;
-      const int nmax = (int)__builtin_amdgcn_readfirstlane(wave_max_u((uint32_t)nl));
-      uint32_t slot[LANE_TILES];
-      int x = x0, y = y0;
-#pragma unroll
-      for (int k = 0; k < LANE_TILES; ++k) {
-        slot[k] = 0xFFFFFFFFu;
-        if (k < nmax) {
-          const uint32_t u = (uint32_t)(y * gx + x - t0);
-          if (k < nl && u < (uint32_t)nt) slot[k] = atomicAdd(&s_bin[u], 1u);
-          if (++x == x0 + w) { x = x0; ++y; }
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < LANE_TILES; ++k)
-        if (k < nmax && slot[k] != 0xFFFFFFFFu) a.keys[slot[k]] = key;
-    } else
-#endif
     if (n > 0 && n <= LANE_TILES) {
       const int h = n / w;
       for (int y = y0; y < y0 + h; ++y)
@@ -159,7 +124,7 @@ __global__ __launch_bounds__(TB_THREADS) void tile_hist_kernel(TileArgs a0, CamB
   }
 }
 
-// Bucket pass with the block's keys staged in LDS (GS_BUCKET_DIRECT: the
+// Bucket pass with the block's keys staged in LDS (the direct pass, the
 // tile_hist_kernel<true> walk above, every key stored where its slot lands).
 // Consecutive lanes of that walk hold unrelated Gaussians, so each key store
 // is its own 8-B request to a different line; storing every key twice cost
@@ -294,13 +259,10 @@ __global__ __launch_bounds__(TB_THREADS) void tile_bucket_kernel(TileArgs a0, Ca
 // 16 bg .. 16 bg + 15 of tile tt (16 tiles x 4 B = one 64-B piece per block
 // row and load), the RS_BG block-group partial sums are scanned through LDS.
 static_assert(TB_BLOCKS % 64 == 0 && TB_BLOCKS <= 256, "tile_rowscan_kernel: 4 to 16 block groups of 16 blocks");
-#ifndef GS_RS_THREADS
-#define GS_RS_THREADS 1024
-#endif
 // RS_THREADS threads: RS_T = RS_THREADS / RS_BG tiles per workgroup, so each
 // load instruction of a wave reads 64 consecutive tiles of one block row
 // (256 contiguous bytes at 1024 threads; 4 x 64 B pieces at 256)
-constexpr int RS_THREADS = GS_RS_THREADS;
+constexpr int RS_THREADS = 1024;
 constexpr int RS_BG = TB_BLOCKS / 16, RS_T = RS_THREADS / RS_BG;
 __global__ __launch_bounds__(RS_THREADS) void tile_rowscan_kernel(uint32_t* __restrict__ thist0,
                                                            uint32_t* __restrict__ ttotal0, int T, CamBatch cb) {
@@ -396,9 +358,9 @@ __global__ __launch_bounds__(OFF_T) void tile_offsets_kernel(const uint32_t* __r
   }
   // Where the sort's length classes sit in tile_order_kernel's dispatch order
   // (descending by the bucket v >> sh, the same sh): the tiles longer than
-  // GS_SORT_SMALL all lie in the prefix of the P1 tiles whose bucket reaches
-  // (GS_SORT_SMALL + 1) >> sh, the Q1 tiles whose bucket exceeds
-  // GS_SORT_SMALL >> sh are all long, and the P2 prefix likewise holds every
+  // SORT_SMALL all lie in the prefix of the P1 tiles whose bucket reaches
+  // (SORT_SMALL + 1) >> sh, the Q1 tiles whose bucket exceeds
+  // SORT_SMALL >> sh are all long, and the P2 prefix likewise holds every
   // tile longer than TS_CAP -- so each class launch covers only its part.
   {
     const uint32_t mxl = s_max;
@@ -406,8 +368,8 @@ __global__ __launch_bounds__(OFF_T) void tile_offsets_kernel(const uint32_t* __r
     uint32_t p1 = 0, q1 = 0, p2 = 0;
     for (int t = a0; t < a1; ++t) {
       const uint32_t b = ttotal[t] >> sh;
-      p1 += b >= ((uint32_t)(GS_SORT_SMALL + 1) >> sh) ? 1u : 0u;
-      q1 += b > ((uint32_t)GS_SORT_SMALL >> sh) ? 1u : 0u;
+      p1 += b >= ((uint32_t)(SORT_SMALL + 1) >> sh) ? 1u : 0u;
+      q1 += b > ((uint32_t)SORT_SMALL >> sh) ? 1u : 0u;
       p2 += b >= ((uint32_t)(TS_CAP + 1) >> sh) ? 1u : 0u;
     }
     if (p1) atomicAdd(&s_cnt[0], p1);
@@ -505,17 +467,8 @@ __device__ inline uint64_t match_digit8(uint32_t d, uint64_t valid) {
 
 // Bucket bits of the MSD sort: 2^10 buckets, 2^11 for the longer length
 // classes of long-tile scenes (tile_sort_launches).
-#ifndef GS_BS_BITS
-#define GS_BS_BITS 10
-#endif
-#ifndef GS_BS_BITS_LONG
-#define GS_BS_BITS_LONG 11
-#endif
-constexpr int BS_BITS = GS_BS_BITS, BS_BITS_LONG = GS_BS_BITS_LONG;
-#ifndef GS_BS_KPT
-#define GS_BS_KPT 8
-#endif
-constexpr int BS_KPT = GS_BS_KPT;  // keys per thread held in registers
+constexpr int BS_BITS = 10, BS_BITS_LONG = 11;
+constexpr int BS_KPT = 8;  // keys per thread held in registers
 constexpr int BS_RUN_MAX = 48;  // longest per-thread run handed to the insertion sort
 
 template <int NT, int BINS>
@@ -779,12 +732,9 @@ __global__ __launch_bounds__(NT) void tile_sort_kernel(TileArgs a0, CamBatch cb,
     for (int i = threadIdx.x; i < n; i += NT) s_key[i] = keys[r.x + i];
     __syncthreads();
     const uint64_t* out;
-#ifndef GS_NO_BUCKET_SORT
     if (tile_bucket_sort<NT, BITS>(s_key, s_key + cap, n, sm)) {
       out = s_key + cap;
-    } else
-#endif
-    {
+    } else {
 #ifdef GS_STATS
       if (threadIdx.x == 0) atomicAdd(&g_sort_stats[1], 1ull);
 #endif
@@ -824,7 +774,6 @@ void launch_tile_bucket(const TileArgs& a, const CamBatch& cb, hipStream_t s) {
   const int T = a.num_tiles;
   for (int t0 = 0; t0 < T; t0 += TB_BINS) {
     const int nt = min(TB_BINS, T - t0);
-#ifndef GS_BUCKET_DIRECT
     // staged: the whole LDS of a CU (one workgroup) for the cursors, the run
     // offsets and as many keys as fit (10 B each: the key and its tile)
     constexpr int kLds = 160 * 1024 - 1024;  // minus the static arrays
@@ -834,7 +783,8 @@ void launch_tile_bucket(const TileArgs& a, const CamBatch& cb, hipStream_t s) {
                          (size_t)10 * cap + (size_t)8 * nt, s, a, cb, t0, nt, cap);
       continue;
     }
-#endif
+    // more keys per workgroup than the LDS holds: every key stored where its
+    // slot lands
     hipLaunchKernelGGL(tile_hist_kernel<true>, dim3(TB_BLOCKS, cb.C), dim3(TB_THREADS), sizeof(uint32_t) * nt, s,
                        a, cb, t0, nt);
   }
@@ -861,15 +811,6 @@ static void tile_sort_launches(const TileArgs& a, const CamBatch& cb, int64_t ma
   auto launch = [&](int cap, int lo, int hi, int ofs, int n) {
     if (n <= 0) return;
     const dim3 grid(n, cb.C);
-#ifdef GS_SORT_MID512
-    // the tiles past the short class sorted by 512-thread workgroups at the
-    // short class's bucket bits
-    if (NT == 256 && lo > 0) {
-      hipLaunchKernelGGL((tile_sort_kernel<512, BS_BITS>), grid, dim3(512), 2 * sizeof(uint64_t) * (cap > 0 ? cap : 1),
-                         s, a, cb, cap > 0 ? cap : 1, lo, hi, ofs);
-      return;
-    }
-#endif
     if (lo == 0 || !long_bits)
       hipLaunchKernelGGL((tile_sort_kernel<NT, BS_BITS>), grid, block, 2 * sizeof(uint64_t) * (cap > 0 ? cap : 1), s,
                          a, cb, cap > 0 ? cap : 1, lo, hi, ofs);
@@ -883,7 +824,7 @@ static void tile_sort_launches(const TileArgs& a, const CamBatch& cb, int64_t ma
     launch(TS_CAP_LONG, TS_CAP, big, 0, T);
     return;
   }
-  const int64_t small = GS_SORT_SMALL;
+  const int64_t small = SORT_SMALL;
   const bool known = sc.valid;
   const int q1 = known ? sc.q1 : 0;
   launch((int)(max_len < small ? max_len : small), 0, (int)small, q1, T - q1);

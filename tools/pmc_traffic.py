@@ -16,7 +16,8 @@ import os
 import sys
 
 STAGE_OF = {"preprocess_fwd": "preprocess", "tile_hist_kernel<false>": "scan", "tile_rowscan": "scan",
-            "tile_offsets": "scan", "tile_hist_kernel<true>": "duplicate", "tile_sort": "sort",
+            "tile_offsets": "scan", "tile_hist_kernel<true>": "duplicate", "tile_bucket": "duplicate",
+            "tile_order": "ranges", "tile_sort": "sort",
             "render_fwd": "render_fwd", "render_bwd": "render_bwd", "preprocess_bwd": "preprocess_bwd"}
 
 
