@@ -149,6 +149,19 @@ def params2rendervar(params, label):
     return rv
 
 
+def raw_rendervar(params, label, means2D):
+    """params2rendervar's inputs for GaussianRasterizerBatch(raw_params=True):
+    the raw parameters themselves, activated inside the preprocess kernels
+    (sigmoid / exp / normalize, GS_FLAG_ACTIVATE); means2D is a placeholder
+    (the batch keeps the densification statistics itself)."""
+    rv = {"means3D": params["means3D"], "colors_precomp": params["rgb_colors"],
+          "rotations": params["unnorm_rotations"], "opacities": params["logit_opacities"],
+          "scales": params["log_scales"], "means2D": means2D, "label": label}
+    if "semantic_feature" in params:
+        rv["semantic_feature"] = params["semantic_feature"]
+    return rv
+
+
 def make_settings(cams, dev, compat, sink=None):
     out = []
     for c in cams:
@@ -459,19 +472,26 @@ def main():
         # the leaves' accumulation crosses the camera streams by design
         torch.autograd.graph.set_warn_on_accumulate_grad_stream_mismatch(False)
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(device=dev) for _ in range(n_streams - 1)]
+    # The camera batch takes the raw parameters and applies params2rendervar's
+    # activations in its preprocess kernels (GS_FLAG_ACTIVATE: ~20 fewer
+    # elementwise launches per step; tests/test_gpu_raw_params.py holds it to
+    # the torch-activation step); GS_BENCH_RAW=0 keeps torch's activations.
+    raw = os.environ.get("GS_BENCH_RAW", "1") != "0"
+    means2D_placeholder = torch.zeros_like(params["means3D"])
+
     # one upstream gradient per camera, materialized once (the batch's
     # backward reads [C, ...] images like C per-camera backwards do)
     def batch_inputs(setts):
         C_ = len(setts)
         ups = (up_color.expand(C_, -1, -1, -1).contiguous(), up_depth.expand(C_, -1, -1, -1).contiguous(),
                up_feat.expand(C_, -1, -1, -1).contiguous() if up_feat is not None else None)
-        return GaussianRasterizerBatch(setts), ups
+        return GaussianRasterizerBatch(setts, raw_params=raw), ups
 
     batch_ras, ups_b = batch_inputs(settings)
 
     def step_batch(ras=batch_ras, ups=ups_b):
         bucket.zero_grad()
-        rv = params2rendervar(params, label)
+        rv = raw_rendervar(params, label, means2D_placeholder) if raw else params2rendervar(params, label)
         up_c, up_d, up_f = ups
         if up_f is not None:  # G3 call (label + semantic_feature)
             im, radius, feat, depth, _ = ras(**rv)
@@ -658,6 +678,8 @@ def main():
                    "mode": ("camera batch (GaussianRasterizerBatch: one launch per stage for the rank's "
                             "cameras)" if args.mode == "batch" else "per camera (GaussianRasterizer drop-in)"),
                    "optimizer": optim_kind, "streams": n_streams if args.mode == "percam" else 1,
+                   "activations": ("in-kernel (raw parameters, GS_FLAG_ACTIVATE)" if raw and args.mode == "batch"
+                                   else "torch ops (params2rendervar)"),
                    "grad_sum": ("in-kernel (camera sum in preprocess_bwd)" if args.mode == "batch" else
                                 "in-kernel (GradientSink)" if use_sink else "autograd"),
                    "gaussians": args.gaussians, "cams_per_rank": len(my_cams), "width": W_,

@@ -152,13 +152,13 @@ class _Inputs:
         else:
             self.F_user, self.F, self.sem = 0, 0, None
 
-    def struct(self) -> GsGaussians:
+    def struct(self, flags: int = 0) -> GsGaussians:
         return GsGaussians(P=self.P, D=self.D, M=self.M, F=self.F,
                            means3D=_ptr(self.means3D), shs=_ptr(self.sh),
                            colors_precomp=_ptr(self.colors), semantic_feature=_ptr(self.sem),
                            opacities=_ptr(self.opacity), scales=_ptr(self.scales),
                            rotations=_ptr(self.rotations), cov3D_precomp=_ptr(self.cov3D),
-                           scale_modifier=self.scale_modifier, flags=0, grad_mask=None,
+                           scale_modifier=self.scale_modifier, flags=flags, grad_mask=None,
                            densify_accum=None, densify_denom=None, max_radius=None)
 
 
@@ -439,14 +439,16 @@ def _camera_batch(dev, background, viewmatrices, projmatrices, campos, c_x, c_y,
 def rasterize_gaussians_batch(background, means3D, colors, semantic_feature, opacity, scales, rotations,
                               scale_modifier, cov3D_precomp, viewmatrices, projmatrices, c_x, c_y, tan_fovx,
                               tan_fovy, image_height, image_width, sh, degree, campos, prefiltered, debug,
-                              *, compat=None):
+                              *, compat=None, activate=False):
     """The forward of C cameras at once (gs_forward_plan_batch +
     gs_forward_render_batch): the arguments of rasterize_gaussians with
     per-camera matrices stacked ([C,4,4] or [C,16], campos [C,3]) and the
     camera scalars as length-C sequences.  Returns (num_rendered[C],
     color[C,3,H,W], feature_map[C,F,H,W], depth[C,1,H,W], alpha[C,1,H,W],
     radii[C,P] int32, geomBuffer, binningBuffer, imgBuffer, num_instances[C]);
-    camera c's outputs equal rasterize_gaussians' for that camera."""
+    camera c's outputs equal rasterize_gaussians' for that camera.
+    `activate`: opacity / scales / rotations are the raw parameters
+    (logit, log, unnormalised; GS_FLAG_ACTIVATE)."""
     L_ = _lib.load()
     cm = _compat_code(compat)
     inp = _Inputs(means3D, colors, semantic_feature, opacity, scales, rotations, scale_modifier,
@@ -462,7 +464,7 @@ def rasterize_gaussians_batch(background, means3D, colors, semantic_feature, opa
                 torch.zeros(C, 1, H, W, **f32), torch.zeros(C, 1, H, W, **f32),
                 torch.zeros(C, 0, dtype=torch.int32, device=dev), torch.empty(0, **u8), torch.empty(0, **u8),
                 torch.empty(0, **u8), [0] * C)
-    g = inp.struct()
+    g = inp.struct(_lib.GS_FLAG_ACTIVATE if activate else 0)
     out_color = torch.empty(C, 3, H, W, **f32)
     out_feature = torch.empty(C, inp.F, H, W, **f32)
     out_depth = torch.empty(C, 1, H, W, **f32)
@@ -492,17 +494,22 @@ def rasterize_gaussians_batch_backward(background, means3D, radii, colors, seman
                                        c_x, c_y, tan_fovx, tan_fovy, dL_dout_color, dL_dout_feature,
                                        dL_dout_depth, dL_dout_alpha, sh, degree, campos, geomBuffer,
                                        num_instances, binningBuffer, imageBuffer, alphas, debug, *,
-                                       compat=None, grad_mask=None, densify=None):
+                                       compat=None, grad_mask=None, densify=None, opacity=None,
+                                       activate=False):
     """The backward of a camera batch (gs_backward_batch): the arguments of
     rasterize_gaussians_backward with stacked per-camera matrices, scalars
     and upstream gradients ([C, ...]), in the binding's positional camera
     semantics.  Returns the rasterize_gaussians_backward tuple with every
     per-Gaussian gradient SUMMED over the cameras.  `densify` as in
-    rasterize_gaussians_backward (per-camera statistics, summed)."""
+    rasterize_gaussians_backward (per-camera statistics, summed).
+    `activate` (with the raw `opacity`): the gradients of the raw opacity /
+    scale / rotation parameters (GS_FLAG_ACTIVATE)."""
     L_ = _lib.load()
     cm = _compat_code(compat)
-    inp = _Inputs(means3D, colors, semantic_feature, None, scales, rotations, scale_modifier,
-                  cov3D_precomp, sh, degree)
+    if activate and not _present(opacity):
+        raise RuntimeError("activate=True needs the raw opacities")
+    inp = _Inputs(means3D, colors, semantic_feature, opacity if activate else None, scales, rotations,
+                  scale_modifier, cov3D_precomp, sh, degree)
     dev, P = inp.device, inp.P
     C = len(c_x)
     img_ref = dL_dout_color if _present(dL_dout_color) else alphas
@@ -514,7 +521,7 @@ def rasterize_gaussians_batch_backward(background, means3D, radii, colors, seman
                 z(0, 3), z(0, 4))
     cams, C, keep = _camera_batch(dev, background, viewmatrices, projmatrices, campos, c_x, c_y, tan_fovx,
                                   tan_fovy, W, H)
-    g = inp.struct()
+    g = inp.struct(_lib.GS_FLAG_ACTIVATE if activate else 0)
     if grad_mask is not None:
         gm = grad_mask.to(device=dev, dtype=torch.float32).reshape(-1).contiguous()
         if gm.numel() != P:

@@ -16,8 +16,9 @@ _lock = threading.Lock()
 _lib = None
 
 c_void_p = ctypes.c_void_p
-ABI_VERSION = 7  # include/gsplat_hip.h GS_ABI_VERSION
+ABI_VERSION = 8  # include/gsplat_hip.h GS_ABI_VERSION
 GS_FLAG_ACCUMULATE = 1  # include/gsplat_hip.h
+GS_FLAG_ACTIVATE = 2  # include/gsplat_hip.h: raw opacity / scale / rotation parameters
 c_int32, c_int64, c_float, c_size_t = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_size_t
 
 GS_COMPAT = {"reference": 0, "fixed": 1}

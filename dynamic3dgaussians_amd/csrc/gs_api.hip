@@ -341,6 +341,7 @@ static int plan_impl(const gs_gaussians* g, const gs_camera* cams, int C, int pr
   a.P = P; a.D = g->D; a.M = g->M; a.W = W; a.H = H;
   a.grid_x = ta.grid_x; a.grid_y = ta.grid_y;
   a.prefiltered = prefiltered;
+  a.activate = (g->flags & GS_FLAG_ACTIVATE) != 0;
   a.means3D = g->means3D; a.scales = g->scales; a.rotations = g->rotations; a.opacities = g->opacities;
   a.shs = g->shs; a.cov3D_precomp = g->cov3D_precomp; a.colors_precomp = g->colors_precomp;
   a.scale_modifier = g->scale_modifier;
@@ -471,6 +472,8 @@ static int backward_impl(const gs_gaussians* g, const gs_camera* cams, int C, co
   if (P == 0) return 0;
   if (!geom || !image || !scratch || !radii) return fail(-1, "state buffers are required");
   if (!alphas) return fail(-1, "the forward's alpha image is required");
+  if ((g->flags & GS_FLAG_ACTIVATE) && !g->opacities)
+    return fail(-1, "GS_FLAG_ACTIVATE: the backward needs the raw opacities");
   if (!dL_dmeans2D || !dL_dcolors || !dL_dopacity || !dL_dmeans3D || !dL_dcov3D || !dL_dscales ||
       !dL_drotations || (g->F > 0 && !dL_dsemantic) || (g->M > 0 && !dL_dsh))
     return fail(-1, "gradient outputs are required");
@@ -517,6 +520,8 @@ static int backward_impl(const gs_gaussians* g, const gs_camera* cams, int C, co
   PreprocessBwdArgs b{};
   b.P = P; b.D = g->D; b.M = g->M; b.F = g->F; b.W = W; b.H = H; b.compat = compat;
   b.accumulate = accumulate ? 1 : 0;
+  b.activate = (g->flags & GS_FLAG_ACTIVATE) != 0;
+  b.opacities = g->opacities;
   b.means3D = g->means3D; b.radii = radii; b.shs = g->shs; b.clamped = at<uint8_t>(geom, gl.clamped);
   b.scales = g->scales; b.rotations = g->rotations;
   b.cov3D = at<float>(geom, gl.cov3D);

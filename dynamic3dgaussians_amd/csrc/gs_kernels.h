@@ -12,6 +12,7 @@ namespace gs {
 
 struct PreprocessArgs {
   int P, D, M, W, H, grid_x, grid_y, prefiltered;
+  int activate;  // GS_FLAG_ACTIVATE: opacities / scales / rotations are raw parameters
   const float* means3D;
   const float* scales;
   const float* rotations;
@@ -35,6 +36,8 @@ struct PreprocessArgs {
 struct PreprocessBwdArgs {
   int P, D, M, F, W, H, compat;
   int accumulate;  // add into the gradient outputs (GS_FLAG_ACCUMULATE)
+  int activate;    // GS_FLAG_ACTIVATE: gradients of the raw opacity / scale / rotation parameters
+  const float* opacities;  // read with `activate` only
   const float* means3D;
   const int* radii;
   const float* shs;

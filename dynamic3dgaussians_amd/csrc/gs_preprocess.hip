@@ -165,6 +165,46 @@ __device__ inline void sh_fwd(int deg, int M, V3 p, V3 cp, const float* __restri
   }
 }
 
+// ------------------------------------------------------------------ activations
+// GS_FLAG_ACTIVATE: the Dynamic3DGaussians parameterisation of
+// helpers.py:98-107 (params2rendervar) applied in the kernels, in the
+// operation order of torch's kernels for the same ops (this file is compiled
+// without fma contraction): sigmoid = 1 / (1 + exp(-x)), exp, and
+// F.normalize = q / max(|q|, 1e-12) (torch.nn.functional.normalize, p = 2,
+// dim = 1).  Their backward follows autograd's formulas: sigmoid_backward
+// g (1 - y) y, exp's g y, and normalize's div / clamp_min / norm chain.
+// The squared norm is summed pairwise, (x^2 + y^2) + (z^2 + w^2): the order
+// that reproduces torch's GPU reduction bit for bit (tools/act_probe.py on an
+// MI355X: 100 % of 400k quaternions vs 88 % for the sequential sum,
+// profiles/r04b/act_probe.txt).
+constexpr float NORMALIZE_EPS = 1e-12f;
+__device__ inline float act_sigmoid(float x) { return 1.0f / (1.0f + expf(-x)); }
+__device__ inline float act_norm(float4 q) { return sqrtf((q.x * q.x + q.y * q.y) + (q.z * q.z + q.w * q.w)); }
+__device__ inline float4 act_normalize(float4 q) {
+  const float d = fmaxf(act_norm(q), NORMALIZE_EPS);
+  return make_float4(q.x / d, q.y / d, q.z / d, q.w / d);
+}
+// dL/dq of q_hat = q / max(|q|, eps) for the upstream gradient gq of q_hat:
+// DivBackward (g / d for q, -g (q / d) / d summed for the denominator),
+// ClampMinBackward (passes where |q| >= eps), NormBackward (q (g_n / |q|)).
+__device__ inline float4 act_normalize_bwd(float4 q, float4 gq) {
+  const float n = act_norm(q);
+  const float d = fmaxf(n, NORMALIZE_EPS);
+  const float gd = (-gq.x * ((q.x / d) / d) + -gq.y * ((q.y / d) / d)) +
+                   (-gq.z * ((q.z / d) / d) + -gq.w * ((q.w / d) / d));
+  const float gn = (n >= NORMALIZE_EPS && n != 0.0f) ? gd / n : 0.0f;
+  return make_float4(gq.x / d + q.x * gn, gq.y / d + q.y * gn, gq.z / d + q.z * gn, gq.w / d + q.w * gn);
+}
+// The activated rotation / scale of Gaussian g.
+__device__ inline float4 rotation_of(const float* __restrict__ rotations, int g, int activate) {
+  const float4 q = reinterpret_cast<const float4*>(rotations)[g];
+  return activate ? act_normalize(q) : q;
+}
+__device__ inline V3 scale_of(const float* __restrict__ scales, int g, int activate) {
+  const V3 s = ld3(scales + 3 * g);
+  return activate ? V3{expf(s.x), expf(s.y), expf(s.z)} : s;
+}
+
 // ------------------------------------------------------------------ forward
 
 // Camera c (blockIdx.y) of a batch: its parameters and per-camera outputs.
@@ -211,9 +251,9 @@ __global__ __launch_bounds__(256) void preprocess_fwd_kernel(PreprocessArgs a0, 
     for (int i = 0; i < 6; ++i) c3[i] = a.cov3D_precomp[6 * g + i];
   } else {
     float rc[3][3];
-    const float4 q = reinterpret_cast<const float4*>(a.rotations)[g];
+    const float4 q = rotation_of(a.rotations, g, a.activate);
     quat_cols(q, rc);
-    const V3 s = ld3(a.scales + 3 * g);
+    const V3 s = scale_of(a.scales, g, a.activate);
     const float sx = a.scale_modifier * s.x, sy = a.scale_modifier * s.y, sz = a.scale_modifier * s.z;
     float m[3][3];
 #pragma unroll
@@ -267,7 +307,7 @@ __global__ __launch_bounds__(256) void preprocess_fwd_kernel(PreprocessArgs a0, 
     sh_fwd(a.D, a.M, p, ld3(a.campos), a.shs, g, rgb, cl);
     a.clamped[g] = cl;
   }
-  const float op = a.opacities[g];
+  const float op = a.activate ? act_sigmoid(a.opacities[g]) : a.opacities[g];
   float ex, ey, tq;
   alpha_extent(ca, cb, cc, op, ex, ey, tq);
   float4* rec = reinterpret_cast<float4*>(a.rec + (size_t)REC * g);
@@ -591,9 +631,12 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdArgs a
   }
   }
   float dscale[3] = {0.f, 0.f, 0.f}, drot[4] = {0.f, 0.f, 0.f, 0.f};
-  if (any_vis && a.scales)
-    cov3d_bwd(ld3(a.scales + 3 * g), a.scale_modifier, reinterpret_cast<const float4*>(a.rotations)[g], dcov,
-              dscale, drot);
+  const int act = a.activate;
+  V3 sc{0.f, 0.f, 0.f};
+  if (any_vis && a.scales) {
+    sc = scale_of(a.scales, g, act);
+    cov3d_bwd(sc, a.scale_modifier, rotation_of(a.rotations, g, act), dcov, dscale, drot);
+  }
   gput(a.dmeans2D + 3 * g, am[0], ac); gput(a.dmeans2D + 3 * g + 1, am[1], ac);
   if (!ac) a.dmeans2D[3 * g + 2] = 0.f;
   if (a.st_accum) gput(a.st_accum + g, st_acc, ac);
@@ -603,7 +646,14 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdArgs a
   // the reference's elementwise `grad * label` (the chain rule uses unmasked dcol).
   gput(a.dcolors + 3 * g, dcol[0] * mk, ac); gput(a.dcolors + 3 * g + 1, dcol[1] * mk, ac);
   gput(a.dcolors + 3 * g + 2, dcol[2] * mk, ac);
-  gput(a.dopacity + g, dop * mk, ac);
+  if (act) {
+    // through the activations (the label mask applies to the activated
+    // gradients, then autograd's backward of params2rendervar)
+    const float y = act_sigmoid(a.opacities[g]);
+    gput(a.dopacity + g, ((dop * mk) * (1.0f - y)) * y, ac);
+  } else {
+    gput(a.dopacity + g, dop * mk, ac);
+  }
   if (!sh_written && a.M > 0) {  // no SH gradient: zeros (masked like the rest)
     float* ds = a.dsh + (size_t)g * a.M * 3;
     for (int i = 0; i < 3 * a.M; ++i) ds[i] = 0.f * mk;
@@ -612,14 +662,25 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(PreprocessBwdArgs a
   for (int i = 0; i < 3; ++i) gput(a.dmeans3D + 3 * g + i, dm[i] * mk, ac);
 #pragma unroll
   for (int i = 0; i < 6; ++i) gput(a.dcov3D + 6 * g + i, dcov[i] * mk, ac);
+  if (act && a.scales) {
+    const float sv[3] = {sc.x, sc.y, sc.z};
+    // an unseen Gaussian keeps zero gradients (sc is never evaluated for it)
 #pragma unroll
-  for (int i = 0; i < 3; ++i) gput(a.dscales + 3 * g + i, dscale[i] * mk, ac);
+    for (int i = 0; i < 3; ++i) gput(a.dscales + 3 * g + i, any_vis ? (dscale[i] * mk) * sv[i] : 0.f * mk, ac);
+    float4 dq = make_float4(drot[0] * mk, drot[1] * mk, drot[2] * mk, drot[3] * mk);
+    if (any_vis) dq = act_normalize_bwd(reinterpret_cast<const float4*>(a.rotations)[g], dq);
+    drot[0] = dq.x; drot[1] = dq.y; drot[2] = dq.z; drot[3] = dq.w;
+  } else {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) gput(a.dscales + 3 * g + i, dscale[i] * mk, ac);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) drot[i] = drot[i] * mk;
+  }
   if (ac) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) a.drot[4 * g + i] += drot[i] * mk;
+    for (int i = 0; i < 4; ++i) a.drot[4 * g + i] += drot[i];
   } else {
-    reinterpret_cast<float4*>(a.drot)[g] =
-        make_float4(drot[0] * mk, drot[1] * mk, drot[2] * mk, drot[3] * mk);
+    reinterpret_cast<float4*>(a.drot)[g] = make_float4(drot[0], drot[1], drot[2], drot[3]);
   }
 }
 

@@ -424,7 +424,7 @@ class _RasterizeGaussiansBatch(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, means3D, means2D, sh, colors_precomp, semantic_feature, opacities, scales, rotations,
-                cov3Ds_precomp, cams, label, densify_out):
+                cov3Ds_precomp, cams, label, densify_out, raw_params=False):
         if not isinstance(cams, _BatchCameras):
             cams = _BatchCameras(cams)
         rs0 = cams.rs0
@@ -440,7 +440,8 @@ class _RasterizeGaussiansBatch(torch.autograd.Function):
         out = _C.rasterize_gaussians_batch(
             rs0.bg, means3D, colors_precomp, semantic_feature, opacities, scales, rotations, rs0.scale_modifier,
             cov3Ds_precomp, views, projs, [p[0] for p in pp], [p[1] for p in pp], tx, ty, rs0.image_height,
-            rs0.image_width, sh, rs0.sh_degree, cpos, rs0.prefiltered, rs0.debug, compat=compat)
+            rs0.image_width, sh, rs0.sh_degree, cpos, rs0.prefiltered, rs0.debug, compat=compat,
+            activate=raw_params)
         num_rendered, color, feature_map, depth, alpha, radii, geom, binning, img, num_instances = out
         ctx.rs0 = rs0
         ctx.cams = (views, projs, cpos, pp, tx, ty)
@@ -449,11 +450,13 @@ class _RasterizeGaussiansBatch(torch.autograd.Function):
         ctx.compat = compat
         ctx.C = C
         ctx.densify_out = densify_out
+        ctx.raw_params = raw_params
         ctx.set_materialize_grads(False)
         ctx.sem_shape = None if semantic_feature is None else tuple(semantic_feature.shape)
         ctx.save_for_backward(colors_precomp, semantic_feature, means3D, scales, rotations, cov3Ds_precomp,
                               radii, sh, geom, binning, img, alpha,
-                              label if isinstance(label, torch.Tensor) else None)
+                              label if isinstance(label, torch.Tensor) else None,
+                              opacities if raw_params else None)
         ctx.mark_non_differentiable(radii)
         return color, radii, feature_map, depth, alpha
 
@@ -462,7 +465,7 @@ class _RasterizeGaussiansBatch(torch.autograd.Function):
         rs0 = ctx.rs0
         views, projs, cpos, pp, tx, ty = ctx.cams
         (colors_precomp, semantic_feature, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geom,
-         binning, img, alpha, label) = ctx.saved_tensors
+         binning, img, alpha, label, raw_opacities) = ctx.saved_tensors
         cx, cy = [p[0] for p in pp], [p[1] for p in pp]
         # Q2 in reference mode, per camera (see _RasterizeGaussians.backward)
         cam4 = (tx, ty, cx, cy) if ctx.compat == "reference" else (cx, cy, tx, ty)
@@ -472,7 +475,8 @@ class _RasterizeGaussiansBatch(torch.autograd.Function):
             rs0.bg, means3D, radii, colors_precomp, semantic_feature, scales, rotations, rs0.scale_modifier,
             cov3Ds_precomp, views, projs, *cam4, grad_color, grad_out_feature, grad_depth, grad_alpha, sh,
             rs0.sh_degree, cpos, geom, ctx.num_instances, binning, img, alpha, rs0.debug, compat=ctx.compat,
-            grad_mask=label if fuse else None, densify=ctx.densify_out)
+            grad_mask=label if fuse else None, densify=ctx.densify_out, opacity=raw_opacities,
+            activate=ctx.raw_params)
         (grad_means2D, grad_colors_precomp, grad_semantic_feature, grad_opacities, grad_means3D,
          grad_cov3Ds_precomp, grad_sh, grad_scales, grad_rotations) = grads
         if ctx.sem_shape is not None:
@@ -480,6 +484,9 @@ class _RasterizeGaussiansBatch(torch.autograd.Function):
         else:
             grad_semantic_feature = None
         if label is not None and not fuse:
+            if ctx.raw_params:
+                raise RuntimeError("raw_params=True needs a per-Gaussian fp32 label (or none): the mask is "
+                                   "applied in-kernel before the activations' backward")
             lab = label.unsqueeze(1)
             grad_means3D = grad_means3D * lab
             grad_sh = grad_sh * lab[..., None]
@@ -489,19 +496,24 @@ class _RasterizeGaussiansBatch(torch.autograd.Function):
             grad_rotations = grad_rotations * lab
             grad_cov3Ds_precomp = grad_cov3Ds_precomp * lab
         grads = (grad_means3D, grad_means2D, grad_sh, grad_colors_precomp, grad_semantic_feature,
-                 grad_opacities, grad_scales, grad_rotations, grad_cov3Ds_precomp, None, None, None)
+                 grad_opacities, grad_scales, grad_rotations, grad_cov3Ds_precomp, None, None, None, None)
         return tuple(g if need else None for g, need in zip(grads, ctx.needs_input_grad))
 
 
 def rasterize_gaussians_batch(means3D, means2D, sh, colors_precomp, semantic_feature, opacities, scales,
-                              rotations, cov3Ds_precomp, settings_list, label=None, densify_out=None):
+                              rotations, cov3Ds_precomp, settings_list, label=None, densify_out=None,
+                              raw_params=False):
     """rasterize_gaussians over a list of camera settings; outputs [C, ...]
     (color, radii, feature_map, depth, alpha).  `densify_out`: optional
     (accum, denom, max_radius) fp32 [P] tensors the backward fills with the
-    cameras' densification statistics (GradientSink.densify_stats)."""
+    cameras' densification statistics (GradientSink.densify_stats).
+    `raw_params`: opacities / scales / rotations are the raw parameters of
+    helpers.py:98-107 (logit_opacities, log_scales, unnorm_rotations); the
+    kernels apply sigmoid / exp / normalize and return their gradients."""
     cams = settings_list if isinstance(settings_list, _BatchCameras) else _BatchCameras(list(settings_list))
     return _RasterizeGaussiansBatch.apply(means3D, means2D, sh, colors_precomp, semantic_feature, opacities,
-                                          scales, rotations, cov3Ds_precomp, cams, label, densify_out)
+                                          scales, rotations, cov3Ds_precomp, cams, label, densify_out,
+                                          bool(raw_params))
 
 
 class GaussianRasterizerBatch(nn.Module):
@@ -513,13 +525,21 @@ class GaussianRasterizerBatch(nn.Module):
     (the reference's accumulate_mean2d_gradient / max_2D_radius inputs,
     external.py:136-140, train.py:288-290; see GradientSink).  The cameras'
     matrices are stacked once at construction: build a new rasterizer when
-    they change (as the reference builds its settings per camera)."""
+    they change (as the reference builds its settings per camera).
 
-    def __init__(self, settings_list, track_densify=False):
+    `raw_params=True` takes the Dynamic3DGaussians raw parameters as
+    opacities / scales / rotations (logit_opacities, log_scales,
+    unnorm_rotations: helpers.py:98-107 params2rendervar) and applies the
+    activations -- sigmoid, exp, F.normalize -- inside the preprocess kernels,
+    forward and backward (GS_FLAG_ACTIVATE): the same step without the ~20
+    elementwise launches of the activations and their autograd backward."""
+
+    def __init__(self, settings_list, track_densify=False, raw_params=False):
         super().__init__()
         self.settings_list = list(settings_list)
         self._cams = _BatchCameras(self.settings_list)
         self.track_densify = track_densify
+        self.raw_params = bool(raw_params)
         self.densify_stats = None
 
     def forward(self, means3D, means2D, opacities=None, shs=None, semantic_feature=None, colors_precomp=None,
@@ -544,7 +564,7 @@ class GaussianRasterizerBatch(nn.Module):
             self.densify_stats = {"means2D_gradient_accum": dens[0], "denom": dens[1], "max_2D_radius": dens[2]}
         color, radii, feature_map, depth, alpha = rasterize_gaussians_batch(
             means3D, means2D, shs, colors_precomp, semantic_feature, opacities, scales, rotations,
-            cov3D_precomp, self._cams, lab, dens)
+            cov3D_precomp, self._cams, lab, dens, self.raw_params)
         has_sem = semantic_feature is not None
         if has_label and has_sem:      # G3
             return color, radii, feature_map, depth, alpha

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 7
+#define GS_ABI_VERSION 8
 
 /* compat modes: numerics of the as-shipped reference vs corrected ones */
 #define GS_COMPAT_REFERENCE 0
@@ -50,7 +50,18 @@ typedef void *gs_stream_t;
  * flag); calls accumulating into the same outputs must be ordered on one
  * stream (the non-atomic read-modify-write of the per-Gaussian outputs is
  * not safe across concurrent streams). */
-#define GS_FLAG_ACCUMULATE 1u /* a hipStream_t (NULL = legacy default stream) */
+#define GS_FLAG_ACCUMULATE 1u
+/* GS_FLAG_ACTIVATE (ABI 8; no reference analogue): opacities, scales and
+ * rotations are the Dynamic3DGaussians raw parameters -- logit_opacities,
+ * log_scales, unnorm_rotations -- and the kernels apply the activations of
+ * helpers.py:98-107 (params2rendervar) themselves: sigmoid, exp and
+ * F.normalize (q / max(|q|, 1e-12)).  The backward's dL_dopacity,
+ * dL_dscales and dL_drotations are then the gradients of the raw parameters
+ * (through the activations, with grad_mask applied to the activated
+ * gradients first, as the reference's label mask precedes autograd through
+ * params2rendervar).  Replaces ~20 elementwise launches of the caller's
+ * activations and their backward per step. */
+#define GS_FLAG_ACTIVATE 2u
 
 /* Per-Gaussian inputs (device pointers, fp32, row-major/contiguous).
  * Mirrors the tensor arguments of RasterizeGaussiansCUDA
