@@ -451,6 +451,18 @@ def rasterize_gaussians_batch(background, means3D, colors, semantic_feature, opa
     (logit, log, unnormalised; GS_FLAG_ACTIVATE)."""
     L_ = _lib.load()
     cm = _compat_code(compat)
+    nat = _native_mod()
+    if nat is not None and means3D.is_cuda and means3D.dim() == 2 and means3D.size(0) > 0:
+        try:
+            return nat.forward_batch(background, means3D, _opt(colors), _opt(semantic_feature), _opt(opacity),
+                                     _opt(scales), _opt(rotations), float(scale_modifier), _opt(cov3D_precomp),
+                                     viewmatrices, projmatrices, [float(x) for x in c_x], [float(x) for x in c_y],
+                                     [float(x) for x in tan_fovx], [float(x) for x in tan_fovy], int(image_height),
+                                     int(image_width), _opt(sh), int(degree), campos, bool(prefiltered),
+                                     bool(debug), cm, bool(activate),
+                                     torch.cuda.current_stream(means3D.device).cuda_stream)
+        except RuntimeError as ex:
+            raise _lib.GsplatError(str(ex)) from None
     inp = _Inputs(means3D, colors, semantic_feature, opacity, scales, rotations, scale_modifier,
                   cov3D_precomp, sh, degree)
     dev, P = inp.device, inp.P
@@ -508,6 +520,21 @@ def rasterize_gaussians_batch_backward(background, means3D, radii, colors, seman
     cm = _compat_code(compat)
     if activate and not _present(opacity):
         raise RuntimeError("activate=True needs the raw opacities")
+    nat = _native_mod()
+    if nat is not None and means3D.is_cuda and means3D.dim() == 2 and means3D.size(0) > 0:
+        try:
+            return nat.backward_batch(background, means3D, radii, _opt(colors), _opt(semantic_feature),
+                                      _opt(scales), _opt(rotations), float(scale_modifier), _opt(cov3D_precomp),
+                                      viewmatrices, projmatrices, [float(x) for x in c_x],
+                                      [float(x) for x in c_y], [float(x) for x in tan_fovx],
+                                      [float(x) for x in tan_fovy], _opt(dL_dout_color), _opt(dL_dout_feature),
+                                      _opt(dL_dout_depth), _opt(dL_dout_alpha), _opt(sh), int(degree), campos,
+                                      geomBuffer, [int(x) for x in num_instances], _opt(binningBuffer),
+                                      imageBuffer, alphas, bool(debug), cm, _opt(grad_mask),
+                                      None if densify is None else list(densify), _opt(opacity), bool(activate),
+                                      torch.cuda.current_stream(means3D.device).cuda_stream)
+        except RuntimeError as ex:
+            raise _lib.GsplatError(str(ex)) from None
     inp = _Inputs(means3D, colors, semantic_feature, opacity if activate else None, scales, rotations,
                   scale_modifier, cov3D_precomp, sh, degree)
     dev, P = inp.device, inp.P

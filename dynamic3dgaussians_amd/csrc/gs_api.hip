@@ -136,6 +136,20 @@ struct PlanInfo {
 };
 thread_local PlanInfo g_plan;
 
+// Page-locked host landing area of the plan headers (GS_MAX_CAMS x M_WORDS
+// words, 2 KiB per calling thread, allocated on first use and never freed:
+// freeing it from a thread-exit destructor could run after the HIP runtime
+// is gone): a device->host copy into pageable memory is staged through a
+// driver bounce buffer, an extra copy on the forward's one host round trip.
+// Host memory: the library still allocates no device memory.
+thread_local uint32_t* g_hdr = nullptr;
+static uint32_t* pinned_headers() {
+  if (!g_hdr && hipHostMalloc(reinterpret_cast<void**>(&g_hdr), sizeof(uint32_t) * GS_MAX_CAMS * M_WORDS,
+                              hipHostMallocDefault) != hipSuccess)
+    g_hdr = nullptr;
+  return g_hdr;
+}
+
 TileArgs tile_args(int P, int W, int H, void* geom, void* image) {
   TileArgs t{};
   const GeomLayout gl(P);
@@ -367,9 +381,11 @@ static int plan_impl(const gs_gaussians* g, const gs_camera* cams, int C, int pr
   // The one host read of the forward (CR/rasterizer_impl.cu:287), one for
   // the whole batch: the list instance counts size the binning buffer; the
   // reference's counts and the rest of the headers ride along.
-  uint32_t host[GS_MAX_CAMS][M_WORDS];
-  hipError_t he = hipMemcpy2DAsync(host, sizeof(host[0]), ta.meta, (size_t)cb.img_stride, sizeof(host[0]), C,
-                                   hipMemcpyDeviceToHost, s);
+  uint32_t stack_hdr[GS_MAX_CAMS][M_WORDS];
+  uint32_t* pin = pinned_headers();
+  uint32_t(*host)[M_WORDS] = pin ? reinterpret_cast<uint32_t(*)[M_WORDS]>(pin) : stack_hdr;
+  hipError_t he = hipMemcpy2DAsync(host, sizeof(uint32_t) * M_WORDS, ta.meta, (size_t)cb.img_stride,
+                                   sizeof(uint32_t) * M_WORDS, C, hipMemcpyDeviceToHost, s);
   if (he == hipSuccess) he = hipStreamSynchronize(s);
   if (he != hipSuccess) return fail((int)he, "num_rendered readback: %s", hipGetErrorString(he));
   int64_t max_len = 0, total = 0;

@@ -232,6 +232,151 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tenso
   return {o[0], o[1], dsem, o[3], o[4], o[5], o[6], o[7], o[8]};
 }
 
+// ---- camera batches (gs_*_batch): the C++ counterpart of
+// _C.rasterize_gaussians_batch / rasterize_gaussians_batch_backward.  The
+// forward's one host round trip (the plan header) sits between the two ABI
+// calls, so the host work around it is on the step's critical path.
+
+struct Cameras {
+  Tensor view, proj, cpos, bg;
+  std::vector<gs_camera> cams;
+  Cameras(const at::Device& dev, const Tensor& bg_, const Tensor& views, const Tensor& projs, const Tensor& campos,
+          const std::vector<double>& cx, const std::vector<double>& cy, const std::vector<double>& tx,
+          const std::vector<double>& ty, int64_t W, int64_t H) {
+    const int64_t C = (int64_t)cx.size();
+    if (C < 1 || C > 64) throw std::runtime_error("camera batch size " + std::to_string(C) + " outside 1..64");
+    if ((int64_t)cy.size() != C || (int64_t)tx.size() != C || (int64_t)ty.size() != C)
+      throw std::runtime_error("per-camera scalars must all have C entries");
+    view = dev_f32(views, dev, "viewmatrices").reshape({C, 16}).contiguous();
+    proj = dev_f32(projs, dev, "projmatrices").reshape({C, 16}).contiguous();
+    cpos = dev_f32(campos, dev, "campos").reshape({C, 3}).contiguous();
+    bg = dev_f32(bg_, dev, "bg").reshape({-1});
+    cams.resize(C);
+    for (int64_t c = 0; c < C; ++c) {
+      gs_camera& k = cams[c];
+      k.viewmatrix = view.data_ptr<float>() + 16 * c;
+      k.projmatrix = proj.data_ptr<float>() + 16 * c;
+      k.campos = cpos.data_ptr<float>() + 3 * c;
+      k.background = bg.data_ptr<float>();
+      k.c_x = (float)cx[c];
+      k.c_y = (float)cy[c];
+      k.tan_fovx = (float)tx[c];
+      k.tan_fovy = (float)ty[c];
+      k.image_width = (int32_t)W;
+      k.image_height = (int32_t)H;
+    }
+  }
+};
+
+std::tuple<std::vector<int64_t>, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, std::vector<int64_t>>
+forward_batch(const Tensor& bg, const Tensor& means3D, const OptT& colors, const OptT& sem, const OptT& opacity,
+              const OptT& scales, const OptT& rotations, double scale_modifier, const OptT& cov3D, const Tensor& views,
+              const Tensor& projs, const std::vector<double>& cx, const std::vector<double>& cy,
+              const std::vector<double>& tx, const std::vector<double>& ty, int64_t H, int64_t W, const OptT& sh,
+              int64_t degree, const Tensor& campos, bool prefiltered, bool debug, int64_t compat, bool activate,
+              int64_t stream) {
+  Inputs in(means3D, colors, sem, opacity, scales, rotations, scale_modifier, cov3D, sh, degree);
+  if (activate) in.g.flags |= GS_FLAG_ACTIVATE;
+  Cameras k(in.dev, bg, views, projs, campos, cx, cy, tx, ty, W, H);
+  const int32_t C = (int32_t)k.cams.size();
+  const auto f32 = at::TensorOptions().dtype(at::kFloat).device(in.dev);
+  const auto u8 = at::TensorOptions().dtype(at::kByte).device(in.dev);
+  Tensor out_color = at::empty({C, 3, H, W}, f32);
+  Tensor out_feature = at::empty({C, in.F, H, W}, f32);
+  Tensor out_depth = at::empty({C, 1, H, W}, f32);
+  Tensor out_alpha = at::empty({C, 1, H, W}, f32);
+  Tensor radii = at::empty({C, in.P}, f32.dtype(at::kInt));
+  Tensor geom = at::empty({(int64_t)gs_batch_geom_buffer_bytes(in.P, C)}, u8);
+  Tensor img = at::empty({(int64_t)gs_batch_image_buffer_bytes((int32_t)W, (int32_t)H, C)}, u8);
+  std::vector<int64_t> NR(C, 0), NI(C, 0);
+  gs_stream_t s = reinterpret_cast<gs_stream_t>(stream);
+  check(gs_forward_plan_batch(&in.g, k.cams.data(), C, prefiltered ? 1 : 0, debug ? 1 : 0, (int)compat,
+                              geom.data_ptr(), img.data_ptr(), radii.data_ptr<int32_t>(), NR.data(), NI.data(), s),
+        "rasterize_gaussians_batch (preprocess)");
+  const int64_t nb = (int64_t)gs_batch_binning_buffer_bytes(C, NI.data());
+  Tensor binning = at::empty({nb > 1 ? nb : 1}, u8);
+  check(gs_forward_render_batch(&in.g, k.cams.data(), C, debug ? 1 : 0, (int)compat, geom.data_ptr(),
+                                binning.data_ptr(), img.data_ptr(), NI.data(), radii.data_ptr<int32_t>(),
+                                out_color.data_ptr<float>(), in.F ? out_feature.data_ptr<float>() : nullptr,
+                                out_depth.data_ptr<float>(), out_alpha.data_ptr<float>(), s),
+        "rasterize_gaussians_batch (render)");
+  Tensor feature_map = in.F_user != in.F ? out_feature.narrow(1, 0, in.F_user) : out_feature;
+  return {NR, out_color, feature_map, out_depth, out_alpha, radii, geom, binning, img, NI};
+}
+
+// [C, ch, H, W] fp32 of an upstream gradient (channels zero-padded to ch), or undefined
+Tensor batch_image(const OptT& t, int64_t C, int64_t ch, int64_t H, int64_t W, const at::Device& dev,
+                   const char* name) {
+  if (!present(t)) return Tensor();
+  Tensor u = dev_f32(*t, dev, name).reshape({C, -1, H, W});
+  if (u.size(1) < ch)
+    u = at::cat({u, at::zeros({C, ch - u.size(1), H, W}, u.options())}, 1);
+  return u.contiguous();
+}
+
+std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> backward_batch(
+    const Tensor& bg, const Tensor& means3D, const Tensor& radii, const OptT& colors, const OptT& sem,
+    const OptT& scales, const OptT& rotations, double scale_modifier, const OptT& cov3D, const Tensor& views,
+    const Tensor& projs, const std::vector<double>& cx, const std::vector<double>& cy, const std::vector<double>& tx,
+    const std::vector<double>& ty, const OptT& dL_color, const OptT& dL_feature, const OptT& dL_depth,
+    const OptT& dL_alpha, const OptT& sh, int64_t degree, const Tensor& campos, const Tensor& geom,
+    const std::vector<int64_t>& num_instances, const OptT& binning, const Tensor& img, const Tensor& alphas,
+    bool debug, int64_t compat, const OptT& grad_mask, c10::optional<std::vector<Tensor>> densify,
+    const OptT& opacity, bool activate, int64_t stream) {
+  if (activate && !present(opacity)) throw std::runtime_error("activate=True needs the raw opacities");
+  Inputs in(means3D, colors, sem, activate ? opacity : c10::nullopt, scales, rotations, scale_modifier, cov3D, sh,
+            degree);
+  if (activate) in.g.flags |= GS_FLAG_ACTIVATE;
+  const int64_t C = (int64_t)cx.size();
+  const Tensor& img_ref = present(dL_color) ? *dL_color : alphas;
+  const int64_t H = img_ref.size(-2), W = img_ref.size(-1);
+  Cameras k(in.dev, bg, views, projs, campos, cx, cy, tx, ty, W, H);
+  const auto f32 = at::TensorOptions().dtype(at::kFloat).device(in.dev);
+  const int64_t P = in.P;
+  Tensor gm;
+  if (grad_mask.has_value() && grad_mask->defined()) {
+    gm = grad_mask->to(in.dev, at::kFloat).reshape({-1}).contiguous();
+    if (gm.numel() != P) throw std::runtime_error("grad_mask must have " + std::to_string(P) + " elements");
+    in.g.grad_mask = gm.data_ptr<float>();
+  }
+  Tensor dLc = batch_image(dL_color, C, 3, H, W, in.dev, "dL_dout_color");
+  Tensor dLd = batch_image(dL_depth, C, 1, H, W, in.dev, "dL_dout_depth");
+  Tensor dLa = batch_image(dL_alpha, C, 1, H, W, in.dev, "dL_dout_alpha");
+  Tensor dLf = in.F ? batch_image(dL_feature, C, in.F, H, W, in.dev, "dL_dout_feature") : Tensor();
+  Tensor alphas_c = dev_f32(alphas, in.dev, "alpha");
+  Tensor radii_c = radii.to(in.dev, at::kInt).contiguous();
+  if (radii_c.dim() != 2 || radii_c.size(0) != C || radii_c.size(1) != P)
+    throw std::runtime_error("radii must be [C=" + std::to_string(C) + ", P=" + std::to_string(P) + "]");
+  if ((int64_t)num_instances.size() != C) throw std::runtime_error("num_instances must have C entries");
+  const std::vector<std::vector<int64_t>> shapes = {{P, 3}, {P, 3}, {P, in.F}, {P, 1}, {P, 3},
+                                                    {P, 6}, {P, in.M, 3}, {P, 3}, {P, 4}};
+  std::vector<Tensor> o;
+  for (int i = 0; i < 9; ++i) o.push_back(at::empty(shapes[i], f32));
+  if (densify.has_value()) {
+    const auto& d = *densify;
+    if (d.size() != 3) throw std::runtime_error("densify must hold (accum, denom, max_radius)");
+    for (const auto& t : d)
+      if (t.dim() != 1 || t.size(0) != P || t.scalar_type() != at::kFloat || t.device() != in.dev || !t.is_contiguous())
+        throw std::runtime_error("densify statistics must be contiguous fp32 (P,) tensors on the device");
+    in.g.densify_accum = d[0].data_ptr<float>();
+    in.g.densify_denom = d[1].data_ptr<float>();
+    in.g.max_radius = d[2].data_ptr<float>();
+  }
+  Tensor scratch = at::empty({(int64_t)gs_batch_backward_scratch_bytes(P, (int32_t)in.F, (int32_t)C)},
+                             f32.dtype(at::kByte));
+  const Tensor bin = binning.has_value() ? *binning : Tensor();
+  auto fp = [](const Tensor& t) -> const float* { return t.defined() ? t.data_ptr<float>() : nullptr; };
+  check(gs_backward_batch(&in.g, k.cams.data(), (int32_t)C, radii_c.data_ptr<int32_t>(), debug ? 1 : 0, (int)compat,
+                          geom.data_ptr(), nz(bin), img.data_ptr(), num_instances.data(), alphas_c.data_ptr<float>(),
+                          fp(dLc), fp(dLf), fp(dLd), fp(dLa), scratch.data_ptr(), o[0].data_ptr<float>(),
+                          o[1].data_ptr<float>(), static_cast<float*>(nz(o[2])), o[3].data_ptr<float>(),
+                          o[4].data_ptr<float>(), o[5].data_ptr<float>(), static_cast<float*>(nz(o[6])),
+                          o[7].data_ptr<float>(), o[8].data_ptr<float>(), reinterpret_cast<gs_stream_t>(stream)),
+        "rasterize_gaussians_batch_backward");
+  Tensor dsem = in.F_user != in.F ? o[2].narrow(1, 0, in.F_user) : o[2];
+  return {o[0], o[1], dsem, o[3], o[4], o[5], o[6], o[7], o[8]};
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -239,4 +384,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("abi_version", []() { return gs_version(); });
   m.def("forward", &forward);
   m.def("backward", &backward);
+  m.def("forward_batch", &forward_batch);
+  m.def("backward_batch", &backward_batch);
 }

@@ -169,3 +169,42 @@ def test_raw_params_render_records_match_torch_activations(P=30000, W=160, H=128
     scale = np.maximum(np.abs(c0[vis, 0]), np.abs(c0[vis, 2]))[:, None]
     assert np.all(np.abs(c1[vis, :3] - c0[vis, :3]) <= 1e-5 * scale)
     assert float(np.mean(r0 == r1)) >= 0.999
+
+
+@pytest.mark.parametrize("raw_params,F", [(True, 32), (False, 35)])
+def test_native_batch_binding_matches_ctypes_binding(raw_params, F, P=12000, W=144, H=112, C=3):
+    """The C++ batch fast path (lib/_gs_native.so forward_batch /
+    backward_batch) and the ctypes batch binding drive the same C ABI:
+    identical forward outputs and the same gradients (label mask, densify
+    statistics, a padded feature width 35 -> 36, raw parameters)."""
+    from dynamic3dgaussians_amd import _C
+    assert _C.native_loaded()
+    raw = _raw_scene(P, F, False, seed=77)
+    sets = _settings(camera_rig(C, W, H), W, H, "reference")
+    gen = torch.Generator(device=DEV).manual_seed(9)
+    label = (torch.rand(P, device=DEV, generator=gen) > 0.2).float()
+    ups = [torch.randn(C, 3, H, W, device=DEV, generator=gen), torch.randn(C, 1, H, W, device=DEV, generator=gen),
+           torch.randn(C, F, H, W, device=DEV, generator=gen)]
+    res = {}
+    keep = _C._native
+    try:
+        for mode in ("native", "ctypes"):
+            _C._native = keep if mode == "native" else None
+            leaves = {k: v.clone().requires_grad_(True) for k, v in raw.items()}
+            ras = GaussianRasterizerBatch(sets, track_densify=True, raw_params=raw_params)
+            im, radii, feat, depth, alpha = ras(means2D=torch.zeros(P, 3, device=DEV), label=label,
+                                                **_kw(leaves, raw_params))
+            torch.autograd.backward([im, depth, feat], ups)
+            torch.cuda.synchronize()
+            res[mode] = ([t.detach().cpu().numpy() for t in (im, radii, feat, depth, alpha)],
+                         {k: v.grad.cpu().numpy() for k, v in leaves.items()},
+                         {k: v.cpu().numpy() for k, v in ras.densify_stats.items()})
+    finally:
+        _C._native = keep
+    (fa, ga, sa), (fb, gb, sb) = res["native"], res["ctypes"]
+    for a, b in zip(fa, fb):
+        np.testing.assert_array_equal(a, b)
+    for k in ga:  # fp32 atomics: the summation order may differ between runs
+        assert np.linalg.norm(ga[k] - gb[k]) <= 1e-5 * max(np.linalg.norm(gb[k]), 1e-30), k
+    for k in sa:
+        np.testing.assert_allclose(sa[k], sb[k], rtol=1e-5, atol=1e-7)
