@@ -175,85 +175,110 @@ def make_settings(cams, dev, compat, sink=None):
     return out
 
 
-def stage_bytes(L, Pv, P, W, H, F, C=3, TB=256):
-    """Algorithmic HBM bytes per launch (with this build's
-    binning: tile plan, bucket, per-tile sort); K=1 (precomputed colours)."""
+def stage_bytes(L, Pv, P, W, H, F, compat, cams, C=3, TB=128):
+    """Algorithmic HBM bytes per camera and stage (restated
+    for this build's kernels) in a launch of `cams` cameras: per-Gaussian
+    inputs and outputs shared by the launch's cameras count once per launch
+    (1/cams per camera).  TB = binning workgroups per camera (gs_common.h
+    TB_BLOCKS); K = 1 (precomputed colours).  Reference numerics never read
+    the feature rows in the blend backward (their term of dL/dalpha is dead,
+    Q5; gs_render.hip FIXED_FEAT): no 4F per instance there."""
     npix = W * H
     T = ((W + 15) // 16) * ((H + 15) // 16)
+    feat_bwd = 4 * F if compat == "fixed" else 0
     return {
-        "preprocess": P * (12 + 12 + 16 + 4 + 12) + P * (4 + 64 + 24 + 4 + 8),
-        "scan": 8 * P + 3 * 4 * TB * T + 12 * T,       # tile histograms, row scans, ranges
-        "duplicate": 12 * P + 4 * TB * T + 8 * L,      # bucket (depth, id) keys by tile
+        # means, scales, rotations, opacity, colours in (+ the 3D covariance out)
+        # once per launch; per camera radii, render record, tile count, rect out
+        "preprocess": P * (56 + 24) / cams + P * (4 + 64 + 4 + 16),
+        "scan": 16 * P + 3 * 4 * TB * T + 12 * T,      # rect records in, block-tile counts, ranges
+        "duplicate": 16 * P + 4 * TB * T + 8 * L,      # rect records, block offsets, (depth, id) keys out
         "sort": 8 * L + 4 * L,                          # per-tile sort: keys in, ids out
-        "ranges": 0,
+        "ranges": 8 * T + 16 * T,                       # dispatch records from the ranges
         "render_fwd": L * (4 + 8 + 16 + 4 * C + 4 + 4 * F) + npix * 4 * (C + F + 2 + 1),
-        "render_bwd": L * (4 + 8 + 16 + 4 * C + 4 + 4 * F) + npix * 4 * (C + F + 4 + 1)
+        "render_bwd": L * (4 + 8 + 16 + 4 * C + 4) + L * feat_bwd + npix * 4 * (C + F + 4 + 1)
         + Pv * 4 * (3 + 4 + 1 + C + F + 1),
-        "preprocess_bwd": P * (12 + 12 + 16 + 24 + 12 + 12) + P * 4 * (3 + 6 + 3 + 4 + 3),
+        # per launch: means, scales, rotations, 3D covariance, opacity in and the
+        # 7 gradient outputs (92 B) out; per camera the accumulation record,
+        # radius and conic
+        "preprocess_bwd": P * (72 + 92) / cams + P * (40 + 4 + 20),
     }
 
 
-def load_pmc_traffic(stage, cams_per_launch):
-    """HBM bytes per launch from a committed rocprofv3 PMC summary, if any
-    (profiles/pmc_traffic.json, written by tools/pmc_traffic.py: bytes per
-    camera, measured on 27-camera batch launches) x the launch's cameras."""
-    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
-    try:
-        with open(path) as f:
-            d = json.load(f)
-        per_cam = d.get("bytes_per_camera", {}).get(stage)
-        return None if per_cam is None else int(per_cam * cams_per_launch)
-    except Exception:
-        return None
+def pmc_for(workload):
+    """The committed rocprofv3 PMC summaries (profiles/pmc_traffic.json,
+    pmc_valu.json, pmc_atomic.json: tools/gpu_pmc.sh) -- only when they were
+    measured on this bench line's exact workload (the record's `workload`
+    block); per-camera counts of another scene or rig say nothing about this
+    one.  Returns {name: summary} of the matching files."""
+    out = {}
+    for name in ("traffic", "valu", "atomic"):
+        try:
+            with open(os.path.join(REPO, "profiles", f"pmc_{name}.json")) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if d.get("workload") == workload:
+            out[name] = d
+    return out
 
 
 # stage -> (kernel key in profiles/pmc_valu.json, matrix-core cycles per MFMA)
 # matrix-core cycles per MFMA on one SIMD (MI355X_MICROARCH.md constants):
 # v_mfma_f32_16x16x32_bf16 16 (backward), v_mfma_f32_32x32x16_bf16 32 (forward)
 VALU_KERNEL = {"render_bwd": ("render_bwd", 16), "render_fwd": ("render_fwd", 32),
-               "sort": ("tile_sort", 0), "duplicate": ("tile_hist_kernel<true>", 0),
-               "preprocess": ("preprocess_fwd", 0), "preprocess_bwd": ("preprocess_bwd", 0)}
+               "sort": ("tile_sort", 0), "preprocess": ("preprocess_fwd", 0), "preprocess_bwd": ("preprocess_bwd", 0)}
 SIMDS, CLOCK_GHZ, VALU_ISSUE_CYC = 1024, 2.4, 4  # MI355X: 256 CUs x 4 SIMDs; wave64 VALU = 4 cycles
-
-
-def valu_view(stage, avg_ms, cams_per_launch):
-    """Issue-rate view of a kernel (the blend kernels are VALU/MFMA-issue
-    bound): committed per-camera instruction counts
-    (profiles/pmc_valu.json) x the launch's cameras, over the live launch time."""
-    try:
-        d = json.load(open(os.path.join(REPO, "profiles", "pmc_valu.json")))
-        if d.get("per") != "camera":
-            return None
-        key, mfma_cyc = VALU_KERNEL[stage]
-        k = {c: v * cams_per_launch for c, v in d["kernels"][key].items()}
-    except Exception:
-        return None
-    cyc = k["SQ_INSTS_VALU"] * VALU_ISSUE_CYC + k.get("SQ_INSTS_MFMA", 0) * mfma_cyc
-    avail = SIMDS * CLOCK_GHZ * 1e9 * avg_ms * 1e-3
-    return {"valu_insts_per_launch": k["SQ_INSTS_VALU"], "mfma_insts_per_launch": k.get("SQ_INSTS_MFMA", 0),
-            "issue_cycles_per_launch": int(cyc), "issue_frac": round(cyc / avail, 4),
-            "peak": f"{SIMDS} SIMDs x {CLOCK_GHZ} GHz, {VALU_ISSUE_CYC} cycles per wave64 VALU instruction"}
-
-
 ATOMIC_PEAK_GBS = 1300.0  # chip-wide float-atomic rate, MI355X_MICROARCH.md "Global float atomics"
 
 
-def atomic_view(stage, avg_ms, cams_per_launch):
-    """Memory-side float-atomic rate of a kernel (the backward blend commits
-    its per-Gaussian sums with global float atomics, which execute at the
-    memory side at one chip-wide rate): committed per-camera 64-B request
-    counts (profiles/pmc_atomic.json) x the launch's cameras, over the live
-    launch time, against that rate."""
+def issue_view(pmc, stage, avg_ms, cams):
+    """VALU + matrix-core issue cycles of a kernel (matching PMC counts per
+    camera x the launch's cameras) over the SIMD-cycles of its live launch time."""
     try:
-        d = json.load(open(os.path.join(REPO, "profiles", "pmc_atomic.json")))
-        req = d["requests_per_camera"][stage] * cams_per_launch
-    except Exception:
+        key, mfma_cyc = VALU_KERNEL[stage]
+        k = {c: v * cams for c, v in pmc["valu"]["kernels"][key].items()}
+    except (KeyError, TypeError):
+        return None
+    cyc = k["SQ_INSTS_VALU"] * VALU_ISSUE_CYC + k.get("SQ_INSTS_MFMA", 0) * mfma_cyc
+    avail = SIMDS * CLOCK_GHZ * 1e9 * avg_ms * 1e-3
+    return {"valu_insts_per_launch": int(k["SQ_INSTS_VALU"]), "mfma_insts_per_launch": int(k.get("SQ_INSTS_MFMA", 0)),
+            "issue_cycles_per_launch": int(cyc), "frac": round(cyc / avail, 4),
+            "peak": f"{SIMDS} SIMDs x {CLOCK_GHZ} GHz, {VALU_ISSUE_CYC} cycles per wave64 VALU instruction"}
+
+
+def atomic_view(pmc, stage, avg_ms, cams):
+    """Memory-side float-atomic traffic of a kernel (matching PMC 64-B request
+    counts per camera x the launch's cameras) over its live launch time,
+    against the chip-wide float-atomic rate."""
+    try:
+        req = pmc["atomic"]["requests_per_camera"][stage] * cams
+    except (KeyError, TypeError):
         return None
     if not req or avg_ms <= 0:
         return None
-    gbs = req * d.get("bytes_per_request", 64) / (avg_ms * 1e-3) / 1e9
+    gbs = req * pmc["atomic"].get("bytes_per_request", 64) / (avg_ms * 1e-3) / 1e9
     return {"requests_per_launch": int(req), "achieved": round(gbs, 1), "peak": ATOMIC_PEAK_GBS, "unit": "GB/s",
             "frac": round(gbs / ATOMIC_PEAK_GBS, 4)}
+
+
+def stage_table(stage_ms, alg_per_cam, pmc, cams):
+    """Per-stage HBM roofline of one step: algorithmic bytes (the 8(d) model)
+    and, with matching PMC counts, measured HBM bytes (FETCH_SIZE x 2 +
+    WRITE_SIZE, tools/pmc_traffic.py) over the stage's device time."""
+    meas = (pmc.get("traffic") or {}).get("bytes_per_camera", {})
+    out = {}
+    for st, ms in stage_ms.items():
+        if ms <= 0 or st not in alg_per_cam:
+            continue
+        row = {"ms": round(ms, 4), "alg_bytes": int(alg_per_cam[st] * cams)}
+        row["alg_frac"] = round(row["alg_bytes"] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+        if st in meas:
+            b = meas[st] * cams
+            row["hbm_bytes"] = int(b)
+            row["hbm_GBs"] = round(b / (ms * 1e-3) / 1e9, 1)
+            row["hbm_frac"] = round(b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+        out[st] = row
+    return out
 
 
 def calc_psnr(img1, img2):
@@ -646,20 +671,43 @@ def main():
     value = mpix_total / (ms_per_step / 1e3)
 
     # roofline of the dominant stage (live HIP-event durations over the timed region)
-    per_cam_bytes = [stage_bytes(L, Pv, args.gaussians, W_, H_, args.features) for L, Pv, _ in inst]
+    cams_per_launch = len(my_cams) if args.mode == "batch" else 1
+    per_cam_bytes = [stage_bytes(L, Pv, args.gaussians, W_, H_, args.features, args.compat, cams_per_launch)
+                     for L, Pv, _ in inst]
     launches = stages[dom][1]
     alg_bytes_total = sum(b[dom] for b in per_cam_bytes) * args.steps
     avg_ms = stages[dom][0] / max(launches, 1)
     alg_per_launch = alg_bytes_total / max(launches, 1)
     achieved = alg_per_launch / (avg_ms / 1e3) / 1e9 if avg_ms > 0 else 0.0
-    cams_per_launch = len(my_cams) if args.mode == "batch" else 1
-    traffic = load_pmc_traffic(dom, cams_per_launch)
-    roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic, "kernel": dom, "avg_launch_ms": round(avg_ms, 4),
-                "alg_bytes_per_launch": int(alg_per_launch),
-                "issue": valu_view(dom, avg_ms, cams_per_launch), "atomics": atomic_view(dom, avg_ms, cams_per_launch),
-                "cams_per_launch": cams_per_launch}
+    # the PMC-derived views only for the workload the counters were measured on
+    workload = {"gaussians": args.gaussians, "width": W_, "height": H_, "features": args.features,
+                "compat": args.compat, "rig": len(rig), "cams_per_launch": cams_per_launch, "seed": args.seed}
+    pmc = pmc_for(workload) if args.mode == "batch" and world == 1 else {}
+    meas = (pmc.get("traffic") or {}).get("bytes_per_camera", {})
+    hbm = {"achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(achieved / HBM_PEAK_GBS, 4),
+           "traffic": int(meas[dom] * cams_per_launch) if dom in meas else None}
+    issue = issue_view(pmc, dom, avg_ms, cams_per_launch)
+    atomics = atomic_view(pmc, dom, avg_ms, cams_per_launch)
+    # the binding roof: the highest of the HBM (algorithmic bytes), float-atomic
+    # and issue fractions of the dominant kernel
+    roofs = {"hbm": hbm}
+    if atomics:
+        roofs["atomics"] = atomics
+    if issue:
+        roofs["issue"] = issue
+    bound = max(roofs, key=lambda r: roofs[r]["frac"])
+    b = roofs[bound]
+    if bound == "issue":
+        b = {"achieved": b["frac"], "peak": 1.0, "unit": "fraction of SIMD issue cycles", "frac": b["frac"]}
+    roofline = {"bound": bound, "achieved": b["achieved"], "peak": b["peak"], "unit": b["unit"], "frac": b["frac"],
+                "traffic": hbm["traffic"], "kernel": dom, "avg_launch_ms": round(avg_ms, 4),
+                "alg_bytes_per_launch": int(alg_per_launch), "cams_per_launch": cams_per_launch,
+                "hbm": hbm, "atomics": atomics, "issue": issue,
+                "pmc_workload_matched": bool(pmc),
+                "stages": stage_table(stage_ms, {k: np.mean([pb[k] for pb in per_cam_bytes])
+                                                 for k in per_cam_bytes[0]}, pmc,
+                                      cams_per_launch if args.mode == "batch" else len(my_cams))}
 
     result = {
         "metric": METRIC, "value": round(value, 3), "unit": "Mpix/s", "n_gpus": world,

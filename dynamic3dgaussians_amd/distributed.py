@@ -61,12 +61,21 @@ class GradBucket:
     all_reduce() needs no pack/unpack copies of the gradients.  Clear the
     gradients with zero_grad() (one fill of the buffer) instead of the
     optimizer's zero_grad(set_to_none=True), which would unbind them.
+
+    track_reached=True (bound mode): a bound .grad exists whether or not the
+    step's loss reached the parameter, so an optimizer would step every
+    parameter (Adam moving an unreached one on its old moments) where the
+    single-process run leaves .grad None and skips it.  The bucket notes on
+    each rank which parameters autograd accumulated into (post-accumulate
+    hooks), sums those flags over the ranks in the same all_reduce, and after
+    it sets .grad = None on the parameters no rank reached (one small
+    device->host read of the flags); zero_grad() binds them again.
     """
 
     def __init__(self, params: Iterable[torch.Tensor] | Mapping[str, torch.Tensor],
                  extras: Dict[str, torch.Tensor] | None = None,
                  extras_from: tuple[Mapping[str, torch.Tensor], Sequence[str]] | None = None,
-                 bind_grads: bool = False, keys: Sequence[str] | None = None):
+                 bind_grads: bool = False, keys: Sequence[str] | None = None, track_reached: bool = False):
         if isinstance(params, Mapping):
             self._param_src, self._param_keys = params, list(keys if keys is not None else params.keys())
             self.params = [params[k] for k in self._param_keys]
@@ -85,8 +94,16 @@ class GradBucket:
         sizes = self._param_numel + list(self._extra_numel.values())
         self.sizes = sizes
         dev = self.params[0].device
-        self.flat = torch.zeros(sum(sizes), dtype=torch.float32, device=dev)
+        self.track = bool(track_reached and bind_grads)
+        n_flags = len(self.params) if self.track else 0
+        self.flat = torch.zeros(sum(sizes) + n_flags, dtype=torch.float32, device=dev)
         self.bound = bind_grads
+        self._reached = [False] * len(self.params)
+        self._unbound = set()
+        self._hooks = []
+        if self.track:
+            for i, p in enumerate(self.params):
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._hook(i)))
         self._views = []
         o = 0
         for p in self.params:
@@ -98,6 +115,11 @@ class GradBucket:
                 p.grad = v
         self._base = {}
         self.resync()
+
+    def _hook(self, i):
+        def mark(_p):
+            self._reached[i] = True
+        return mark
 
     # ---------------------------------------------------------------- checks
     def check_live(self) -> None:
@@ -121,6 +143,8 @@ class GradBucket:
                 raise StaleBucketError(f"statistic '{k}' changed size: build a new GradBucket")
         if self.bound:
             for i, (p, v) in enumerate(zip(self.params, self._views)):
+                if i in self._unbound and p.grad is None:
+                    continue  # unbound by all_reduce (reached by no rank); zero_grad() binds it again
                 if p.grad is None or p.grad.data_ptr() != v.data_ptr():
                     raise StaleBucketError(
                         f"parameter {i}'s .grad is no longer the bucket's view (zero_grad(set_to_none=True)?): "
@@ -130,6 +154,10 @@ class GradBucket:
     def zero_grad(self) -> None:
         """Bound mode: zero every gradient with one fill of the buffer."""
         if self.bound:
+            for i in self._unbound:
+                self.params[i].grad = self._views[i]
+            self._unbound.clear()
+            self._reached = [False] * len(self.params)
             n = sum(self._param_numel)
             self.flat[:n].zero_()
         else:
@@ -157,6 +185,8 @@ class GradBucket:
             # this rank's increment since the last synchronisation point
             torch.sub(t.reshape(-1), self._base[k].reshape(-1), out=self.flat[o:o + n])
             o += n
+        if self.track:
+            self.flat[o:].copy_(torch.tensor(self._reached, dtype=torch.float32))
 
     def unpack(self):
         o = 0
@@ -183,6 +213,12 @@ class GradBucket:
         self.pack()
         dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
         self.unpack()
+        if self.track:
+            reached = self.flat[len(self.flat) - len(self.params):].cpu()
+            for i, p in enumerate(self.params):
+                if reached[i] == 0:
+                    p.grad = None
+                    self._unbound.add(i)
         self.resync()
 
 

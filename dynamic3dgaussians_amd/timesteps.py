@@ -168,14 +168,25 @@ class TimestepDriver:
     losses.  `render(rendervar, cams)` returns the
     cameras' images [C, 3, H, W] and optional densification statistics
     (default: batch_renderer(settings_all)).  `targets(t)` -> [n_cams, 3, H, W]
-    images of timestep t (or [C_rank, ...] with `targets_sharded=True`)."""
+    images of timestep t, or only this rank's cameras' [C_rank, 3, H, W] with
+    `targets_sharded=True`.
+
+    Densification statistics: the loss divides every camera's image loss by
+    n_cams (the rig's mean), so each camera's means2D gradient is 1/n_cams of
+    the reference's one-camera-per-step gradient (train.py:422-425); the
+    statistic external.py:136-140 accumulates is the NORM of that gradient
+    (compared with an absolute threshold, external.py:247-259), so the
+    driver scales the increments back by n_cams: means2D_gradient_accum
+    holds the reference's per-view norms (the image loss being the only
+    term that reaches means2D, as in train.py's get_loss)."""
 
     def __init__(self, params: dict, variables: dict, optimizer, n_cams: int, render: Callable,
                  rank: int = 0, world: int = 1, group=None,
                  image_loss: Callable = l1_image_loss, extra_loss: Optional[Callable] = None,
-                 densify: Optional[Callable] = None):
+                 densify: Optional[Callable] = None, targets_sharded: bool = False):
         self.params, self.variables, self.optimizer = params, variables, optimizer
         self.n_cams = n_cams
+        self.targets_sharded = targets_sharded
         self.cams = shard_cameras(n_cams, rank, world)
         self.rank, self.world, self.group = rank, world, group
         self.render = render
@@ -196,7 +207,7 @@ class TimestepDriver:
         # hands the backward's tensors to the leaves, no accumulate kernels)
         self.bucket = GradBucket(self.params, extras_from=(self.variables, list(STATS[:2])),
                                  bind_grads=self.world > 1,
-                                 keys=keys)
+                                 keys=keys, track_reached=True)
 
     def _live_bucket(self):
         try:
@@ -215,7 +226,11 @@ class TimestepDriver:
         stats = None
         if self.cams:
             im, stats = self.render(rv, self.cams)
-            tg = targets if targets.shape[0] == len(self.cams) else targets[self.cams]
+            want = len(self.cams) if self.targets_sharded else self.n_cams
+            if targets.shape[0] != want:
+                raise ValueError(f"targets hold {targets.shape[0]} images; expected {want} "
+                                 f"({'this rank' if self.targets_sharded else 'the rig'}'s cameras)")
+            tg = targets if (self.targets_sharded or len(self.cams) == self.n_cams) else targets[self.cams]
             loss = self.image_loss(im, tg) / self.n_cams
         if self.extra_loss is not None:
             le = self.extra_loss(self.params, self.variables, rv, t) / self.world
@@ -227,7 +242,7 @@ class TimestepDriver:
             if stats is not None:
                 # this rank's cameras' statistics (external.py:136-140,
                 # train.py:288-290); the bucket sums the increments
-                v["means2D_gradient_accum"] += stats["means2D_gradient_accum"]
+                v["means2D_gradient_accum"] += stats["means2D_gradient_accum"] * float(self.n_cams)
                 v["denom"] += stats["denom"]
                 torch.maximum(v["max_2D_radius"], stats["max_2D_radius"], out=v["max_2D_radius"])
             bucket.all_reduce(self.group)

@@ -241,3 +241,50 @@ def test_bound_gradients_accumulate_into_the_bucket():
     p.grad = None  # what zero_grad(set_to_none=True) does
     with pytest.raises(StaleBucketError, match="zero_grad"):
         b.all_reduce()
+
+
+def _reach_worker(rank, world, port, q):
+    """a: reached on every rank; b: only on rank 0; c: on no rank."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        a, b, c = (torch.nn.Parameter(torch.ones(5)) for _ in range(3))
+        bucket = GradBucket({"a": a, "b": b, "c": c}, bind_grads=True, track_reached=True)
+        out = []
+        for step in range(2):
+            bucket.zero_grad()
+            bucket.check_live()
+            loss = (a * (rank + 1)).sum()
+            if rank == 0:
+                loss = loss + 2 * b.sum()
+            loss.backward()
+            bucket.all_reduce()
+            out.append([None if p.grad is None else p.grad.numpy().copy() for p in (a, b, c)])
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bucket_unbinds_parameters_no_rank_reached():
+    """with bound gradients every parameter has a .grad (a zero
+    view) whether or not the loss reached it, so Adam would step unreached
+    parameters on their old moments where one process leaves .grad None.
+    track_reached=True: after the all-reduce a parameter reached by no rank
+    has .grad None (the optimizer skips it), one reached by any rank keeps
+    the summed gradient, and zero_grad() binds the gradients again."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_reach_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(world):
+        for ga, gb, gc in res[r]:
+            assert (ga == 3.0).all()      # 1 + 2 from the two ranks
+            assert (gb == 2.0).all()      # rank 0 only, still summed and bound
+            assert gc is None             # no rank reached it

@@ -30,6 +30,9 @@ def main():
            "bytes_per_request": 64, "cams_per_launch": cams,
            "method": "rocprofv3 --pmc TCC_EA0_ATOMIC_sum on tools/batch_steps.py (27-camera launches), "
                      "per launch / cameras per launch"}
+    wl = os.environ.get("PMC_WORKLOAD")
+    if wl:
+        out["workload"] = json.loads(wl)
     path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_atomic.json")
     with open(path, "w") as f:
         json.dump(out, f, indent=1)

@@ -51,6 +51,9 @@ def main():
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate passes), FETCH_SIZE x2 "
                      "(gfx950 correction), KB -> bytes; tools/batch_steps.py (300k Gaussians, "
                      f"{cams} cameras 800x800 per launch, F = 32)"}
+    wl = os.environ.get("PMC_WORKLOAD")
+    if wl:
+        out["workload"] = json.loads(wl)
     path = os.environ.get("PMC_TRAFFIC_OUT") or os.path.join(
         os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_traffic.json")
     json.dump(out, open(path, "w"), indent=1)

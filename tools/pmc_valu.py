@@ -24,6 +24,9 @@ def main():
            "per": "camera", "cams_per_launch": cams,
            "method": "rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_SALU SQ_WAVES; per launch / cameras "
                      f"per launch; tools/batch_steps.py ({cams} cameras per launch)"}
+    wl = os.environ.get("PMC_WORKLOAD")
+    if wl:
+        out["workload"] = json.loads(wl)
     path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
                         "pmc_valu.json")
     json.dump(out, open(path, "w"), indent=1)
