@@ -87,6 +87,9 @@ def parse():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--step-times", action="store_true",
                     help="also report host timestamps of the timed steps (diagnostic)")
+    ap.add_argument("--sub-batches", type=int, default=int(os.environ.get("GS_BENCH_SUB_BATCHES", "1")),
+                    help="batch mode: the rank's cameras as this many camera batches (round robin) on their own "
+                         "HIP streams, so one batch's binning and launch tails overlap another's blend kernels")
     ap.add_argument("--mode", default=os.environ.get("GS_BENCH_MODE", "batch"), choices=["batch", "percam"],
                     help="batch: the rank's cameras through GaussianRasterizerBatch (one launch per stage "
                          "for all of them); percam: one GaussianRasterizer call per camera (the drop-in)")
@@ -506,17 +509,20 @@ def main():
 
     # one upstream gradient per camera, materialized once (the batch's
     # backward reads [C, ...] images like C per-camera backwards do)
-    def batch_inputs(setts):
-        C_ = len(setts)
-        ups = (up_color.expand(C_, -1, -1, -1).contiguous(), up_depth.expand(C_, -1, -1, -1).contiguous(),
-               up_feat.expand(C_, -1, -1, -1).contiguous() if up_feat is not None else None)
-        return GaussianRasterizerBatch(setts, raw_params=raw), ups
+    def batch_inputs(setts, n_sub=1):
+        n_sub = max(1, min(n_sub, len(setts), len(streams)))
+        parts = []
+        for gi in range(n_sub):
+            idx = list(range(gi, len(setts), n_sub))
+            C_ = len(idx)
+            ups = (up_color.expand(C_, -1, -1, -1).contiguous(), up_depth.expand(C_, -1, -1, -1).contiguous(),
+                   up_feat.expand(C_, -1, -1, -1).contiguous() if up_feat is not None else None)
+            parts.append((GaussianRasterizerBatch([setts[i] for i in idx], raw_params=raw), ups, streams[gi]))
+        return parts
 
-    batch_ras, ups_b = batch_inputs(settings)
+    batch_parts = batch_inputs(settings, args.sub_batches)
 
-    def step_batch(ras=batch_ras, ups=ups_b):
-        bucket.zero_grad()
-        rv = raw_rendervar(params, label, means2D_placeholder) if raw else params2rendervar(params, label)
+    def run_part(ras, ups, rv):
         up_c, up_d, up_f = ups
         if up_f is not None:  # G3 call (label + semantic_feature)
             im, radius, feat, depth, _ = ras(**rv)
@@ -524,6 +530,24 @@ def main():
         else:                 # G2 call (label only)
             im, radius, depth, _ = ras(**rv)
             torch.autograd.backward([im, depth], [up_c, up_d])
+
+    def step_batch(parts=batch_parts):
+        bucket.zero_grad()
+        rv = raw_rendervar(params, label, means2D_placeholder) if raw else params2rendervar(params, label)
+        if len(parts) == 1:
+            run_part(parts[0][0], parts[0][1], rv)
+        else:
+            # sub-batches on their own streams: autograd keeps each one's
+            # backward on its forward's stream and orders the leaves'
+            # gradient accumulation across them
+            main = torch.cuda.current_stream(dev)
+            for _, _, st in parts:
+                st.wait_stream(main)
+            for ras, ups, st in parts:
+                with torch.cuda.stream(st):
+                    run_part(ras, ups, rv)
+            for _, _, st in parts:
+                main.wait_stream(st)
         bucket.all_reduce()
         opt.step()
 
@@ -654,10 +678,10 @@ def main():
         if world > 1 and n_split >= world:
             rig_s = camera_rig(n_split, args.width, args.height, seed=args.seed)
             mine = shard_cameras(n_split, rank, world)
-            ras_s, ups_s = batch_inputs(make_settings([rig_s[c] for c in mine], dev, args.compat))
-            el_s = timed(lambda: step_batch(ras_s, ups_s))
+            parts_s = batch_inputs(make_settings([rig_s[c] for c in mine], dev, args.compat), args.sub_batches)
+            el_s = timed(lambda: step_batch(parts_s))
             cams_rank = [len(shard_cameras(n_split, r, world)) for r in range(world)]
-            del ras_s, ups_s
+            del parts_s
         else:
             el_s, cams_rank = elapsed, [args.cams]
         ms_s = el_s / args.steps * 1e3
@@ -671,7 +695,7 @@ def main():
     value = mpix_total / (ms_per_step / 1e3)
 
     # roofline of the dominant stage (live HIP-event durations over the timed region)
-    cams_per_launch = len(my_cams) if args.mode == "batch" else 1
+    cams_per_launch = len(batch_parts[0][0].settings_list) if args.mode == "batch" else 1
     per_cam_bytes = [stage_bytes(L, Pv, args.gaussians, W_, H_, args.features, args.compat, cams_per_launch)
                      for L, Pv, _ in inst]
     launches = stages[dom][1]
@@ -707,7 +731,7 @@ def main():
                 "pmc_workload_matched": bool(pmc),
                 "stages": stage_table(stage_ms, {k: np.mean([pb[k] for pb in per_cam_bytes])
                                                  for k in per_cam_bytes[0]}, pmc,
-                                      cams_per_launch if args.mode == "batch" else len(my_cams))}
+                                      len(my_cams))}
 
     result = {
         "metric": METRIC, "value": round(value, 3), "unit": "Mpix/s", "n_gpus": world,
@@ -725,7 +749,8 @@ def main():
                                "fwd+bwd of every camera + grad all-reduce + Adam",
                    "mode": ("camera batch (GaussianRasterizerBatch: one launch per stage for the rank's "
                             "cameras)" if args.mode == "batch" else "per camera (GaussianRasterizer drop-in)"),
-                   "optimizer": optim_kind, "streams": n_streams if args.mode == "percam" else 1,
+                   "optimizer": optim_kind,
+                   "streams": n_streams if args.mode == "percam" else len(batch_parts),
                    "activations": ("in-kernel (raw parameters, GS_FLAG_ACTIVATE)" if raw and args.mode == "batch"
                                    else "torch ops (params2rendervar)"),
                    "grad_sum": ("in-kernel (camera sum in preprocess_bwd)" if args.mode == "batch" else

@@ -21,6 +21,12 @@ F = 32 the pass is the F = 36 instantiation (32 matrix-core channels + a
 4-channel VALU tail: seg and ones) instead of a padded 64.  The ones channel
 renders sum(w) = 1 - T, which gives the seg channels their background term
 T * bg in reference numerics (where the alpha output is never written, Q1).
+In this layout the seg image is NOT bit-identical to the reference's second
+render when the background is nonzero: the second render adds T_final * bg
+with T_final the blend's running product, the fused pass (1 - sum w) * bg,
+equal in exact arithmetic and within fp32 rounding of each other -- the
+1e-5 bar of tests/test_gpu_fused.py::test_fused_colour_seg_f32_against_oracle
+(bit-identity holds only at bg = 0 and in the F = 3 layout above).
 
 Gradients.  dL/dseg_colors is the same per-Gaussian sum of w * dL/dseg as
 the second pass's dL/dcolors_precomp.  Geometry: in reference numerics the

@@ -17,6 +17,23 @@ fixtures -- data only -- are committed, the reference never travels).
    masks the gradients with `label` (Q12).  The stand-in replaces only the
    missing extension; nothing of the reference is built.
 
+3. cov3d.npz -- the reference's 3D covariance in Python: utils/general_utils.py
+   build_rotation / build_scaling_rotation / strip_symmetric (:78-110), composed
+   as scene/gaussian_model.py:40-44 (build_covariance_from_scaling_rotation:
+   L = R S, Sigma = L L^T, upper triangle), the Python twin of
+   CR/forward.cu:129-163 computeCov3D.  The module hard-codes device="cuda";
+   here its `torch` is a view of torch whose zeros() drop the device argument
+   (there is no GPU in the dev container) -- nothing else is changed.  Its
+   build_rotation normalises the quaternion; the CUDA kernel does not (Q7):
+   the fixture holds raw and normalised quaternions so the test can show both.
+
+4. cameras.npz -- the 3DGS camera matrices: utils/graphics_utils.py
+   getWorld2View2 / getProjectionMatrix (:38-71), composed as
+   scene/cameras.py:49-52 (world_view_transform, full_proj_transform,
+   camera_center; the .cuda() moves left out), for seeded R, T and fields of
+   view.  Pins camera.setup_camera (the helpers.py:68-95 form every G1 caller
+   uses) at a centred principal point, where the two forms must agree.
+
 Usage: python tests/golden/make_golden.py [--reference /root/reference]
 """
 from __future__ import annotations
@@ -159,12 +176,70 @@ def make_conventions(ref):
         json.dump(res, f)
 
 
+class _TorchOnCPU(types.ModuleType):
+    """torch as utils/general_utils.py sees it, with the hard-coded
+    device="cuda" of its zeros() calls redirected to the CPU."""
+
+    def __getattr__(self, k):
+        return getattr(torch, k)
+
+    @staticmethod
+    def zeros(*a, **kw):
+        kw.pop("device", None)
+        return torch.zeros(*a, **kw)
+
+
+def make_cov3d(ref):
+    gu = _load_module("ref_general_utils", os.path.join(ref, "utils", "general_utils.py"))
+    gu.torch = _TorchOnCPU("torch")
+    g = torch.Generator().manual_seed(3)
+    P = 512
+    scales = torch.exp(torch.randn(P, 3, generator=g) * 0.7 - 3.0)
+    rot_raw = torch.randn(P, 4, generator=g) * torch.exp(0.5 * torch.randn(P, 1, generator=g))
+    rot_unit = rot_raw / rot_raw.norm(dim=1, keepdim=True)
+    out = {"scales": scales.numpy(), "rotations_raw": rot_raw.numpy(), "rotations_unit": rot_unit.numpy()}
+    for tag, mod in (("1", 1.0), ("0p7", 0.7)):
+        # scene/gaussian_model.py:40-44 build_covariance_from_scaling_rotation
+        L = gu.build_scaling_rotation(mod * scales, rot_raw)
+        cov = L @ L.transpose(1, 2)
+        out[f"cov3D_mod{tag}"] = gu.strip_symmetric(cov).numpy().astype(np.float32)
+    np.savez_compressed(os.path.join(HERE, "cov3d.npz"), **out)
+
+
+def make_cameras(ref):
+    gr = _load_module("ref_graphics_utils", os.path.join(ref, "utils", "graphics_utils.py"))
+    rng = np.random.default_rng(4)
+    n = 16
+    Rs, Ts, fx, fy, Ws, Hs, wvt, full, centre = [], [], [], [], [], [], [], [], []
+    for i in range(n):
+        q, _ = np.linalg.qr(rng.standard_normal((3, 3)))
+        if np.linalg.det(q) < 0:
+            q[:, 0] = -q[:, 0]
+        R = q.astype(np.float64)
+        T = rng.uniform(-3, 3, 3)
+        W, H = int(rng.integers(64, 1921)), int(rng.integers(64, 1081))
+        fovx = float(rng.uniform(0.5, 1.6))
+        fovy = 2 * np.arctan(np.tan(fovx / 2) * H / W)
+        # scene/cameras.py:49-52
+        w = torch.tensor(gr.getWorld2View2(R, T)).transpose(0, 1)
+        p = gr.getProjectionMatrix(znear=0.01, zfar=100.0, fovX=fovx, fovY=fovy).transpose(0, 1)
+        f = w.unsqueeze(0).bmm(p.unsqueeze(0)).squeeze(0)
+        c = w.inverse()[3, :3]
+        Rs.append(R); Ts.append(T); fx.append(fovx); fy.append(fovy); Ws.append(W); Hs.append(H)  # noqa: E702
+        wvt.append(w.numpy()); full.append(f.numpy()); centre.append(c.numpy())  # noqa: E702
+    np.savez_compressed(os.path.join(HERE, "cameras.npz"), R=np.array(Rs), T=np.array(Ts), fovx=np.array(fx),
+                        fovy=np.array(fy), W=np.array(Ws), H=np.array(Hs), world_view_transform=np.array(wvt),
+                        full_proj_transform=np.array(full), camera_center=np.array(centre))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reference", default="/root/reference")
     a = ap.parse_args()
     make_sh(a.reference)
     make_conventions(a.reference)
+    make_cov3d(a.reference)
+    make_cameras(a.reference)
     print("wrote", os.listdir(HERE))
 
 

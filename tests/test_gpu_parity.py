@@ -416,3 +416,34 @@ def test_debug_mode_validates_and_passes_on_a_valid_scene():
     assert a[0] == b[0]
     for x, y in zip(a[1:6], b[1:6]):
         assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("compat", ["reference", "fixed"])
+def test_unnormalised_quaternions_q7(compat):
+    """Q7 (CR/forward.cu:129-163 and backward.cu:295-358): the reference's
+    kernels build the rotation from the RAW quaternion, without normalising
+    it (its Python callers normalise first, helpers.py:102, but the kernel
+    boundary does not).  Every other test scene feeds unit quaternions, where
+    the raw and the normalised forms coincide; here |q| spans about
+    0.6 .. 1.6, so the covariance, its 2D projection and the scale / rotation
+    gradients are the raw-quaternion ones: preprocess records bit-exact vs the
+    oracle, images at the forward bar, gradients <= 1e-4 relative L2."""
+    inp = H.scene(P=3000, F=8)
+    g = torch.Generator().manual_seed(17)
+    f = torch.exp(0.2 * torch.randn(3000, 1, generator=g)).clamp(0.6, 1.6)
+    inp["rotations"] = (inp["rotations"] * f).contiguous()
+    gf, of = _cmp_forward(inp, compat, 8)
+    P, W, Hh = 3000, inp["image_width"], inp["image_height"]
+    st_g, st_o = H.export_state(P, W, Hh, gf), of[6]
+    vis = st_o.radii > 0
+    np.testing.assert_array_equal(st_g["conic_opacity"][vis], st_o.conic_opacity[vis])
+    # the raw quaternion really changes the covariance (Q7 is exercised)
+    unit = dict(inp, rotations=torch.nn.functional.normalize(inp["rotations"], dim=1))
+    assert not np.array_equal(H.oracle_forward(unit, compat)[6].conic_opacity[vis], st_o.conic_opacity[vis])
+    grads = H.upstream_grads(Hh, W, 8)
+    gb = H.gpu_backward(inp, gf, grads, compat)
+    ob = H.oracle_backward(inp, of, grads, compat)
+    for name, a, b in zip(GRAD_NAMES, gb, ob):
+        if b.size == 0 or not np.any(b):
+            continue
+        assert H.rel_l2(a, b) <= 1e-4, (name, H.rel_l2(a, b))
