@@ -23,7 +23,12 @@ Scaling (headline: weak): every rank renders its own 27 cameras of a 27*N
 camera rig with the full Gaussian set replicated; value = all ranks' pixels /
 step time.  `--cams-total T` makes the headline the north star's step split
 across the ranks instead (BASELINE.json configs[3], strong scaling): ONE rig
-of T cameras, camera c on rank c mod N (distributed.shard_cameras), each rank
+of T cameras split over the ranks (--split cameras, the default: camera c on
+rank c mod N, distributed.shard_cameras; --split windows: the first
+N * (T // N) cameras whole, c mod N, the T % N left over cut into N bands of
+tile rows, band k on rank k -- image sharding, gs_camera tile_*,
+distributed.shard_camera_windows; measured slower on the 27-camera rig at
+8 ranks), each rank
 renders its share as one batch, then the gradient all-reduce and Adam;
 value = T cameras' pixels / step time.  At N > 1 the weak headline is
 followed by the same measurement of the 27-camera split step, reported as
@@ -58,7 +63,7 @@ sys.path.insert(0, REPO)
 
 from dynamic3dgaussians_amd import _lib  # noqa: E402
 from dynamic3dgaussians_amd.camera import camera_rig  # noqa: E402
-from dynamic3dgaussians_amd.distributed import GradBucket, shard_cameras  # noqa: E402
+from dynamic3dgaussians_amd.distributed import GradBucket, shard_camera_windows, shard_cameras  # noqa: E402
 from dynamic3dgaussians_amd.optim import FusedAdam  # noqa: E402
 from dynamic3dgaussians_amd.rasterizer import (GaussianRasterizationSettings,  # noqa: E402
                                                GaussianRasterizer, GaussianRasterizerBatch, GradientSink)
@@ -76,7 +81,14 @@ def parse():
     ap.add_argument("--gaussians", type=int, default=300_000)
     ap.add_argument("--cams", type=int, default=27, help="cameras per rank per step (weak scaling)")
     ap.add_argument("--cams-total", type=int, default=0,
-                    help="strong scaling: one rig of this many cameras split over the ranks (c mod N)")
+                    help="strong scaling: one rig of this many cameras split over the ranks (see --split)")
+    ap.add_argument("--split", default="cameras", choices=["cameras", "windows"],
+                    help="strong-scaling split: balanced with image sharding of the left-over cameras "
+                         "(windows) or whole cameras c mod N (cameras)")
+    ap.add_argument("--proxy-world", type=int, default=0,
+                    help="one GPU standing in for rank --proxy-rank of an N-rank --cams-total split: the "
+                         "rank's own cameras and windows, no collective (the per-rank shape)")
+    ap.add_argument("--proxy-rank", type=int, default=0)
     ap.add_argument("--cpu-tiles", type=int, default=10,
                     help="CPU baseline sample: a TxT block of 16x16 tiles at the centre of camera 0")
     ap.add_argument("--width", type=int, default=800)
@@ -165,16 +177,25 @@ def raw_rendervar(params, label, means2D):
     return rv
 
 
-def make_settings(cams, dev, compat, sink=None):
+def split_shard(n_cams, rank, world, how, W, H):
+    """[(camera, tile window or None)] of `rank` in a `world`-rank split of an
+    n_cams rig (--split)."""
+    if how == "cameras":
+        return [(c, None) for c in shard_cameras(n_cams, rank, world)]
+    return shard_camera_windows(n_cams, rank, world, (W + 15) // 16, (H + 15) // 16)
+
+
+def make_settings(cams, dev, compat, sink=None, windows=None):
     out = []
-    for c in cams:
+    for i, c in enumerate(cams):
         out.append(GaussianRasterizationSettings(
             image_height=c.H, image_width=c.W, tanfovx=c.tanfovx, tanfovy=c.tanfovy,
             c_x=c.c_x, c_y=c.c_y, bg=torch.zeros(3, device=dev), scale_modifier=1.0,
             viewmatrix=torch.from_numpy(c.viewmatrix.copy()).to(dev),
             projmatrix=torch.from_numpy(c.projmatrix.copy()).to(dev), sh_degree=0,
             campos=torch.from_numpy(c.campos.copy()).to(dev), prefiltered=False, debug=False,
-            confidence=None, compat=compat, grad_sink=sink))
+            confidence=None, compat=compat, grad_sink=sink,
+            tile_window=None if windows is None else windows[i]))
     return out
 
 
@@ -429,12 +450,19 @@ def main():
     torch.manual_seed(args.seed)
 
     strong = args.cams_total > 0
+    my_windows = None
+    if args.proxy_world and (world > 1 or not strong):
+        raise SystemExit("--proxy-world stands in for one rank of a --cams-total split on ONE process")
     if strong:
-        # the north star's step: one rig, camera c on rank c mod N
-        if args.cams_total < world:
-            raise SystemExit(f"--cams-total {args.cams_total} < {world} ranks")
+        # the north star's step: one rig split over the ranks (--split)
+        s_rank, s_world = (args.proxy_rank, args.proxy_world) if args.proxy_world else (rank, world)
+        if args.split == "cameras" and args.cams_total < s_world:
+            raise SystemExit(f"--cams-total {args.cams_total} < {s_world} ranks")
         rig = camera_rig(args.cams_total, args.width, args.height, seed=args.seed)
-        my_cams = [rig[c] for c in shard_cameras(args.cams_total, rank, world)]
+        shard = split_shard(args.cams_total, s_rank, s_world, args.split, args.width, args.height)
+        my_cams = [rig[c] for c, _ in shard]
+        if any(w is not None for _, w in shard):
+            my_windows = [w for _, w in shard]
     else:
         rig = camera_rig(args.cams * world, args.width, args.height, seed=args.seed)
         my_cams = rig[rank * args.cams:(rank + 1) * args.cams]
@@ -444,7 +472,7 @@ def main():
     # leaves; GS_BENCH_SINK=0 restores autograd's accumulation.
     use_sink = os.environ.get("GS_BENCH_SINK", "1") != "0"
     sink = GradientSink() if use_sink else None
-    settings = make_settings(my_cams, dev, args.compat, sink)
+    settings = make_settings(my_cams, dev, args.compat, sink, my_windows)
     params, label = make_params(args, dev)
     # the CPU-baseline / PSNR leg renders the initial scene (independent of the
     # optimizer steps taken by warmup and timing)
@@ -481,16 +509,18 @@ def main():
     inst = []
     with torch.no_grad():
         rv = params2rendervar(params, label)
+        from dynamic3dgaussians_amd import _C
         for s in settings:
-            from dynamic3dgaussians_amd import _C
-            out = _C.rasterize_gaussians(
+            # one camera (and its tile window) through the batch entry point
+            out = _C.rasterize_gaussians_batch(
                 s.bg, rv["means3D"], rv["colors_precomp"], rv.get("semantic_feature"),
                 rv["opacities"], rv["scales"], rv["rotations"], 1.0, torch.Tensor([]),
-                s.viewmatrix, s.projmatrix, s.c_x, s.c_y, s.tanfovx, s.tanfovy, H_, W_,
-                torch.Tensor([]), 0, s.campos, False, False, compat=args.compat)
-            # list instances actually binned (the byte model's L) and the
-            # reference's num_rendered
-            inst.append((_C.binned_instances(out[8], H_, W_), int((out[5] > 0).sum().item()), out[0]))
+                s.viewmatrix.reshape(1, 16), s.projmatrix.reshape(1, 16), [s.c_x], [s.c_y], [s.tanfovx],
+                [s.tanfovy], H_, W_, torch.Tensor([]), 0, s.campos.reshape(1, 3), False, False,
+                compat=args.compat, windows=[s.tile_window])
+            # list instances actually binned (the byte model's L), visible
+            # Gaussians and the reference's num_rendered
+            inst.append((int(out[9][0]), int((out[5][0] > 0).sum().item()), int(out[0][0])))
     del out
 
     # 4 = the box's hardware queues per process (GPU_MAX_HW_QUEUES): measured
@@ -630,13 +660,15 @@ def main():
     # the other call pattern on the same scene, timed the same way (reported
     # beside the headline: the per-camera drop-in or the camera batch)
     other = "percam" if args.mode == "batch" else "batch"
-    for _ in range(args.warmup):
+    if my_windows is not None:
+        other = None  # the per-camera drop-in renders whole cameras only
+    for _ in range(args.warmup if other else 0):
         step(other)
     torch.cuda.synchronize()
     if dist_on:
         dist.barrier()
     t1 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(args.steps if other else 0):
         step(other)
     torch.cuda.synchronize()
     if dist_on:
@@ -673,25 +705,37 @@ def main():
     # scaling), measured after a weak-scaling headline at N > 1; at N = 1 it
     # is the headline's own step (27 cameras on one rank).
     split = None
+    sharding_note = ("first N*(T//N) cameras whole, c mod N; the T%N left over in N bands of tile rows "
+                     "(distributed.shard_camera_windows)" if args.split == "windows" else
+                     "camera c on rank c mod N (distributed.shard_cameras)")
     if not strong and args.mode == "batch":
         n_split = args.cams
-        if world > 1 and n_split >= world:
+        if world > 1:
             rig_s = camera_rig(n_split, args.width, args.height, seed=args.seed)
-            mine = shard_cameras(n_split, rank, world)
-            parts_s = batch_inputs(make_settings([rig_s[c] for c in mine], dev, args.compat), args.sub_batches)
+            mine = split_shard(n_split, rank, world, args.split, args.width, args.height)
+            wins = [w for _, w in mine] if any(w is not None for _, w in mine) else None
+            parts_s = batch_inputs(make_settings([rig_s[c] for c, _ in mine], dev, args.compat, None, wins),
+                                   args.sub_batches)
             el_s = timed(lambda: step_batch(parts_s))
-            cams_rank = [len(shard_cameras(n_split, r, world)) for r in range(world)]
+            cams_rank = [len(split_shard(n_split, r, world, args.split, args.width, args.height))
+                         for r in range(world)]
             del parts_s
         else:
             el_s, cams_rank = elapsed, [args.cams]
         ms_s = el_s / args.steps * 1e3
         split = {"cams_total": n_split, "cams_per_rank": cams_rank, "ms_per_step": round(ms_s, 3),
                  "value": round(n_split * W_ * H_ / 1e6 / (ms_s / 1e3), 3), "unit": "Mpix/s",
-                 "scaling": "strong", "sharding": "camera c on rank c mod N (distributed.shard_cameras)"}
+                 "scaling": "strong", "sharding": sharding_note}
 
     ms_per_step = elapsed / args.steps * 1e3
     n_cams_total = args.cams_total if strong else world * args.cams
     mpix_total = n_cams_total * W_ * H_ / 1e6
+    if args.proxy_world:
+        # one rank's share: its own windows' pixels
+        gx, gy = (W_ + 15) // 16, (H_ + 15) // 16
+        share = sum(1.0 if w is None else (w[2] - w[0]) * (w[3] - w[1]) / (gx * gy)
+                    for w in (my_windows or [None] * len(my_cams)))
+        mpix_total = share * W_ * H_ / 1e6
     value = mpix_total / (ms_per_step / 1e3)
 
     # roofline of the dominant stage (live HIP-event durations over the timed region)
@@ -742,8 +786,10 @@ def main():
                        "sums as MFMA contractions of 3-piece bf16 splits (products to 2^-26 relative, "
                        "fp32 accumulation): tests/test_gpu_parity.py holds them to the oracle at 1e-5 / 1e-4"),
         "data": "synthetic",
-        "config": {"workload": (f"{args.gaussians // 1000}k Gaussians x {args.cams_total} cams split over "
-                                f"{world} rank(s)" if strong else
+        "config": {"workload": (f"rank {args.proxy_rank} of {args.proxy_world} of {args.gaussians // 1000}k "
+                                f"Gaussians x {args.cams_total} cams split ({args.split})" if args.proxy_world else
+                                f"{args.gaussians // 1000}k Gaussians x {args.cams_total} cams split over "
+                                f"{world} rank(s) ({args.split})" if strong else
                                 f"{args.gaussians // 1000}k Gaussians x {args.cams} cams/rank") +
                                f" x {W_}x{H_}, F={args.features} semantic channels, colors_precomp; "
                                "fwd+bwd of every camera + grad all-reduce + Adam",
@@ -761,16 +807,17 @@ def main():
         "roofline": roofline,
         "stages_ms_per_step": {k: round(v, 4) for k, v in stage_ms.items()},
         "split_step": split,
-        "other_mode": {"mode": other, "ms_per_step": round(other_elapsed / args.steps * 1e3, 3),
-                       "value": round(mpix_total / (other_elapsed / args.steps), 3),
-                       "streams": n_streams if other == "percam" else 1},
+        "other_mode": None if other is None else {
+            "mode": other, "ms_per_step": round(other_elapsed / args.steps * 1e3, 3),
+            "value": round(mpix_total / (other_elapsed / args.steps), 3),
+            "streams": n_streams if other == "percam" else 1},
         "instances_per_cam": int(np.mean([L for L, _, _ in inst])),
         "num_rendered_per_cam": int(np.mean([R for _, _, R in inst])),
     }
     if args.step_times:
         result["host_step_ms"] = [round((b - a) * 1e3, 3) for a, b in zip([t0] + host_marks, host_marks)]
         result["tail_ms"] = round((t0 + elapsed - host_marks[-1]) * 1e3, 3) if world == 1 else None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and settings[0].tile_window is None:
         cb, psnr, psnr_gt = cpu_baseline(args, params0, label, my_cams[0], settings[0], dev)
         result["cpu_baseline"] = cb
         result["psnr_vs_oracle_db"] = round(psnr, 2) if np.isfinite(psnr) else "inf"

@@ -417,8 +417,11 @@ def mark_visible(means3D, viewmatrix, projmatrix):
 # Camera batches (include/gsplat_hip.h gs_*_batch; no reference analogue): the
 # C cameras of one multi-camera step rendered with one launch per stage.
 
-def _camera_batch(dev, background, viewmatrices, projmatrices, campos, c_x, c_y, tan_fovx, tan_fovy, W, H):
+def _camera_batch(dev, background, viewmatrices, projmatrices, campos, c_x, c_y, tan_fovx, tan_fovy, W, H,
+                  windows=None):
     C = len(c_x)
+    if windows is not None and len(windows) != C:
+        raise RuntimeError("tile windows: one (x0, y0, x1, y1) per camera")
     if not (1 <= C <= 64):
         raise _lib.GsplatError(f"camera batch size {C} outside 1..64")
     if not (len(c_y) == len(tan_fovx) == len(tan_fovy) == C):
@@ -433,13 +436,23 @@ def _camera_batch(dev, background, viewmatrices, projmatrices, campos, c_x, c_y,
                            campos=cpos.data_ptr() + 12 * c, background=bg.data_ptr(), c_x=float(c_x[c]),
                            c_y=float(c_y[c]), tan_fovx=float(tan_fovx[c]), tan_fovy=float(tan_fovy[c]),
                            image_width=int(W), image_height=int(H))
+        if windows is not None and windows[c] is not None:
+            cams[c].tile_x0, cams[c].tile_y0, cams[c].tile_x1, cams[c].tile_y1 = (int(v) for v in windows[c])
     return cams, C, [view, proj, cpos, bg]
+
+
+def _windows_arg(windows, C):
+    """Tile windows as the native binding takes them: C x [x0, y0, x1, y1]
+    (all 0 = the whole image), or an empty list for none."""
+    if windows is None:
+        return []
+    return [[0, 0, 0, 0] if w is None else [int(v) for v in w] for w in windows]
 
 
 def rasterize_gaussians_batch(background, means3D, colors, semantic_feature, opacity, scales, rotations,
                               scale_modifier, cov3D_precomp, viewmatrices, projmatrices, c_x, c_y, tan_fovx,
                               tan_fovy, image_height, image_width, sh, degree, campos, prefiltered, debug,
-                              *, compat=None, activate=False):
+                              *, compat=None, activate=False, windows=None):
     """The forward of C cameras at once (gs_forward_plan_batch +
     gs_forward_render_batch): the arguments of rasterize_gaussians with
     per-camera matrices stacked ([C,4,4] or [C,16], campos [C,3]) and the
@@ -448,7 +461,8 @@ def rasterize_gaussians_batch(background, means3D, colors, semantic_feature, opa
     radii[C,P] int32, geomBuffer, binningBuffer, imgBuffer, num_instances[C]);
     camera c's outputs equal rasterize_gaussians' for that camera.
     `activate`: opacity / scales / rotations are the raw parameters
-    (logit, log, unnormalised; GS_FLAG_ACTIVATE)."""
+    (logit, log, unnormalised; GS_FLAG_ACTIVATE).  `windows`: per camera a
+    tile window (x0, y0, x1, y1) or None (gs_camera tile_*)."""
     L_ = _lib.load()
     cm = _compat_code(compat)
     nat = _native_mod()
@@ -459,7 +473,7 @@ def rasterize_gaussians_batch(background, means3D, colors, semantic_feature, opa
                                      viewmatrices, projmatrices, [float(x) for x in c_x], [float(x) for x in c_y],
                                      [float(x) for x in tan_fovx], [float(x) for x in tan_fovy], int(image_height),
                                      int(image_width), _opt(sh), int(degree), campos, bool(prefiltered),
-                                     bool(debug), cm, bool(activate),
+                                     bool(debug), cm, bool(activate), _windows_arg(windows, len(c_x)),
                                      torch.cuda.current_stream(means3D.device).cuda_stream)
         except RuntimeError as ex:
             raise _lib.GsplatError(str(ex)) from None
@@ -468,7 +482,7 @@ def rasterize_gaussians_batch(background, means3D, colors, semantic_feature, opa
     dev, P = inp.device, inp.P
     H, W = int(image_height), int(image_width)
     cams, C, keep = _camera_batch(dev, background, viewmatrices, projmatrices, campos, c_x, c_y, tan_fovx,
-                                  tan_fovy, W, H)
+                                  tan_fovy, W, H, windows)
     f32 = dict(dtype=torch.float32, device=dev)
     u8 = dict(dtype=torch.uint8, device=dev)
     if P == 0:
@@ -507,7 +521,7 @@ def rasterize_gaussians_batch_backward(background, means3D, radii, colors, seman
                                        dL_dout_depth, dL_dout_alpha, sh, degree, campos, geomBuffer,
                                        num_instances, binningBuffer, imageBuffer, alphas, debug, *,
                                        compat=None, grad_mask=None, densify=None, opacity=None,
-                                       activate=False):
+                                       activate=False, windows=None):
     """The backward of a camera batch (gs_backward_batch): the arguments of
     rasterize_gaussians_backward with stacked per-camera matrices, scalars
     and upstream gradients ([C, ...]), in the binding's positional camera
@@ -532,6 +546,7 @@ def rasterize_gaussians_batch_backward(background, means3D, radii, colors, seman
                                       geomBuffer, [int(x) for x in num_instances], _opt(binningBuffer),
                                       imageBuffer, alphas, bool(debug), cm, _opt(grad_mask),
                                       None if densify is None else list(densify), _opt(opacity), bool(activate),
+                                      _windows_arg(windows, len(c_x)),
                                       torch.cuda.current_stream(means3D.device).cuda_stream)
         except RuntimeError as ex:
             raise _lib.GsplatError(str(ex)) from None
@@ -547,7 +562,7 @@ def rasterize_gaussians_batch_backward(background, means3D, radii, colors, seman
         return (z(0, 3), z(0, 3), z(0, inp.F_user), z(0, 1), z(0, 3), z(0, 6), z(0, inp.M, 3),
                 z(0, 3), z(0, 4))
     cams, C, keep = _camera_batch(dev, background, viewmatrices, projmatrices, campos, c_x, c_y, tan_fovx,
-                                  tan_fovy, W, H)
+                                  tan_fovy, W, H, windows)
     g = inp.struct(_lib.GS_FLAG_ACTIVATE if activate else 0)
     if grad_mask is not None:
         gm = grad_mask.to(device=dev, dtype=torch.float32).reshape(-1).contiguous()

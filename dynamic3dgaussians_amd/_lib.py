@@ -16,7 +16,7 @@ _lock = threading.Lock()
 _lib = None
 
 c_void_p = ctypes.c_void_p
-ABI_VERSION = 8  # include/gsplat_hip.h GS_ABI_VERSION
+ABI_VERSION = 9  # include/gsplat_hip.h GS_ABI_VERSION
 GS_FLAG_ACCUMULATE = 1  # include/gsplat_hip.h
 GS_FLAG_ACTIVATE = 2  # include/gsplat_hip.h: raw opacity / scale / rotation parameters
 c_int32, c_int64, c_float, c_size_t = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_size_t
@@ -39,7 +39,8 @@ class GsCamera(ctypes.Structure):
     _fields_ = [("viewmatrix", c_void_p), ("projmatrix", c_void_p), ("campos", c_void_p),
                 ("background", c_void_p), ("c_x", c_float), ("c_y", c_float),
                 ("tan_fovx", c_float), ("tan_fovy", c_float),
-                ("image_width", c_int32), ("image_height", c_int32)]
+                ("image_width", c_int32), ("image_height", c_int32),
+                ("tile_x0", c_int32), ("tile_y0", c_int32), ("tile_x1", c_int32), ("tile_y1", c_int32)]
 
 
 class GsNeighborGraph(ctypes.Structure):

@@ -230,6 +230,17 @@ static int make_batch(const gs_camera* cams, int C, int P, int W, int H, CamBatc
       return fail(-1, "camera %d: batch camera matrices must be contiguous ([C,16], [C,16], [C,3])", c);
     if (k.background != cams[0].background)
       return fail(-1, "camera %d: the cameras of a batch share one background", c);
+    const int gx = (W + TILE - 1) / TILE, gy = (H + TILE - 1) / TILE;
+    if (k.tile_x0 == 0 && k.tile_y0 == 0 && k.tile_x1 == 0 && k.tile_y1 == 0) {
+      cb.win[c][0] = 0; cb.win[c][1] = 0; cb.win[c][2] = (uint16_t)gx; cb.win[c][3] = (uint16_t)gy;
+    } else {
+      if (k.tile_x0 < 0 || k.tile_y0 < 0 || k.tile_x0 >= k.tile_x1 || k.tile_y0 >= k.tile_y1 || k.tile_x1 > gx ||
+          k.tile_y1 > gy)
+        return fail(-1, "camera %d: tile window [%d, %d) x [%d, %d) outside the %d x %d tile grid", c, k.tile_x0,
+                    k.tile_x1, k.tile_y0, k.tile_y1, gx, gy);
+      cb.win[c][0] = (uint16_t)k.tile_x0; cb.win[c][1] = (uint16_t)k.tile_y0;
+      cb.win[c][2] = (uint16_t)k.tile_x1; cb.win[c][3] = (uint16_t)k.tile_y1;
+    }
     cb.c_x[c] = k.c_x;
     cb.c_y[c] = k.c_y;
     cb.tanx[c] = k.tan_fovx;

@@ -178,7 +178,11 @@ struct CamBatch {
   float c_x[GS_MAX_CAMS], c_y[GS_MAX_CAMS], tanx[GS_MAX_CAMS], tany[GS_MAX_CAMS];
   int64_t bin_off[GS_MAX_CAMS];  // byte offset of camera c's binning buffer
   int64_t bin_L[GS_MAX_CAMS];    // camera c's tile-list length (instances)
+  uint16_t win[GS_MAX_CAMS][4];  // camera c's tile window [x0, x1) x [y0, y1) (gs_camera tile_*)
 };
+__host__ __device__ inline bool in_window(const CamBatch& cb, int c, int tx, int ty) {
+  return tx >= cb.win[c][0] && tx < cb.win[c][2] && ty >= cb.win[c][1] && ty < cb.win[c][3];
+}
 template <class T>
 __host__ __device__ inline T* shift_bytes(T* p, int64_t bytes) {
   return p ? reinterpret_cast<T*>(reinterpret_cast<char*>(const_cast<typename std::remove_const<T>::type*>(p)) + bytes)

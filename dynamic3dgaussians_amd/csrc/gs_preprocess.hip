@@ -325,8 +325,10 @@ __global__ __launch_bounds__(256) void preprocess_fwd_kernel(PreprocessArgs a0, 
   const float fx1 = fminf(fmaxf(floorf((px + ex) / TILE) + 1.f, (float)rmin.x), (float)rmax.x);
   const float fy0 = fminf(fmaxf(ceilf((py - ey - (TILE - 1)) / TILE), (float)rmin.y), (float)rmax.y);
   const float fy1 = fminf(fmaxf(floorf((py + ey) / TILE) + 1.f, (float)rmin.y), (float)rmax.y);
-  const int bx0 = (int)fx0, by0 = (int)fy0;
-  const int bx1 = max((int)fx1, bx0), by1 = max((int)fy1, by0);
+  // ... and to the camera's tile window (gs_camera tile_*: image sharding)
+  const uint16_t* win = batch.win[blockIdx.y];
+  const int bx0 = max((int)fx0, (int)win[0]), by0 = max((int)fy0, (int)win[1]);
+  const int bx1 = max(min((int)fx1, (int)win[2]), bx0), by1 = max(min((int)fy1, (int)win[3]), by0);
   a.rect[g] = make_uint4((uint32_t)bx0 | ((uint32_t)by0 << 16), (uint32_t)bx1 | ((uint32_t)by1 << 16),
                          __float_as_uint(pv.z), (uint32_t)((rmax.y - rmin.y) * (rmax.x - rmin.x)));
 }

@@ -415,6 +415,22 @@ __global__ __launch_bounds__(64 * WPB_FWD) __attribute__((amdgpu_waves_per_eu(fw
   const float sx0 = (float)qx0, sx1 = sx0 + (float)(STRIP_W - 1);
   const float sy0 = (float)qy0, sy1 = sy0 + (float)(STRIP_H - 1);
   const uint2 range = make_uint2(trec.y, trec.z);
+  if (!in_window(cb, cam, tx, ty)) {
+    // outside the camera's tile window (image sharding, gs_camera tile_*):
+    // zeros, and an empty walk for the backward
+    if (lane == 0) ca.smax[item] = 0u;
+    if (inside) {
+      const size_t HW = (size_t)H * W, pix = (size_t)py * W + px;
+      n_contrib[pix] = 0u;
+      out_color[pix] = 0.f;
+      out_color[HW + pix] = 0.f;
+      out_color[2 * HW + pix] = 0.f;
+      out_depth[pix] = 0.f;
+      if (out_alpha) out_alpha[pix] = 0.f;
+      for (int c = 0; c < F; ++c) out_feature[(size_t)c * HW + pix] = 0.f;
+    }
+    return;
+  }
 
   float T = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f, Dp = 0.f;
   float SF[NSF];
@@ -841,6 +857,7 @@ __global__ __launch_bounds__(64 * WPB_BWD) __attribute__((amdgpu_waves_per_eu(bw
   const float sy0 = (float)qy0, sy1 = sy0 + (float)(STRIP_H - 1);
   const float cx = sx0 + 0.5f * (STRIP_W - 1), cy = sy0 + 0.5f * (STRIP_H - 1);  // strip centre
   const uint2 range = make_uint2(trec.y, trec.z);
+  if (!in_window(cb, cam, tx, ty)) return;  // outside the camera's tile window: no contribution
   const size_t HW = (size_t)H * W, pix = inside ? (size_t)py * W + px : 0;
 
 #ifdef GS_STAMPS

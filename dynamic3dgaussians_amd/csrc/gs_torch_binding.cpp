@@ -242,7 +242,7 @@ struct Cameras {
   std::vector<gs_camera> cams;
   Cameras(const at::Device& dev, const Tensor& bg_, const Tensor& views, const Tensor& projs, const Tensor& campos,
           const std::vector<double>& cx, const std::vector<double>& cy, const std::vector<double>& tx,
-          const std::vector<double>& ty, int64_t W, int64_t H) {
+          const std::vector<double>& ty, int64_t W, int64_t H, const std::vector<std::vector<int64_t>>& windows) {
     const int64_t C = (int64_t)cx.size();
     if (C < 1 || C > 64) throw std::runtime_error("camera batch size " + std::to_string(C) + " outside 1..64");
     if ((int64_t)cy.size() != C || (int64_t)tx.size() != C || (int64_t)ty.size() != C)
@@ -251,9 +251,18 @@ struct Cameras {
     proj = dev_f32(projs, dev, "projmatrices").reshape({C, 16}).contiguous();
     cpos = dev_f32(campos, dev, "campos").reshape({C, 3}).contiguous();
     bg = dev_f32(bg_, dev, "bg").reshape({-1});
-    cams.resize(C);
+    if (!windows.empty() && (int64_t)windows.size() != C)
+      throw std::runtime_error("tile windows: one (x0, y0, x1, y1) per camera");
+    cams.assign(C, gs_camera{});
     for (int64_t c = 0; c < C; ++c) {
       gs_camera& k = cams[c];
+      if (!windows.empty()) {
+        if (windows[c].size() != 4) throw std::runtime_error("a tile window is (x0, y0, x1, y1)");
+        k.tile_x0 = (int32_t)windows[c][0];
+        k.tile_y0 = (int32_t)windows[c][1];
+        k.tile_x1 = (int32_t)windows[c][2];
+        k.tile_y1 = (int32_t)windows[c][3];
+      }
       k.viewmatrix = view.data_ptr<float>() + 16 * c;
       k.projmatrix = proj.data_ptr<float>() + 16 * c;
       k.campos = cpos.data_ptr<float>() + 3 * c;
@@ -274,10 +283,10 @@ forward_batch(const Tensor& bg, const Tensor& means3D, const OptT& colors, const
               const Tensor& projs, const std::vector<double>& cx, const std::vector<double>& cy,
               const std::vector<double>& tx, const std::vector<double>& ty, int64_t H, int64_t W, const OptT& sh,
               int64_t degree, const Tensor& campos, bool prefiltered, bool debug, int64_t compat, bool activate,
-              int64_t stream) {
+              const std::vector<std::vector<int64_t>>& windows, int64_t stream) {
   Inputs in(means3D, colors, sem, opacity, scales, rotations, scale_modifier, cov3D, sh, degree);
   if (activate) in.g.flags |= GS_FLAG_ACTIVATE;
-  Cameras k(in.dev, bg, views, projs, campos, cx, cy, tx, ty, W, H);
+  Cameras k(in.dev, bg, views, projs, campos, cx, cy, tx, ty, W, H, windows);
   const int32_t C = (int32_t)k.cams.size();
   const auto f32 = at::TensorOptions().dtype(at::kFloat).device(in.dev);
   const auto u8 = at::TensorOptions().dtype(at::kByte).device(in.dev);
@@ -322,7 +331,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tenso
     const OptT& dL_alpha, const OptT& sh, int64_t degree, const Tensor& campos, const Tensor& geom,
     const std::vector<int64_t>& num_instances, const OptT& binning, const Tensor& img, const Tensor& alphas,
     bool debug, int64_t compat, const OptT& grad_mask, c10::optional<std::vector<Tensor>> densify,
-    const OptT& opacity, bool activate, int64_t stream) {
+    const OptT& opacity, bool activate, const std::vector<std::vector<int64_t>>& windows, int64_t stream) {
   if (activate && !present(opacity)) throw std::runtime_error("activate=True needs the raw opacities");
   Inputs in(means3D, colors, sem, activate ? opacity : c10::nullopt, scales, rotations, scale_modifier, cov3D, sh,
             degree);
@@ -330,7 +339,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tenso
   const int64_t C = (int64_t)cx.size();
   const Tensor& img_ref = present(dL_color) ? *dL_color : alphas;
   const int64_t H = img_ref.size(-2), W = img_ref.size(-1);
-  Cameras k(in.dev, bg, views, projs, campos, cx, cy, tx, ty, W, H);
+  Cameras k(in.dev, bg, views, projs, campos, cx, cy, tx, ty, W, H, windows);
   const auto f32 = at::TensorOptions().dtype(at::kFloat).device(in.dev);
   const int64_t P = in.P;
   Tensor gm;

@@ -11,7 +11,7 @@ all_reduce (train.py:288-290, external.py:136-140).
 """
 from __future__ import annotations
 
-from typing import Dict, Iterable, List, Mapping, Sequence
+from typing import Dict, Iterable, List, Mapping, Optional, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
@@ -20,6 +20,26 @@ import torch.distributed as dist
 def shard_cameras(n_cams: int, rank: int, world: int) -> List[int]:
     """Camera c goes to rank c mod world."""
     return [c for c in range(n_cams) if c % world == rank]
+
+
+def shard_camera_windows(n_cams: int, rank: int, world: int, grid_x: int, grid_y: int
+                         ) -> List[Tuple[int, Optional[Tuple[int, int, int, int]]]]:
+    """Balanced split of an n_cams rig over `world` ranks with image sharding
+    (gs_camera tile_*): the first world * (n_cams // world) cameras whole,
+    camera c on rank c mod world, and every one of the n_cams % world left
+    over cameras cut into `world` bands of tile rows, band k on rank k -- so
+    every rank renders n_cams / world cameras' worth of pixels (27 cameras
+    over 8 ranks: 3 whole cameras and 3 eighths, instead of 3 or 4 whole
+    ones).  Returns [(camera, window or None)], window = (x0, y0, x1, y1) in
+    tiles; bands of a grid with fewer tile rows than ranks may be empty and
+    are left out.  The windows of a camera partition its tile grid, so the
+    ranks' gradients sum to the rig's."""
+    q, r = divmod(n_cams, world)
+    out = [(c, None) for c in range(q * world) if c % world == rank]
+    y0, y1 = rank * grid_y // world, (rank + 1) * grid_y // world
+    if r and y1 > y0:
+        out += [(c, (0, y0, grid_x, y1)) for c in range(q * world, n_cams)]
+    return out
 
 
 class StaleBucketError(RuntimeError):

@@ -20,7 +20,7 @@ default, "reference"); see DESIGN.md "Quirks".
 """
 from __future__ import annotations
 
-from typing import NamedTuple, Optional
+from typing import NamedTuple, Optional, Tuple
 
 import torch
 import torch.nn as nn
@@ -208,6 +208,9 @@ class GaussianRasterizationSettings(NamedTuple):
     confidence: Optional[torch.Tensor] = None
     compat: Optional[str] = None
     grad_sink: Optional["GradientSink"] = None  # multi-camera gradient sum (no reference analogue)
+    # image sharding (no reference analogue): render only the 16x16 tiles
+    # [x0, x1) x [y0, y1) of the camera (gs_camera tile_*); camera batches only
+    tile_window: Optional[Tuple[int, int, int, int]] = None
 
 
 class GradientSink:
@@ -348,6 +351,9 @@ class GaussianRasterizer(nn.Module):
     def forward(self, means3D, means2D, opacities=None, shs=None, semantic_feature=None,
                 colors_precomp=None, scales=None, rotations=None, cov3D_precomp=None, label=_UNSET):
         rs = self.raster_settings
+        if getattr(rs, "tile_window", None) is not None:
+            raise NotImplementedError("tile_window (image sharding) is a camera-batch feature: use "
+                                      "GaussianRasterizerBatch")
         if (shs is None and colors_precomp is None) or (shs is not None and colors_precomp is not None):
             raise Exception('Please provide excatly one of either SHs or precomputed colors!')
         if ((scales is None or rotations is None) and cov3D_precomp is None) or \
@@ -416,6 +422,8 @@ class _BatchCameras:
         self.cpos = torch.stack([rs.campos.reshape(3) for rs in settings_list]).float().contiguous()
         self.tx = [rs.tanfovx for rs in settings_list]
         self.ty = [rs.tanfovy for rs in settings_list]
+        wins = [getattr(rs, "tile_window", None) for rs in settings_list]
+        self.windows = wins if any(w is not None for w in wins) else None
 
 
 class _RasterizeGaussiansBatch(torch.autograd.Function):
@@ -441,10 +449,10 @@ class _RasterizeGaussiansBatch(torch.autograd.Function):
             rs0.bg, means3D, colors_precomp, semantic_feature, opacities, scales, rotations, rs0.scale_modifier,
             cov3Ds_precomp, views, projs, [p[0] for p in pp], [p[1] for p in pp], tx, ty, rs0.image_height,
             rs0.image_width, sh, rs0.sh_degree, cpos, rs0.prefiltered, rs0.debug, compat=compat,
-            activate=raw_params)
+            activate=raw_params, windows=cams.windows)
         num_rendered, color, feature_map, depth, alpha, radii, geom, binning, img, num_instances = out
         ctx.rs0 = rs0
-        ctx.cams = (views, projs, cpos, pp, tx, ty)
+        ctx.cams = (views, projs, cpos, pp, tx, ty, cams.windows)
         ctx.num_rendered = num_rendered
         ctx.num_instances = num_instances
         ctx.compat = compat
@@ -463,7 +471,7 @@ class _RasterizeGaussiansBatch(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad_color, grad_radii, grad_out_feature, grad_depth, grad_alpha):
         rs0 = ctx.rs0
-        views, projs, cpos, pp, tx, ty = ctx.cams
+        views, projs, cpos, pp, tx, ty, windows = ctx.cams
         (colors_precomp, semantic_feature, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geom,
          binning, img, alpha, label, raw_opacities) = ctx.saved_tensors
         cx, cy = [p[0] for p in pp], [p[1] for p in pp]
@@ -476,7 +484,7 @@ class _RasterizeGaussiansBatch(torch.autograd.Function):
             cov3Ds_precomp, views, projs, *cam4, grad_color, grad_out_feature, grad_depth, grad_alpha, sh,
             rs0.sh_degree, cpos, geom, ctx.num_instances, binning, img, alpha, rs0.debug, compat=ctx.compat,
             grad_mask=label if fuse else None, densify=ctx.densify_out, opacity=raw_opacities,
-            activate=ctx.raw_params)
+            activate=ctx.raw_params, windows=windows)
         (grad_means2D, grad_colors_precomp, grad_semantic_feature, grad_opacities, grad_means3D,
          grad_cov3Ds_precomp, grad_sh, grad_scales, grad_rotations) = grads
         if ctx.sem_shape is not None:
@@ -538,6 +546,9 @@ class GaussianRasterizerBatch(nn.Module):
         super().__init__()
         self.settings_list = list(settings_list)
         self._cams = _BatchCameras(self.settings_list)
+        if track_densify and self._cams.windows is not None:
+            raise ValueError("densification statistics need whole-image cameras: a tile window counts a "
+                             "Gaussian seen by its camera once per window (gs_camera tile_*)")
         self.track_densify = track_densify
         self.raw_params = bool(raw_params)
         self.densify_stats = None

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 8
+#define GS_ABI_VERSION 9
 
 /* compat modes: numerics of the as-shipped reference vs corrected ones */
 #define GS_COMPAT_REFERENCE 0
@@ -104,7 +104,19 @@ typedef struct gs_gaussians {
 } gs_gaussians;
 
 /* Camera / raster settings (GaussianRasterizationSettings,
- * DGR/diff_gaussian_rasterization/__init__.py:176-192). */
+ * DGR/diff_gaussian_rasterization/__init__.py:176-192).
+ *
+ * Tile window (ABI 9; no reference analogue): render only the 16x16 tiles
+ * [tile_x0, tile_x1) x [tile_y0, tile_y1) of the camera's tile grid -- image
+ * sharding of one camera over several calls or ranks.  All
+ * four 0 = the whole image.  Projection, culling, radii and num_rendered are
+ * the whole camera's; only the window's tiles are binned, blended and
+ * back-propagated, so a window's pixels are bit-identical to the whole
+ * render's and the gradients of windows that partition the grid sum to the
+ * whole camera's.  Pixels outside the window are written as zeros (colour,
+ * features, depth, alpha, n_contrib) and their upstream gradients are
+ * ignored.  The densification statistics (gs_gaussians.densify_*) count a
+ * projected Gaussian in every window call: keep them to whole-image calls. */
 typedef struct gs_camera {
   const float *viewmatrix; /* 16 floats, column-major (device) */
   const float *projmatrix; /* 16 floats, column-major (device) */
@@ -112,6 +124,7 @@ typedef struct gs_camera {
   const float *background; /* 3 floats (device) */
   float c_x, c_y, tan_fovx, tan_fovy;
   int32_t image_width, image_height;
+  int32_t tile_x0, tile_y0, tile_x1, tile_y1; /* tile window; all 0 = whole image */
 } gs_camera;
 
 int gs_version(void);

@@ -288,3 +288,30 @@ def test_bucket_unbinds_parameters_no_rank_reached():
             assert (ga == 3.0).all()      # 1 + 2 from the two ranks
             assert (gb == 2.0).all()      # rank 0 only, still summed and bound
             assert gc is None             # no rank reached it
+
+
+@pytest.mark.parametrize("n_cams,world,gx,gy", [(27, 8, 50, 50), (27, 2, 50, 50), (16, 8, 120, 68),
+                                                 (3, 8, 120, 68), (5, 8, 4, 3)])
+def test_shard_camera_windows_partition_every_camera(n_cams, world, gx, gy):
+    """Image sharding of the rig: every camera's tile grid is covered exactly
+    once over the ranks, whole cameras go c mod N, and the ranks' pixel
+    shares differ by at most one band of tile rows per left-over camera."""
+    from dynamic3dgaussians_amd.distributed import shard_camera_windows
+    cover = {c: [[0] * gx for _ in range(gy)] for c in range(n_cams)}
+    load = []
+    for r in range(world):
+        sh = shard_camera_windows(n_cams, r, world, gx, gy)
+        px = 0
+        for c, w in sh:
+            x0, y0, x1, y1 = w if w is not None else (0, 0, gx, gy)
+            assert 0 <= x0 < x1 <= gx and 0 <= y0 < y1 <= gy
+            for y in range(y0, y1):
+                for x in range(x0, x1):
+                    cover[c][y][x] += 1
+            px += (x1 - x0) * (y1 - y0)
+            if w is None:
+                assert c % world == r
+        load.append(px)
+    assert all(v == 1 for c in cover for row in cover[c] for v in row)
+    left = n_cams % world
+    assert max(load) - min(load) <= left * gx * (gy // world + 1)

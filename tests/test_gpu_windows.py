@@ -1,0 +1,101 @@
+"""Image sharding of one camera (gs_camera tile_* windows):
+a camera rendered through a tile window gives, inside the window, exactly the
+whole render's pixels (bit-identical colour, depth, features, alpha), zeros
+outside, the whole camera's radii; the gradients of windows that partition
+the camera's tile grid sum to the whole camera's (fp32 atomic order: 1e-5
+relative L2).  This is what the balanced configs[3] split
+(distributed.shard_camera_windows) relies on."""
+from __future__ import annotations
+
+import pytest
+import torch
+
+from dynamic3dgaussians_amd.camera import camera_rig
+from dynamic3dgaussians_amd.rasterizer import GaussianRasterizationSettings, GaussianRasterizerBatch
+from dynamic3dgaussians_amd.scene import make_gaussians
+from dynamic3dgaussians_amd import _lib
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+def _settings(cams, W, H, windows, compat="reference"):
+    return [GaussianRasterizationSettings(
+        image_height=H, image_width=W, tanfovx=c.tanfovx, tanfovy=c.tanfovy, c_x=c.c_x, c_y=c.c_y,
+        bg=torch.tensor([0.2, 0.1, 0.3], device=DEV), viewmatrix=torch.from_numpy(c.viewmatrix.copy()).to(DEV),
+        projmatrix=torch.from_numpy(c.projmatrix.copy()).to(DEV), sh_degree=0,
+        campos=torch.from_numpy(c.campos.copy()).to(DEV), compat=compat, tile_window=w)
+        for c, w in zip(cams, windows)]
+
+
+def _scene(P, F, seed=0):
+    g = make_gaussians(P, F=F, seed=seed, device=DEV)
+    return {"means3D": g["means3D"], "colors_precomp": g["colors"], "opacities": g["opacities"],
+            "scales": g["scales"], "rotations": g["rotations"], "semantic_feature": g["semantic_feature"]}
+
+
+def _rel(a, b):
+    a, b = a.double(), b.double()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+def _mask(W, H, w):
+    m = torch.zeros(H, W, dtype=torch.bool, device=DEV)
+    x0, y0, x1, y1 = w
+    m[y0 * 16:min(y1 * 16, H), x0 * 16:min(x1 * 16, W)] = True
+    return m
+
+
+@pytest.mark.parametrize("compat", ["reference", "fixed"])
+def test_window_pixels_equal_the_whole_render(compat, P=20000, W=200, H=152, F=32):
+    src = _scene(P, F)
+    cam = camera_rig(5, W, H)[2]
+    gx, gy = (W + 15) // 16, (H + 15) // 16
+    wins = [None, (0, 2, gx, 5), (1, 1, 6, 4), (gx - 1, gy - 1, gx, gy)]
+    sets = _settings([cam] * len(wins), W, H, wins, compat)
+    lab = torch.ones(P, device=DEV)
+    im, radii, feat, depth, alpha = GaussianRasterizerBatch(sets)(means2D=torch.zeros(P, 3, device=DEV),
+                                                                  label=lab, **src)
+    for k in range(1, len(wins)):
+        m = _mask(W, H, wins[k])
+        assert torch.equal(radii[k], radii[0])
+        for t in (im, feat, depth, alpha):
+            assert torch.equal(t[k][:, m], t[0][:, m]), k
+            assert not torch.any(t[k][:, ~m]), k
+
+
+def test_window_gradients_sum_to_the_whole_camera(P=20000, W=200, H=152, F=32):
+    src = _scene(P, F, seed=3)
+    cams = camera_rig(5, W, H)
+    gx, gy = (W + 15) // 16, (H + 15) // 16
+    # camera 1 whole, camera 3 as a partition of 4 windows (row bands and a split band)
+    part = [(0, 0, gx, 3), (0, 3, 5, gy - 2), (5, 3, gx, gy - 2), (0, gy - 2, gx, gy)]
+    gen = torch.Generator(device=DEV).manual_seed(1)
+    up = [torch.randn(1, 3, H, W, device=DEV, generator=gen), torch.randn(1, 1, H, W, device=DEV, generator=gen),
+          torch.randn(1, F, H, W, device=DEV, generator=gen)]
+    lab = torch.ones(P, device=DEV)
+
+    def grads(entries):
+        sets = _settings([cams[c] for c, _ in entries], W, H, [w for _, w in entries])
+        leaves = {k: v.clone().requires_grad_(True) for k, v in src.items()}
+        n = len(entries)
+        im, _, feat, depth, _ = GaussianRasterizerBatch(sets)(means2D=torch.zeros(P, 3, device=DEV), label=lab,
+                                                             **leaves)
+        torch.autograd.backward([im, depth, feat], [u.expand(n, -1, -1, -1) for u in up])
+        return {k: v.grad for k, v in leaves.items()}
+
+    whole = grads([(1, None), (3, None)])
+    split = grads([(1, None)] + [(3, w) for w in part])
+    for k in whole:
+        assert _rel(split[k], whole[k]) <= 1e-5, (k, _rel(split[k], whole[k]))
+
+
+def test_window_outside_the_grid_is_refused(W=128, H=96):
+    src = _scene(2000, 8)
+    src.pop("semantic_feature")
+    cam = camera_rig(1, W, H)[0]
+    sets = _settings([cam], W, H, [(0, 0, 9, 3)])
+    with pytest.raises(_lib.GsplatError, match="tile window"):
+        GaussianRasterizerBatch(sets)(means2D=torch.zeros(2000, 3, device=DEV), **src)
+    with pytest.raises(ValueError, match="whole-image"):
+        GaussianRasterizerBatch(_settings([cam], W, H, [(0, 0, 2, 2)]), track_densify=True)
