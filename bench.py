@@ -97,6 +97,8 @@ def parse():
     ap.add_argument("--compat", default="reference", choices=["reference", "fixed"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--dump-params", default="",
+                    help="rank 0 writes the parameters after the timed steps to this .npz (rehearsal checks)")
     ap.add_argument("--step-times", action="store_true",
                     help="also report host timestamps of the timed steps (diagnostic)")
     ap.add_argument("--sub-batches", type=int, default=int(os.environ.get("GS_BENCH_SUB_BATCHES", "1")),
@@ -489,16 +491,40 @@ def main():
     ] + ([{"params": [params["semantic_feature"]], "lr": 1e-3, "name": "semantic_feature"}]
          if args.features else [])
     optim_kind = os.environ.get("GS_BENCH_OPTIM", "fused_hip")
-    if optim_kind == "fused_hip":
-        opt = FusedAdam(groups, lr=0.0, eps=1e-15)
+
+    def make_opt(gs):
+        if optim_kind == "fused_hip":
+            return FusedAdam(gs, lr=0.0, eps=1e-15)
+        return torch.optim.Adam(gs, lr=0.0, eps=1e-15, fused=optim_kind == "torch_fused")
+
+    # N > 1, camera batches, F > 0: the feature gradients (32 of the 46 floats
+    # per Gaussian) are all-reduced behind the next step -- their all-reduce and
+    # Adam update run on a side stream while the next step projects and bins,
+    # and that step's blend waits for the update (gs_gaussians.feature_ready);
+    # only the geometry gradients are exchanged on the step's critical path.
+    # Double-buffered feature gradients: step k writes buffer k % 2 while the
+    # exchange of step k-1 still reads the other.  GS_BENCH_OVERLAP=0: one
+    # bucket, exchanged before Adam.
+    overlap = (dist_on and world > 1 and args.features > 0 and args.mode == "batch"
+               and os.environ.get("GS_BENCH_OVERLAP", "1") != "0")
+    if overlap:
+        opt = make_opt([g_ for g_ in groups if g_["name"] != "semantic_feature"])
+        opt_feat = make_opt([g_ for g_ in groups if g_["name"] == "semantic_feature"])
     else:
-        opt = torch.optim.Adam(groups, lr=0.0, eps=1e-15, fused=optim_kind == "torch_fused")
+        opt = make_opt(groups)
     # N > 1: every parameter's .grad is a view into the all-reduce bucket, so
     # the backward accumulates straight into it (no pack/unpack copies) and
     # one fill clears it.  N = 1 has no exchange: gradients stay unbound, so
     # autograd hands the backward's tensors to the leaves without the six
     # accumulate kernels and the fill (-0.06 ms per step).
-    bucket = GradBucket(params, bind_grads=dist_on)
+    if overlap:
+        bucket = GradBucket({k: v for k, v in params.items() if k != "semantic_feature"}, bind_grads=True)
+        feat_buckets = [GradBucket({"semantic_feature": params["semantic_feature"]}, bind_grads=True)
+                        for _ in range(2)]
+        side = torch.cuda.Stream(device=dev)
+        pipe = {"k": 0, "done": [None, None]}
+    else:
+        bucket = GradBucket(params, bind_grads=dist_on)
     g = torch.Generator(device=dev).manual_seed(1 + rank)
     H_, W_ = args.height, args.width
     up_color = torch.randn(3, H_, W_, device=dev, generator=g)
@@ -552,16 +578,54 @@ def main():
 
     batch_parts = batch_inputs(settings, args.sub_batches)
 
-    def run_part(ras, ups, rv):
+    def run_part(ras, ups, rv, ready=None):
         up_c, up_d, up_f = ups
         if up_f is not None:  # G3 call (label + semantic_feature)
-            im, radius, feat, depth, _ = ras(**rv)
+            im, radius, feat, depth, _ = ras(**rv, feature_ready=ready)
             torch.autograd.backward([im, depth, feat], [up_c, up_d, up_f])
         else:                 # G2 call (label only)
             im, radius, depth, _ = ras(**rv)
             torch.autograd.backward([im, depth], [up_c, up_d])
 
+    def drain():
+        """Overlap mode: the main stream waits for every pending feature update."""
+        if overlap:
+            for ev in pipe["done"]:
+                if ev is not None:
+                    torch.cuda.current_stream(dev).wait_event(ev)
+
+    def step_overlap(parts):
+        main = torch.cuda.current_stream(dev)
+        k = pipe["k"]
+        fb = feat_buckets[k % 2]
+        if pipe["done"][k % 2] is not None:  # the exchange of step k-2 read this buffer
+            main.wait_event(pipe["done"][k % 2])
+        fb.bind()
+        fb.zero_grad()
+        bucket.zero_grad()
+        rv = raw_rendervar(params, label, means2D_placeholder) if raw else params2rendervar(params, label)
+        for ras, ups, _ in parts:
+            run_part(ras, ups, rv, ready=pipe["done"][(k - 1) % 2])
+        bucket.all_reduce()          # geometry: on the critical path, issued first
+        work = fb.all_reduce_async()  # features: behind the next step
+        opt.step()
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            if work is not None:
+                work.wait()
+            opt_feat.step()
+            ev = torch.cuda.Event()
+            ev.record(side)
+        pipe["done"][k % 2] = ev
+        pipe["k"] = k + 1
+
     def step_batch(parts=batch_parts):
+        if overlap and len(parts) == 1:
+            return step_overlap(parts)
+        drain()
+        if overlap:
+            feat_buckets[0].bind()
+            feat_buckets[0].zero_grad()
         bucket.zero_grad()
         rv = raw_rendervar(params, label, means2D_placeholder) if raw else params2rendervar(params, label)
         if len(parts) == 1:
@@ -580,10 +644,17 @@ def main():
                 main.wait_stream(st)
         bucket.all_reduce()
         opt.step()
+        if overlap:
+            feat_buckets[0].all_reduce()
+            opt_feat.step()
 
     def step(mode=args.mode):
         if mode == "batch":
             return step_batch()
+        drain()
+        if overlap:
+            feat_buckets[0].bind()
+            feat_buckets[0].zero_grad()
         bucket.zero_grad()
         if sink is not None:
             sink.reset()
@@ -622,6 +693,9 @@ def main():
         torch.autograd.backward([rv[k] for k in keys], [summed[k] for k in keys])
         bucket.all_reduce()
         opt.step()
+        if overlap:
+            feat_buckets[0].all_reduce()
+            opt_feat.step()
 
     for _ in range(args.warmup):
         step()
@@ -652,6 +726,10 @@ def main():
     elapsed = time.perf_counter() - t0
     stages = _lib.timing_read()
     _lib.timing_enable(False)
+    if args.dump_params and rank == 0:
+        drain()
+        torch.cuda.synchronize()
+        np.savez(args.dump_params, **{k: v.detach().cpu().numpy() for k, v in params.items()})
     if dist_on:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -803,7 +881,10 @@ def main():
                                 "in-kernel (GradientSink)" if use_sink else "autograd"),
                    "gaussians": args.gaussians, "cams_per_rank": len(my_cams), "width": W_,
                    "height": H_, "feature_channels": args.features, "compat": args.compat,
-                   "parallelism": f"camera-sharded dp{world}"},
+                   "parallelism": f"camera-sharded dp{world}",
+                   "grad_exchange": ("geometry all-reduce before Adam; feature all-reduce + Adam overlapped with the "
+                                     "next step's projection and binning" if overlap else
+                                     "one all-reduce before Adam" if world > 1 else "none (one rank)")},
         "roofline": roofline,
         "stages_ms_per_step": {k: round(v, 4) for k, v in stage_ms.items()},
         "split_step": split,

@@ -441,6 +441,11 @@ def _camera_batch(dev, background, viewmatrices, projmatrices, campos, c_x, c_y,
     return cams, C, [view, proj, cpos, bg]
 
 
+def _event_handle(ev) -> int:
+    """The hipEvent_t of a recorded torch.cuda.Event (0 = none)."""
+    return 0 if ev is None else int(ev.cuda_event)
+
+
 def _windows_arg(windows, C):
     """Tile windows as the native binding takes them: C x [x0, y0, x1, y1]
     (all 0 = the whole image), or an empty list for none."""
@@ -452,7 +457,7 @@ def _windows_arg(windows, C):
 def rasterize_gaussians_batch(background, means3D, colors, semantic_feature, opacity, scales, rotations,
                               scale_modifier, cov3D_precomp, viewmatrices, projmatrices, c_x, c_y, tan_fovx,
                               tan_fovy, image_height, image_width, sh, degree, campos, prefiltered, debug,
-                              *, compat=None, activate=False, windows=None):
+                              *, compat=None, activate=False, windows=None, feature_ready=None):
     """The forward of C cameras at once (gs_forward_plan_batch +
     gs_forward_render_batch): the arguments of rasterize_gaussians with
     per-camera matrices stacked ([C,4,4] or [C,16], campos [C,3]) and the
@@ -462,9 +467,19 @@ def rasterize_gaussians_batch(background, means3D, colors, semantic_feature, opa
     camera c's outputs equal rasterize_gaussians' for that camera.
     `activate`: opacity / scales / rotations are the raw parameters
     (logit, log, unnormalised; GS_FLAG_ACTIVATE).  `windows`: per camera a
-    tile window (x0, y0, x1, y1) or None (gs_camera tile_*)."""
+    tile window (x0, y0, x1, y1) or None (gs_camera tile_*).  `feature_ready`:
+    a torch.cuda.Event (recorded) the blend waits for before reading the
+    features (gs_gaussians.feature_ready), or None."""
     L_ = _lib.load()
     cm = _compat_code(compat)
+    if feature_ready is not None and _present(semantic_feature):
+        sf = semantic_feature
+        Fu = sf.numel() // max(means3D.size(0), 1)
+        if not (sf.is_cuda and sf.dtype == torch.float32 and sf.is_contiguous() and _feature_width(Fu) == Fu):
+            # the binding copies / pads the features on the calling stream
+            # before any kernel runs: that copy has to wait too
+            torch.cuda.current_stream(means3D.device).wait_event(feature_ready)
+            feature_ready = None
     nat = _native_mod()
     if nat is not None and means3D.is_cuda and means3D.dim() == 2 and means3D.size(0) > 0:
         try:
@@ -474,6 +489,7 @@ def rasterize_gaussians_batch(background, means3D, colors, semantic_feature, opa
                                      [float(x) for x in tan_fovx], [float(x) for x in tan_fovy], int(image_height),
                                      int(image_width), _opt(sh), int(degree), campos, bool(prefiltered),
                                      bool(debug), cm, bool(activate), _windows_arg(windows, len(c_x)),
+                                     _event_handle(feature_ready),
                                      torch.cuda.current_stream(means3D.device).cuda_stream)
         except RuntimeError as ex:
             raise _lib.GsplatError(str(ex)) from None
@@ -491,6 +507,7 @@ def rasterize_gaussians_batch(background, means3D, colors, semantic_feature, opa
                 torch.zeros(C, 0, dtype=torch.int32, device=dev), torch.empty(0, **u8), torch.empty(0, **u8),
                 torch.empty(0, **u8), [0] * C)
     g = inp.struct(_lib.GS_FLAG_ACTIVATE if activate else 0)
+    g.feature_ready = _event_handle(feature_ready) or None
     out_color = torch.empty(C, 3, H, W, **f32)
     out_feature = torch.empty(C, inp.F, H, W, **f32)
     out_depth = torch.empty(C, 1, H, W, **f32)

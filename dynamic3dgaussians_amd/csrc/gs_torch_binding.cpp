@@ -95,6 +95,7 @@ struct Inputs {
     g.flags = 0;
     g.grad_mask = nullptr;
     g.densify_accum = g.densify_denom = g.max_radius = nullptr;
+    g.feature_ready = nullptr;
   }
 };
 
@@ -283,9 +284,10 @@ forward_batch(const Tensor& bg, const Tensor& means3D, const OptT& colors, const
               const Tensor& projs, const std::vector<double>& cx, const std::vector<double>& cy,
               const std::vector<double>& tx, const std::vector<double>& ty, int64_t H, int64_t W, const OptT& sh,
               int64_t degree, const Tensor& campos, bool prefiltered, bool debug, int64_t compat, bool activate,
-              const std::vector<std::vector<int64_t>>& windows, int64_t stream) {
+              const std::vector<std::vector<int64_t>>& windows, int64_t feature_ready, int64_t stream) {
   Inputs in(means3D, colors, sem, opacity, scales, rotations, scale_modifier, cov3D, sh, degree);
   if (activate) in.g.flags |= GS_FLAG_ACTIVATE;
+  in.g.feature_ready = reinterpret_cast<gs_event_t>(feature_ready);
   Cameras k(in.dev, bg, views, projs, campos, cx, cy, tx, ty, W, H, windows);
   const int32_t C = (int32_t)k.cams.size();
   const auto f32 = at::TensorOptions().dtype(at::kFloat).device(in.dev);

@@ -171,6 +171,27 @@ class GradBucket:
                         "clear gradients with GradBucket.zero_grad()")
 
     # ---------------------------------------------------------------- grads
+    def bind(self) -> None:
+        """Bound mode: make every parameter's .grad this bucket's view (again):
+        several buckets can take turns over the same parameters, e.g. a
+        double-buffered gradient set whose all-reduce runs behind the next
+        step (all_reduce_async)."""
+        for p, v in zip(self.params, self._views):
+            p.grad = v
+        self._unbound.clear()
+
+    def all_reduce_async(self, group=None):
+        """One all_reduce(SUM) of a bound bucket without extras, left running:
+        returns the work handle (wait() on it -- on the stream that consumes
+        the gradients -- before using them), None without a process group.
+        The gradients are summed in place in the bound views."""
+        if not self.bound or self.extras or self.track:
+            raise ValueError("all_reduce_async: bound gradients only (no extras, no reach tracking)")
+        self.check_live()
+        if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+            return None
+        return dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group, async_op=True)
+
     def zero_grad(self) -> None:
         """Bound mode: zero every gradient with one fill of the buffer."""
         if self.bound:

@@ -432,7 +432,7 @@ class _RasterizeGaussiansBatch(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, means3D, means2D, sh, colors_precomp, semantic_feature, opacities, scales, rotations,
-                cov3Ds_precomp, cams, label, densify_out, raw_params=False):
+                cov3Ds_precomp, cams, label, densify_out, raw_params=False, feature_ready=None):
         if not isinstance(cams, _BatchCameras):
             cams = _BatchCameras(cams)
         rs0 = cams.rs0
@@ -449,7 +449,7 @@ class _RasterizeGaussiansBatch(torch.autograd.Function):
             rs0.bg, means3D, colors_precomp, semantic_feature, opacities, scales, rotations, rs0.scale_modifier,
             cov3Ds_precomp, views, projs, [p[0] for p in pp], [p[1] for p in pp], tx, ty, rs0.image_height,
             rs0.image_width, sh, rs0.sh_degree, cpos, rs0.prefiltered, rs0.debug, compat=compat,
-            activate=raw_params, windows=cams.windows)
+            activate=raw_params, windows=cams.windows, feature_ready=feature_ready)
         num_rendered, color, feature_map, depth, alpha, radii, geom, binning, img, num_instances = out
         ctx.rs0 = rs0
         ctx.cams = (views, projs, cpos, pp, tx, ty, cams.windows)
@@ -504,24 +504,27 @@ class _RasterizeGaussiansBatch(torch.autograd.Function):
             grad_rotations = grad_rotations * lab
             grad_cov3Ds_precomp = grad_cov3Ds_precomp * lab
         grads = (grad_means3D, grad_means2D, grad_sh, grad_colors_precomp, grad_semantic_feature,
-                 grad_opacities, grad_scales, grad_rotations, grad_cov3Ds_precomp, None, None, None, None)
+                 grad_opacities, grad_scales, grad_rotations, grad_cov3Ds_precomp, None, None, None, None, None)
         return tuple(g if need else None for g, need in zip(grads, ctx.needs_input_grad))
 
 
 def rasterize_gaussians_batch(means3D, means2D, sh, colors_precomp, semantic_feature, opacities, scales,
                               rotations, cov3Ds_precomp, settings_list, label=None, densify_out=None,
-                              raw_params=False):
+                              raw_params=False, feature_ready=None):
     """rasterize_gaussians over a list of camera settings; outputs [C, ...]
     (color, radii, feature_map, depth, alpha).  `densify_out`: optional
     (accum, denom, max_radius) fp32 [P] tensors the backward fills with the
     cameras' densification statistics (GradientSink.densify_stats).
     `raw_params`: opacities / scales / rotations are the raw parameters of
     helpers.py:98-107 (logit_opacities, log_scales, unnorm_rotations); the
-    kernels apply sigmoid / exp / normalize and return their gradients."""
+    kernels apply sigmoid / exp / normalize and return their gradients.
+    `feature_ready`: a recorded torch.cuda.Event the blend waits for before it
+    reads semantic_feature (an overlapped optimizer update of the features on
+    another stream; gs_gaussians.feature_ready)."""
     cams = settings_list if isinstance(settings_list, _BatchCameras) else _BatchCameras(list(settings_list))
     return _RasterizeGaussiansBatch.apply(means3D, means2D, sh, colors_precomp, semantic_feature, opacities,
                                           scales, rotations, cov3Ds_precomp, cams, label, densify_out,
-                                          bool(raw_params))
+                                          bool(raw_params), feature_ready)
 
 
 class GaussianRasterizerBatch(nn.Module):
@@ -554,7 +557,10 @@ class GaussianRasterizerBatch(nn.Module):
         self.densify_stats = None
 
     def forward(self, means3D, means2D, opacities=None, shs=None, semantic_feature=None, colors_precomp=None,
-                scales=None, rotations=None, cov3D_precomp=None, label=_UNSET):
+                scales=None, rotations=None, cov3D_precomp=None, label=_UNSET, feature_ready=None):
+        """The GaussianRasterizer call; `feature_ready` (keyword, optional): a
+        recorded torch.cuda.Event the blend waits for before reading
+        semantic_feature (gs_gaussians.feature_ready)."""
         if (shs is None and colors_precomp is None) or (shs is not None and colors_precomp is not None):
             raise Exception('Please provide excatly one of either SHs or precomputed colors!')
         if ((scales is None or rotations is None) and cov3D_precomp is None) or \
@@ -575,7 +581,7 @@ class GaussianRasterizerBatch(nn.Module):
             self.densify_stats = {"means2D_gradient_accum": dens[0], "denom": dens[1], "max_2D_radius": dens[2]}
         color, radii, feature_map, depth, alpha = rasterize_gaussians_batch(
             means3D, means2D, shs, colors_precomp, semantic_feature, opacities, scales, rotations,
-            cov3D_precomp, self._cams, lab, dens, self.raw_params)
+            cov3D_precomp, self._cams, lab, dens, self.raw_params, feature_ready)
         has_sem = semantic_feature is not None
         if has_label and has_sem:      # G3
             return color, radii, feature_map, depth, alpha

@@ -34,13 +34,14 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 9
+#define GS_ABI_VERSION 10
 
 /* compat modes: numerics of the as-shipped reference vs corrected ones */
 #define GS_COMPAT_REFERENCE 0
 #define GS_COMPAT_FIXED 1
 
 typedef void *gs_stream_t;
+typedef void *gs_event_t; /* a hipEvent_t */
 
 /* gs_gaussians.flags.  GS_FLAG_ACCUMULATE (gs_backward only; no reference
  * analogue): ADD this call's gradients into the dL_d* outputs instead of
@@ -101,6 +102,13 @@ typedef struct gs_gaussians {
   float *densify_accum;
   float *densify_denom;
   float *max_radius;
+  /* Optional (ABI 10; no reference analogue): an event the forward's blend
+   * launch -- the first reader of semantic_feature -- waits for on the launch
+   * stream (hipStreamWaitEvent), or NULL.  A caller that updates the features
+   * on another stream (an optimizer step behind an overlapped gradient
+   * all-reduce) orders that update before the blend without ordering the
+   * projection and binning behind it. */
+  gs_event_t feature_ready;
 } gs_gaussians;
 
 /* Camera / raster settings (GaussianRasterizationSettings,
