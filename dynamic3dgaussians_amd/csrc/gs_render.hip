@@ -46,7 +46,11 @@ constexpr int CHUNK = 64;
 // same records through one CU's L1: 0.202 vs 0.223 ms), the backward with a
 // wave per workgroup (its 12 KiB of LDS are released the moment its strip is
 // done: 0.330 vs 0.342 ms).
+#ifdef GS_FWD_WPB1
+constexpr int WPB_FWD = 1;
+#else
 constexpr int WPB_FWD = 4;
+#endif
 constexpr int WPB_BWD = 1;
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float float4_t __attribute__((ext_vector_type(4)));
@@ -156,6 +160,9 @@ __device__ inline unsigned long long stamp() {
   return t;
 }
 #define STAMP(v) const unsigned long long v = stamp()
+// the chip-wide real-time clock (100 MHz), comparable across CUs and XCDs:
+// each wave's absolute start and end, for the launch's waves-in-flight curve
+#define RT_STAMP(v) const unsigned long long v = __builtin_amdgcn_s_memrealtime()
 __device__ inline void stamp_store(long long wave_id, unsigned long long a, unsigned long long b,
                                    unsigned long long c, unsigned long long d, unsigned long long e = 0,
                                    unsigned long long f = 0, unsigned long long g = 0, unsigned long long h = 0) {
@@ -178,6 +185,7 @@ extern "C" int gs_stamps_set(void* buf, long long bwd_off) {
 }
 #else
 #define STAMP(v) ((void)0)
+#define RT_STAMP(v) ((void)0)
 #endif
 
 // 1/x as one v_rcp_f32 (1 ulp).
@@ -367,8 +375,12 @@ __global__ __launch_bounds__(64 * WPB_FWD) __attribute__((amdgpu_waves_per_eu(fw
     RenderArgs a0, CamBatch cb) {
   // camera c of the batch: workgroups are dealt camera-minor (see cam_slot)
   STAMP(ts0);
+  RT_STAMP(rt0);
   int cam, bslot;
-  cam_slot(blockIdx.x, cb.C, num_tiles_of(a0) * 4 / WPB_FWD, cam, bslot);
+  if constexpr (WPB_FWD == 1)
+    strip_of_block(blockIdx.x, cb.C, num_tiles_of(a0), cam, bslot);
+  else
+    cam_slot(blockIdx.x, cb.C, num_tiles_of(a0) * 4 / WPB_FWD, cam, bslot);
   const RenderArgs ca = cam_render_args(a0, cb, cam);
   const int W = ca.W, H = ca.H, grid_x = ca.grid_x;
   const uint4* __restrict__ order = ca.order;
@@ -755,7 +767,8 @@ blend_done:
   STAMP(ts3);
   __builtin_amdgcn_s_waitcnt(0);
   STAMP(ts4);
-  stamp_store((long long)blockIdx.x * WPB_FWD + lw, ts1 - ts0, ts2 - ts0, ts3 - ts0, ts4 - ts0);
+  RT_STAMP(rt1);
+  stamp_store((long long)blockIdx.x * WPB_FWD + lw, ts1 - ts0, ts2 - ts0, ts3 - ts0, ts4 - ts0, 0, 0, rt0, rt1);
 #endif
 }
 
@@ -794,6 +807,7 @@ __global__ __launch_bounds__(64 * WPB_BWD) __attribute__((amdgpu_waves_per_eu(bw
     RenderBwdArgs a0, CamBatch cb) {
   // camera c of the batch: workgroups are dealt camera-minor (see cam_slot)
   STAMP(ts0);
+  RT_STAMP(rt0);
   static_assert(WPB_BWD == 1, "strip_of_block maps one strip per workgroup");
   int cam, bslot;
   strip_of_block(blockIdx.x, cb.C, num_tiles_of(a0), cam, bslot);
@@ -1259,8 +1273,14 @@ __global__ __launch_bounds__(64 * WPB_BWD) __attribute__((amdgpu_waves_per_eu(bw
   STAMP(ts3);
   __builtin_amdgcn_s_waitcnt(0);
   STAMP(ts4);
+  RT_STAMP(rt1);
+#ifdef GS_STAMPS_FINE
   stamp_store(g_stamp_bwd_off + (long long)blockIdx.x * WPB_BWD + lw, ts1 - ts0, ts2 - ts0, ts3 - ts0, ts4 - ts0,
-              tA ? tA - ts0 : 0, tB ? tB - ts0 : 0, tC ? tC - ts0 : 0, tD ? tD - ts0 : 0);
+              tA - ts0, tB - ts0, tC - ts0, tD - ts0);
+#else
+  stamp_store(g_stamp_bwd_off + (long long)blockIdx.x * WPB_BWD + lw, ts1 - ts0, ts2 - ts0, ts3 - ts0, ts4 - ts0,
+              0, 0, rt0, rt1);
+#endif
 #endif
 }
 

@@ -84,7 +84,26 @@ def main():
                          "tail_issue": round((v[:, 2] - v[:, 1]).sum() / tot, 4),
                          "drain": round((v[:, 3] - v[:, 2]).sum() / tot, 4), "waves": int(len(v)),
                          "ticks_per_wave": round(float(tot / max(len(v), 1)))}
-            if v[:, 4:].any():  # GS_STAMPS_FINE: backward prologue stages after full waits
+            if (v[:, 6] > 0).all():  # absolute real-time clock (100 MHz): the launch's waves in flight
+                t0, t1 = v[:, 6], v[:, 7]
+                span = t1.max() - t0.min()
+                ev = np.concatenate([np.stack([t0, np.ones_like(t0)], 1), np.stack([t1, -np.ones_like(t1)], 1)])
+                ev = ev[np.lexsort((ev[:, 1], ev[:, 0]))]
+                live = np.cumsum(ev[:, 1])
+                dt = np.diff(ev[:, 0], append=ev[-1, 0])
+                peak = live.max()
+                low = live < 0.5 * peak
+                # the launch's tail: from the last time the chip was at >= half its peak to the end
+                last_full = ev[np.nonzero(~low)[0].max(), 0]
+                out[name]["timeline"] = {
+                    "span_us": round(span / 100.0, 1), "peak_waves": int(peak),
+                    "mean_waves_in_flight": round(float((live * dt).sum() / span), 1),
+                    "below_half_peak_us": round(float(dt[low].sum()) / 100.0, 1),
+                    "tail_us": round(float(t1.max() - last_full) / 100.0, 1),
+                    "ramp_us": round(float(ev[np.nonzero(~low)[0].min(), 0] - t0.min()) / 100.0, 1),
+                    "longest_wave_us": round(float((t1 - t0).max()) / 100.0, 1),
+                    "mean_wave_us": round(float((t1 - t0).mean()) / 100.0, 1)}
+            if (v[:, 4:6] > 0).any():  # GS_STAMPS_FINE: backward prologue stages after full waits
                 d = np.diff(np.concatenate([np.zeros((len(v), 1)), v[:, 4:8]], axis=1), axis=1)
                 out[name]["prologue"] = {k: round(float(d[:, i].sum() / tot), 4) for i, k in
                                          enumerate(["to_record", "pixel_loads", "operands", "first_chunk"])}
