@@ -37,7 +37,6 @@ if VARIANT:
 # copy of a previous product library for A/B timing) and is never rebuilt.
 VARIANT_FLAGS = {"": [], "stats": ["-DGS_STATS"], "stamps": ["-DGS_STAMPS"],
                  "stamps_fine": ["-DGS_STAMPS", "-DGS_STAMPS_FINE"],
-                 "exp_fwd_wpb1": ["-DGS_FWD_WPB1"], "exp_fwd_wpb1_stamps": ["-DGS_FWD_WPB1", "-DGS_STAMPS"],
                  "exp_nofeat": ["-DGS_EXP_NO_FEAT_ATOMIC"],
                  "exp_noatomic": ["-DGS_EXP_NO_FEAT_ATOMIC", "-DGS_EXP_NO_ACC_ATOMIC"]}
 ARCH = os.environ.get("GSPLAT_OFFLOAD_ARCH", "gfx950")

@@ -40,17 +40,19 @@ namespace gs {
 
 constexpr float ALPHA_MIN = 1.0f / 255.0f;
 constexpr int CHUNK = 64;
-// Waves per workgroup in the blend kernels.  Each wave owns one strip
-// and never synchronises with the others.  Measured (bench camera, F = 32):
-// the forward is faster with a tile per workgroup (its 4 waves gather the
-// same records through one CU's L1: 0.202 vs 0.223 ms), the backward with a
-// wave per workgroup (its 12 KiB of LDS are released the moment its strip is
+// Waves per workgroup in the blend kernels: one.  Each wave owns one strip
+// and never synchronises with the others.  Round 1 measured the forward
+// faster with a tile (4 strips) per workgroup on one camera (its 4 waves
+// gathered the same records through one CU's L1: 0.202 vs 0.223 ms); on the
+// camera batches a workgroup's wave slots then idle until its longest strip
+// is done (tools/batch_steps.py --stamps: 3298 of 4096 slots busy on average
+// at 4 cameras, 3642 with a strip per workgroup), and with the XCD rotation
+// of strip_of_block a strip per workgroup wins (4-camera step 1.58-1.60 vs
+// 1.62-1.63 ms with tile workgroups, 1.65-1.66 before the rotation;
+// 27 cameras within noise; profiles/r04j/).  The backward was already
+// faster that way (its 12 KiB of LDS are released the moment its strip is
 // done: 0.330 vs 0.342 ms).
-#ifdef GS_FWD_WPB1
 constexpr int WPB_FWD = 1;
-#else
-constexpr int WPB_FWD = 4;
-#endif
 constexpr int WPB_BWD = 1;
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float float4_t __attribute__((ext_vector_type(4)));
@@ -82,22 +84,26 @@ __device__ inline void cam_slot(int bid, int C, int per_cam, int& cam, int& slot
   cam = g0 + r % gn;
   slot = r / gn;
 }
-// Workgroup -> (camera, strip item) of the wave-per-workgroup backward.  A
-// (camera, tile) unit is 4 strip workgroups, and those 4 must sit on one XCD
-// (one L2 fill of the tile's records and feature rows).  Units are dealt
-// 8 at a time, one per XCD: the k-th group of 8 units is blocks 32k .. 32k+31,
-// unit 8k + x on XCD x (blocks 32k + 8s + x, s = strip).  Units are ordered
-// by cam_slot (groups of 8 cameras, camera-minor), so for C >= 8 this is the
-// same block order as cam_slot over strips, and for C < 8 (an 8-rank split:
-// 3-4 cameras per rank) XCD x renders camera x % C instead of every tile's
-// strips straddling 2 XCDs.  The last U % 8 units keep plain order.
+// Workgroup -> (camera, strip item) of the wave-per-workgroup blend
+// kernels.  A (camera, tile) unit is 4 strip workgroups, and those 4 sit on
+// one XCD (one L2 fill of the tile's records and feature rows): units are
+// dealt 8 at a time, one per XCD -- the k-th group of 8 units is blocks
+// 32k .. 32k+31, strip s of its unit j on XCD (j - k) mod 8 (block
+// 32k + 8s + x holds unit 8k + (x + k) mod 8).  Units are ordered by
+// cam_slot (groups of 8 cameras, camera-minor, longest tiles first).  The
+// rotation by k matters at C < 8 (an 8-rank split: 3-4 cameras per rank):
+// without it XCD x rendered only camera x mod C, and the XCDs holding the
+// heavier cameras finished last (per-XCD work at 4 cameras 698-809 us of
+// the 850 us backward, tools/batch_steps.py --stamps; 4-camera backward
+// 0.785-0.798 vs 0.825-0.832 ms rotated, profiles/r04j/).  The last U % 8
+// units keep plain order.
 __device__ inline void strip_of_block(int bid, int C, int num_tiles, int& cam, int& item) {
   const int U = C * num_tiles, full = U & ~7;
   int u, s;
   if (bid < 4 * full) {
-    const int x = bid & 7, q = bid >> 3;
+    const int x = bid & 7, q = bid >> 3, k = q >> 2;
     s = q & 3;
-    u = ((q >> 2) << 3) + x;
+    u = k * 8 + ((x + k) & 7);
   } else {
     const int r = bid - 4 * full;
     u = full + (r >> 2);
@@ -376,11 +382,9 @@ __global__ __launch_bounds__(64 * WPB_FWD) __attribute__((amdgpu_waves_per_eu(fw
   // camera c of the batch: workgroups are dealt camera-minor (see cam_slot)
   STAMP(ts0);
   RT_STAMP(rt0);
-  int cam, bslot;
-  if constexpr (WPB_FWD == 1)
-    strip_of_block(blockIdx.x, cb.C, num_tiles_of(a0), cam, bslot);
-  else
-    cam_slot(blockIdx.x, cb.C, num_tiles_of(a0) * 4 / WPB_FWD, cam, bslot);
+  static_assert(WPB_FWD == 1, "strip_of_block maps one strip per workgroup");
+  int cam, item0;
+  strip_of_block(blockIdx.x, cb.C, num_tiles_of(a0), cam, item0);
   const RenderArgs ca = cam_render_args(a0, cb, cam);
   const int W = ca.W, H = ca.H, grid_x = ca.grid_x;
   const uint4* __restrict__ order = ca.order;
@@ -416,7 +420,7 @@ __global__ __launch_bounds__(64 * WPB_FWD) __attribute__((amdgpu_waves_per_eu(fw
 
   // strip item = tile * 4 + wave (dispatch order, see strip_item)
   const int lane = threadIdx.x & 63, lw = threadIdx.x >> 6;  // lw: LDS slot of the wave
-  const int item = strip_item(bslot, WPB_FWD) + lw;
+  const int item = item0 + lw;
   const uint4 trec = tile_rec(order, item >> 2);
   const int tile = (int)trec.x, wave = item & 3;
   const int tx = tile % grid_x, ty = tile / grid_x;

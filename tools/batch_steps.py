@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--size", type=int, default=800)
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--stamps", action="store_true", help="read the stamps build's wave-lifetime shares")
+    ap.add_argument("--dump-stamps", default="", help="with --stamps: save the raw per-wave stamps (npz)")
     a = ap.parse_args()
     _lib.load()
     dev = torch.device("cuda", 0)
@@ -76,6 +77,8 @@ def main():
         import json
         st = stamps[0].cpu().numpy().reshape(-1, 8).astype(np.float64)
         nf = stamps[1]
+        if a.dump_stamps:  # rows = waves in block order (forward first, then backward), 8 fields each
+            np.savez_compressed(a.dump_stamps, stamps=stamps[0].cpu().numpy().reshape(-1, 8), n_fwd=nf, cams=C)
         out = {}
         for name, v in (("render_fwd", st[:nf]), ("render_bwd", st[nf:])):
             v = v[v[:, 3] > 0]
