@@ -504,9 +504,11 @@ def main():
     # only the geometry gradients are exchanged on the step's critical path.
     # Double-buffered feature gradients: step k writes buffer k % 2 while the
     # exchange of step k-1 still reads the other.  GS_BENCH_OVERLAP=0: one
-    # bucket, exchanged before Adam.
-    overlap = (dist_on and world > 1 and args.features > 0 and args.mode == "batch"
-               and os.environ.get("GS_BENCH_OVERLAP", "1") != "0")
+    # bucket, exchanged before Adam; =force: overlapped at a world of one too
+    # (rehearses the RCCL async all-reduce + side-stream wait on one GPU).
+    ov_env = os.environ.get("GS_BENCH_OVERLAP", "1")
+    overlap = (dist_on and args.features > 0 and args.mode == "batch"
+               and ((world > 1 and ov_env != "0") or ov_env == "force"))
     if overlap:
         opt = make_opt([g_ for g_ in groups if g_["name"] != "semantic_feature"])
         opt_feat = make_opt([g_ for g_ in groups if g_["name"] == "semantic_feature"])

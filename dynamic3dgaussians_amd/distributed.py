@@ -183,12 +183,13 @@ class GradBucket:
     def all_reduce_async(self, group=None):
         """One all_reduce(SUM) of a bound bucket without extras, left running:
         returns the work handle (wait() on it -- on the stream that consumes
-        the gradients -- before using them), None without a process group.
+        the gradients -- before using them), None without a process group
+        (a world of one still runs the collective: bench.py's RCCL rehearsal).
         The gradients are summed in place in the bound views."""
         if not self.bound or self.extras or self.track:
             raise ValueError("all_reduce_async: bound gradients only (no extras, no reach tracking)")
         self.check_live()
-        if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        if not (dist.is_available() and dist.is_initialized()):
             return None
         return dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group, async_op=True)
 

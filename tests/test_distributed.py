@@ -5,6 +5,7 @@ RCCL is exercised only by the GPU bench (bench.py --gpus N under torchrun)."""
 import os
 import socket
 
+import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
@@ -315,3 +316,52 @@ def test_shard_camera_windows_partition_every_camera(n_cams, world, gx, gy):
     assert all(v == 1 for c in cover for row in cover[c] for v in row)
     left = n_cams % world
     assert max(load) - min(load) <= left * gx * (gy // world + 1)
+
+
+def _async_worker(rank, world, port, q):
+    """bench.py's overlapped exchange on two alternating feature buckets."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        f = torch.nn.Parameter(torch.zeros(7, 3))
+        buckets = [GradBucket({"f": f}, bind_grads=True) for _ in range(2)]
+        works, out = [None, None], []
+        for step in range(4):
+            b = buckets[step % 2]
+            if works[step % 2] is not None:  # the exchange of step - 2 read this buffer
+                works[step % 2].wait()
+            b.bind()
+            b.zero_grad()
+            (f * (rank + 1 + step)).sum().backward()
+            works[step % 2] = b.all_reduce_async()
+            prev = works[(step - 1) % 2]
+            if prev is not None and step > 0:  # step - 1's exchange, consumed behind this step
+                prev.wait()
+                out.append(buckets[(step - 1) % 2].flat[:21].clone().numpy())
+        works[3 % 2].wait()
+        out.append(buckets[3 % 2].flat[:21].clone().numpy())
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bucket_async_all_reduce_on_alternating_buffers():
+    """GradBucket.all_reduce_async + bind(): each step's gradients land in
+    the other buffer while the previous step's exchange may still run; every
+    step's summed gradient comes out of its own buffer (ranks 1 + s and
+    2 + s -> 3 + 2 s at step s)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_async_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(world):
+        assert len(res[r]) == 4
+        for s_, g in enumerate(res[r]):
+            np.testing.assert_array_equal(g, np.full(21, 3.0 + 2 * s_, np.float32))
