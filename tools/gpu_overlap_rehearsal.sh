@@ -15,7 +15,7 @@ run() {  # name, port, extra env
 }
 run ov1 29561 GS_BENCH_OVERLAP=1 && run ov0a 29562 GS_BENCH_OVERLAP=0 && run ov0b 29563 GS_BENCH_OVERLAP=0 || exit 1
 python -c "import json; d=json.load(open('$O/ov1.json')); print(d['config']['grad_exchange'], d['ms_per_step'])"
-python tools/compare_params.py $O/ov1.npz $O/ov0a.npz $O/ov0b.npz || exit 1
+python tools/compare_params.py $O/ov1.npz $O/ov0a.npz $O/ov0b.npz || { rm -f $O/*.npz; exit 1; }
 # The same exchange over RCCL at a world of one (RCCL refuses two ranks on one
 # GPU): GS_BENCH_OVERLAP=force runs the async all-reduce on RCCL's stream and
 # the side stream's wait on it; its parameters against two unoverlapped runs.
@@ -26,4 +26,6 @@ rrun() {  # name, port, overlap setting
 }
 rrun rccl_ov1 29571 force && rrun rccl_ov0a 29572 0 && rrun rccl_ov0b 29573 0 || exit 1
 python -c "import json; d=json.load(open('$O/rccl_ov1.json')); print(d['config']['grad_exchange'], d['ms_per_step'])"
-python tools/compare_params.py $O/rccl_ov1.npz $O/rccl_ov0a.npz $O/rccl_ov0b.npz
+python tools/compare_params.py $O/rccl_ov1.npz $O/rccl_ov0a.npz $O/rccl_ov0b.npz; rc=$?
+rm -f $O/*.npz  # the dumps are large; the comparisons above are the record
+exit $rc

@@ -6,7 +6,9 @@
 #   4. rocprofv3 --kernel-trace --stats of the same bench command
 #   5. a two-rank rehearsal of bench.py's distributed path on the one GPU
 #      (gloo): the weak headline + the 27-camera split step, and --cams-total 27;
-#      tools/timesteps_run.py (configs[3] shape) on one rank and on two
+#      tools/timesteps_run.py (configs[3] shape) on one rank and on two;
+#      the overlapped feature exchange against the serial one, over gloo
+#      (two ranks) and over RCCL (one rank), tools/gpu_overlap_rehearsal.sh
 # Outputs in gpurun_out/$TAG.
 set -o pipefail
 R=$GRAFT_REPO_ROOT
@@ -41,4 +43,6 @@ cat $O/dist2_weak.json $O/dist2_strong.json
 timeout -k 10 300 python tools/timesteps_run.py > $O/ts1.json 2> $O/ts1.err || { tail $O/ts1.err; exit 8; }
 GS_BENCH_BACKEND=gloo GS_BENCH_SHARE_GPU=1 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29541 tools/timesteps_run.py > $O/ts2.json 2> $O/ts2.err || { tail $O/ts2.err; exit 9; }
 cat $O/ts1.json $O/ts2.json
+TAG=$TAG/overlap timeout -k 10 900 bash tools/gpu_overlap_rehearsal.sh > $O/overlap.log 2>&1 || { tail -30 $O/overlap.log; exit 10; }
+grep -E "OK|MISMATCH|exchange" $O/overlap.log
 fi

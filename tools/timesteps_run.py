@@ -81,7 +81,8 @@ def main():
     with torch.no_grad():
         params["rgb_colors"].add_(0.2 * torch.randn(params["rgb_colors"].shape, device=dev, generator=gen))
     opt = FusedAdam([{"params": [params[k]], "name": k, "lr": lr} for k, lr in LRS.items()], lr=0.0, eps=1e-15)
-    drv = TimestepDriver(params, {}, opt, a.cams_total, render, rank=rank, world=world)
+    drv = TimestepDriver(params, {}, opt, a.cams_total, render, rank=rank, world=world,
+                         targets_sharded=True)  # tg holds this rank's cameras only
     # warm-up: one step of timestep 0 (kernel load, allocator), not timed
     drv.step(tg)
     torch.cuda.synchronize()
