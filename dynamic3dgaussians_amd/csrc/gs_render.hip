@@ -103,7 +103,11 @@ __device__ inline void strip_of_block(int bid, int C, int num_tiles, int& cam, i
   if (bid < 4 * full) {
     const int x = bid & 7, q = bid >> 3, k = q >> 2;
     s = q & 3;
+#ifdef GS_EXP_ROT_SMALL_C
+    u = k * 8 + ((x + (C < CAM_GROUP ? k : 0)) & 7);
+#else
     u = k * 8 + ((x + k) & 7);
+#endif
   } else {
     const int r = bid - 4 * full;
     u = full + (r >> 2);
