@@ -806,12 +806,6 @@ __device__ inline int sw_idx(int r, int c) { return r * 64 + ((((c >> 2) ^ r) & 
 // camera (F = 32); with the 3-piece split that needs the colour operand in
 // LDS and one k-step's split weights live at a time (flush), else 27-camera
 // render_bwd 6.0 ms at 2 waves vs 5.45 at 3; the widest instantiations keep 2.
-#ifdef GS_EXP_MERGE_COMMITS
-// timing only: keep a pseudo-random 41 % of the (Gaussian, strip) commits --
-// 1 / 2.43, the strip commits per (Gaussian, tile) commit of the bench scene
-// (one multiply-add and a compare: 0x68F5C28F / 2^32 = 0.41)
-__device__ inline bool exp_kept(uint32_t gi, int wave) { return gi * 2654435761u + (uint32_t)wave * 40503u < 0x68F5C28Fu; }
-#endif
 template <int F, int COMPAT>
 constexpr int bwd_waves_per_simd() {
   return (F < 32 || (F == 32 && COMPAT == COMPAT_REFERENCE)) ? 3 : 2;
@@ -870,12 +864,6 @@ __global__ __launch_bounds__(64 * WPB_BWD) __attribute__((amdgpu_waves_per_eu(bw
   __shared__ float s_w[WPB_BWD][WB * 64];
   __shared__ float s_u[WPB_BWD][WB * 64];
   __shared__ float4 s_slot[WPB_BWD][WB];  // (mean x - cx, mean y - cy, opacity, id bits)
-#ifdef GS_EXP_MERGE_LDS
-  // timing only: the LDS a half-chunk tile merge adds per wave (32 entries x
-  // 42 partial sums), allocated and never used -- its occupancy cost alone
-  __shared__ float s_merge_pad[WPB_BWD][32 * 42];
-  if (a0.W < 0) s_merge_pad[0][threadIdx.x] = 0.f;
-#endif
 
   // strip item = tile * 4 + wave (dispatch order, see strip_item)
   const int lane = threadIdx.x & 63, lw = threadIdx.x >> 6;  // lw: LDS slot of the wave
@@ -1160,9 +1148,6 @@ __global__ __launch_bounds__(64 * WPB_BWD) __attribute__((amdgpu_waves_per_eu(bw
 #ifdef GS_EXP_NO_ACC_ATOMIC
       // timing only (results wrong): the atomic-free ceiling
       if (slot < nb && s_out[i] == 12345.f) *dst = 0.f;
-#elif defined(GS_EXP_MERGE_COMMITS)
-      // timing only (results wrong): the commits a free tile merge would leave
-      if (slot < nb && exp_kept(gi, wave)) atomicAdd(dst, s_out[i]);
 #else
       if (slot < nb) atomicAdd(dst, s_out[i]);
 #endif
@@ -1177,8 +1162,6 @@ __global__ __launch_bounds__(64 * WPB_BWD) __attribute__((amdgpu_waves_per_eu(bw
         const uint32_t gi = fgid[r];
 #ifdef GS_EXP_NO_FEAT_ATOMIC
         if (slot < nb && cf[cb][r] == 12345.f) dsem[(size_t)gi * FS + 16 * cb + g] = 0.f;
-#elif defined(GS_EXP_MERGE_COMMITS)
-        if (slot < nb && exp_kept(gi, wave)) atomicAdd(dsem + (size_t)gi * FS + 16 * cb + g, cf[cb][r]);
 #else
         if (slot < nb) atomicAdd(dsem + (size_t)gi * FS + 16 * cb + g, cf[cb][r]);
 #endif
