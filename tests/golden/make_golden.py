@@ -34,6 +34,22 @@ fixtures -- data only -- are committed, the reference never travels).
    view.  Pins camera.setup_camera (the helpers.py:68-95 form every G1 caller
    uses) at a centred principal point, where the two forms must agree.
 
+5. train_helpers.npz -- the training loop's own helpers around the
+   rasterizer, from helpers.py and external.py: setup_camera (helpers.py:
+   68-95, the camera every Dynamic3DGaussians caller builds, here with
+   off-centre principal points), params2rendervar (:98-107, the activations
+   GS_FLAG_ACTIVATE folds into the kernels), l1_loss_v1/v2 and
+   weighted_l2_loss_v1/v2 (:110-122), quat_mult (:124-133), build_rotation
+   (external.py:61-78), calc_psnr (external.py:85-87), and the neighbour
+   losses composed from them exactly as train.py:256-270 does (rigid, rot,
+   iso).  Both files import Open3D at module level (for o3d_knn, which is not
+   called); Open3D is absent here, so an EMPTY placeholder module is
+   registered under that name while they load -- none of the functions used
+   touches it.  helpers.py's `Camera` (the rasterizer's settings tuple) is
+   replaced by a recorder of its keyword arguments, its `.cuda()` moves are
+   identity and its / external.py's hard-coded device="cuda" goes to the CPU
+   (there is no GPU here); nothing else is changed.
+
 Usage: python tests/golden/make_golden.py [--reference /root/reference]
 """
 from __future__ import annotations
@@ -232,6 +248,132 @@ def make_cameras(ref):
                         full_proj_transform=np.array(full), camera_center=np.array(centre))
 
 
+class _RecordCamera:
+    """helpers.py's `Camera` (GaussianRasterizationSettings): keeps the
+    keyword arguments setup_camera computes."""
+
+    def __init__(self, **kw):
+        self.kw = kw
+
+
+def _load_with_placeholders(name, path):
+    """Load a reference module whose top level imports Open3D (absent) and
+    the rasterizer package: both names point at inert placeholders while it
+    loads."""
+    saved = {k: sys.modules.get(k) for k in ("open3d", "diff_gaussian_rasterization")}
+    sys.modules["open3d"] = types.ModuleType("open3d")
+    dgr = types.ModuleType("diff_gaussian_rasterization")
+    dgr.GaussianRasterizationSettings = _RecordCamera
+    dgr.GaussianRasterizer = None
+    sys.modules["diff_gaussian_rasterization"] = dgr
+    try:
+        return _load_module(name, path)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                sys.modules.pop(k, None)
+            else:
+                sys.modules[k] = v
+
+
+class _TorchOnCPUAll(_TorchOnCPU):
+    """_TorchOnCPU plus zeros_like / ones / tensor without their device."""
+
+    @staticmethod
+    def zeros_like(*a, **kw):
+        kw.pop("device", None)
+        return torch.zeros_like(*a, **kw)
+
+    @staticmethod
+    def ones(*a, **kw):
+        kw.pop("device", None)
+        return torch.ones(*a, **kw)
+
+    @staticmethod
+    def tensor(*a, **kw):
+        kw.pop("device", None)
+        return torch.tensor(*a, **kw)
+
+
+def make_train_helpers(ref):
+    hp = _load_with_placeholders("ref_helpers", os.path.join(ref, "helpers.py"))
+    ex = _load_with_placeholders("ref_external", os.path.join(ref, "external.py"))
+    hp.torch = _TorchOnCPUAll("torch")
+    ex.torch = _TorchOnCPUAll("torch")
+    cuda0 = torch.Tensor.cuda
+    torch.Tensor.cuda = lambda self, *a, **kw: self  # the .cuda() moves of setup_camera
+    out = {}
+    try:
+        rng = np.random.default_rng(7)
+        cams = {k: [] for k in ("w", "h", "k", "w2c", "viewmatrix", "projmatrix", "campos", "tanfovx", "tanfovy",
+                                "c_x", "c_y")}
+        for i in range(12):
+            w, h = int(rng.integers(64, 1921)), int(rng.integers(64, 1081))
+            fx, fy = float(rng.uniform(0.6, 1.6) * w), float(rng.uniform(0.6, 1.6) * w)
+            cx, cy = float(w / 2 + rng.uniform(-0.2, 0.2) * w), float(h / 2 + rng.uniform(-0.2, 0.2) * h)
+            if i == 0:
+                cx, cy = w / 2, h / 2
+            K = [[fx, 0.0, cx], [0.0, fy, cy], [0.0, 0.0, 1.0]]
+            q, _ = np.linalg.qr(rng.standard_normal((3, 3)))
+            if np.linalg.det(q) < 0:
+                q[:, 0] = -q[:, 0]
+            w2c = np.eye(4)
+            w2c[:3, :3], w2c[:3, 3] = q, rng.uniform(-3, 3, 3)
+            cam = hp.setup_camera(w, h, K, w2c.tolist())
+            kw = cam.kw
+            for k, v in (("w", w), ("h", h), ("k", np.array(K)), ("w2c", w2c),
+                         ("viewmatrix", kw["viewmatrix"].reshape(4, 4).numpy()),
+                         ("projmatrix", kw["projmatrix"].reshape(4, 4).numpy()), ("campos", kw["campos"].numpy()),
+                         ("tanfovx", kw["tanfovx"]), ("tanfovy", kw["tanfovy"]), ("c_x", kw["c_x"]),
+                         ("c_y", kw["c_y"])):
+                cams[k].append(v)
+        for k, v in cams.items():
+            out[f"cam_{k}"] = np.array(v)
+        g = torch.Generator().manual_seed(8)
+        P = 2000
+        params = {"means3D": torch.randn(P, 3, generator=g), "rgb_colors": torch.rand(P, 3, generator=g),
+                  "unnorm_rotations": torch.randn(P, 4, generator=g) * torch.exp(torch.randn(P, 1, generator=g)),
+                  "logit_opacities": torch.randn(P, 1, generator=g) * 3,
+                  "log_scales": torch.randn(P, 3, generator=g) - 4}
+        rv = hp.params2rendervar(params)
+        for k, v in params.items():
+            out[f"p_{k}"] = v.numpy()
+        for k in ("rotations", "opacities", "scales"):
+            out[f"rv_{k}"] = rv[k].numpy()
+        x, y = torch.randn(64, 3, generator=g), torch.randn(64, 3, generator=g)
+        wt = torch.rand(64, 1, generator=g)
+        out.update(loss_x=x.numpy(), loss_y=y.numpy(), loss_w=wt.numpy(),
+                   l1_v1=hp.l1_loss_v1(x, y).numpy(), l1_v2=hp.l1_loss_v2(x, y).numpy(),
+                   wl2_v1=hp.weighted_l2_loss_v1(x, y, wt).numpy(), wl2_v2=hp.weighted_l2_loss_v2(x, y, wt[:, 0]).numpy())
+        img1, img2 = torch.rand(3, 48, 40, generator=g), torch.rand(3, 48, 40, generator=g)
+        out.update(psnr_img1=img1.numpy(), psnr_img2=img2.numpy(), psnr=ex.calc_psnr(img1, img2).numpy())
+        # the neighbour losses as train.py:256-270 composes them
+        N, K = 400, 10
+        fg_pts = torch.randn(N, 3, generator=g)
+        fg_rot = torch.nn.functional.normalize(torch.randn(N, 4, generator=g))
+        prev_inv = torch.nn.functional.normalize(torch.randn(N, 4, generator=g))
+        nbr = (torch.arange(N)[:, None] + torch.randint(1, N, (N, K), generator=g)) % N
+        nw = torch.rand(N, K, generator=g)
+        prev_off = torch.randn(N, K, 3, generator=g) * 0.3
+        ndist = torch.rand(N, K, generator=g)
+        rel_rot = hp.quat_mult(fg_rot, prev_inv)
+        rot = ex.build_rotation(rel_rot)
+        neighbor_pts = fg_pts[nbr]
+        curr_offset = neighbor_pts - fg_pts[:, None]
+        cop = (rot.transpose(2, 1)[:, None] @ curr_offset[:, :, :, None]).squeeze(-1)
+        rigid = hp.weighted_l2_loss_v2(cop, prev_off, nw)
+        rot_l = hp.weighted_l2_loss_v2(rel_rot[nbr], rel_rot[:, None], nw)
+        mag = torch.sqrt((curr_offset ** 2).sum(-1) + 1e-20)
+        iso = hp.weighted_l2_loss_v1(mag, ndist, nw)
+        out.update(nb_fg_pts=fg_pts.numpy(), nb_fg_rot=fg_rot.numpy(), nb_prev_inv_rot=prev_inv.numpy(),
+                   nb_indices=nbr.numpy(), nb_weight=nw.numpy(), nb_prev_offset=prev_off.numpy(),
+                   nb_dist=ndist.numpy(), nb_rel_rot=rel_rot.numpy(), nb_rot=rot.numpy(),
+                   nb_rigid=rigid.numpy(), nb_rot_loss=rot_l.numpy(), nb_iso=iso.numpy())
+    finally:
+        torch.Tensor.cuda = cuda0
+    np.savez_compressed(os.path.join(HERE, "train_helpers.npz"), **out)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reference", default="/root/reference")
@@ -240,6 +382,7 @@ def main():
     make_conventions(a.reference)
     make_cov3d(a.reference)
     make_cameras(a.reference)
+    make_train_helpers(a.reference)
     print("wrote", os.listdir(HERE))
 
 

@@ -1,0 +1,73 @@
+"""The training loop's helpers around the rasterizer against the reference's
+own Python (tests/golden/train_helpers.npz, made by tests/golden/make_golden.py
+from helpers.py and external.py): the camera every caller builds, the
+activations GS_FLAG_ACTIVATE folds into the kernels, the losses, the PSNR
+the bench reports, and the neighbour-loss oracle that checks the HIP
+neighbour kernels (oracle/neighbor.py; Open3D's k-NN graph itself stays
+unpinned -- the fixture's neighbour indices are given, not searched)."""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+
+from dynamic3dgaussians_amd.camera import setup_camera
+from dynamic3dgaussians_amd.timesteps import params2rendervar
+from oracle import neighbor as onb
+
+G = np.load(os.path.join(os.path.dirname(__file__), "golden", "train_helpers.npz"))
+
+
+def test_setup_camera_matches_helpers_setup_camera():
+    """helpers.py:68-95, off-centre principal points included: the same
+    view / full-projection matrices (column-major, as the rasterizer reads
+    them), camera centre, tan(fov/2) and principal point."""
+    for i in range(len(G["cam_w"])):
+        c = setup_camera(int(G["cam_w"][i]), int(G["cam_h"][i]), G["cam_k"][i], G["cam_w2c"][i])
+        np.testing.assert_allclose(c.viewmatrix, G["cam_viewmatrix"][i], rtol=0, atol=1e-6)
+        np.testing.assert_allclose(c.projmatrix, G["cam_projmatrix"][i], rtol=1e-6, atol=1e-6)
+        np.testing.assert_allclose(c.campos, G["cam_campos"][i], rtol=1e-6, atol=1e-6)
+        assert c.tanfovx == float(G["cam_tanfovx"][i]) and c.tanfovy == float(G["cam_tanfovy"][i])
+        assert c.c_x == float(G["cam_c_x"][i]) and c.c_y == float(G["cam_c_y"][i])
+
+
+def test_params2rendervar_matches_helpers_bit_for_bit():
+    """helpers.py:98-107 on the CPU: normalise / sigmoid / exp."""
+    params = {k[2:]: torch.from_numpy(G[k]) for k in G.files if k.startswith("p_")}
+    rv = params2rendervar(params)
+    for k in ("rotations", "opacities", "scales"):
+        assert torch.equal(rv[k], torch.from_numpy(G[f"rv_{k}"])), k
+
+
+def test_losses_and_psnr_match_reference():
+    from bench import calc_psnr
+    x, y, w = (torch.from_numpy(G[k]) for k in ("loss_x", "loss_y", "loss_w"))
+    assert torch.abs(x - y).mean().item() == float(G["l1_v1"])          # helpers.py:110-111
+    assert onb._wl2_v1(x, y, w).item() == float(G["wl2_v1"])            # helpers.py:117-118
+    assert onb._wl2_v2(x, y, w[:, 0]).item() == float(G["wl2_v2"])      # helpers.py:121-122
+    # bench.py's PSNR: external.py:85-87 per channel, averaged over the channels
+    ref = np.asarray(G["psnr"], np.float64).reshape(-1)
+    assert abs(calc_psnr(G["psnr_img1"], G["psnr_img2"]) - ref.mean()) < 1e-4
+
+
+def test_neighbour_loss_oracle_matches_reference_composition():
+    """oracle/neighbor.py's torch restatement (fp32, the checker of the HIP
+    neighbour kernels) against train.py:256-270 composed from the
+    reference's quat_mult / build_rotation / weighted_l2 losses; its float64
+    numpy restatement within fp32 rounding."""
+    fg_pts, fg_rot = torch.from_numpy(G["nb_fg_pts"]), torch.from_numpy(G["nb_fg_rot"])
+    variables = {"neighbor_indices": torch.from_numpy(G["nb_indices"]),
+                 "neighbor_weight": torch.from_numpy(G["nb_weight"]),
+                 "prev_inv_rot_fg": torch.from_numpy(G["nb_prev_inv_rot"]),
+                 "prev_offset": torch.from_numpy(G["nb_prev_offset"]),
+                 "neighbor_dist": torch.from_numpy(G["nb_dist"])}
+    assert torch.equal(onb._quat_mult(fg_rot, variables["prev_inv_rot_fg"]), torch.from_numpy(G["nb_rel_rot"]))
+    assert torch.equal(onb._build_rotation(torch.from_numpy(G["nb_rel_rot"])), torch.from_numpy(G["nb_rot"]))
+    rigid, rot, iso = onb.torch_reference(fg_pts, fg_rot, variables)
+    for got, key in ((rigid, "nb_rigid"), (rot, "nb_rot_loss"), (iso, "nb_iso")):
+        assert got.item() == float(G[key]), (key, got.item(), float(G[key]))
+    r64 = onb.numpy_losses(G["nb_fg_pts"], G["nb_fg_rot"], G["nb_indices"], G["nb_weight"], G["nb_dist"],
+                           G["nb_prev_offset"], G["nb_prev_inv_rot"])
+    for got, key in zip(r64, ("nb_rigid", "nb_rot_loss", "nb_iso")):
+        assert abs(got - float(G[key])) <= 2e-6 * abs(float(G[key])), key
