@@ -6,7 +6,11 @@ Panoptic-sized scene of 300k Gaussians rendered from a 27-camera rig at
 800x800 (G3 call pattern of dyn_train.py:244: precomputed colours +
 32-channel semantic features + label), forward AND backward for every camera,
 then ONE flat all-reduce of the per-Gaussian gradients (N > 1) and an Adam
-step -- one step of the per-timestep training loop.  Data is synthetic (no
+step -- one step of the per-timestep training loop.  With features (camera
+batch mode) the features' all-reduce (N > 1) and Adam step run on a side
+stream behind the next step's projection and binning, whose blend waits for
+them (gs_gaussians.feature_ready; GS_BENCH_OVERLAP=0: in line); the timed
+region ends after they do.  Data is synthetic (no
 network): seeded Gaussians and cameras (dynamic3dgaussians_amd/scene.py,
 camera.py).
 
@@ -509,7 +513,12 @@ def main():
     ov_env = os.environ.get("GS_BENCH_OVERLAP", "1")
     overlap = (dist_on and args.features > 0 and args.mode == "batch"
                and ((world > 1 and ov_env != "0") or ov_env == "force"))
-    if overlap:
+    # One rank, no process group: nothing to exchange, but the feature Adam
+    # step (32 of the 46 floats per Gaussian) still runs on the side stream
+    # behind the next step's projection and binning, gated the same way.
+    local_overlap = (not dist_on and args.features > 0 and args.mode == "batch" and ov_env != "0")
+    split_opt = overlap or local_overlap
+    if split_opt:
         opt = make_opt([g_ for g_ in groups if g_["name"] != "semantic_feature"])
         opt_feat = make_opt([g_ for g_ in groups if g_["name"] == "semantic_feature"])
     else:
@@ -523,10 +532,11 @@ def main():
         bucket = GradBucket({k: v for k, v in params.items() if k != "semantic_feature"}, bind_grads=True)
         feat_buckets = [GradBucket({"semantic_feature": params["semantic_feature"]}, bind_grads=True)
                         for _ in range(2)]
-        side = torch.cuda.Stream(device=dev)
-        pipe = {"k": 0, "done": [None, None]}
     else:
         bucket = GradBucket(params, bind_grads=dist_on)
+    if split_opt:
+        side = torch.cuda.Stream(device=dev)
+        pipe = {"k": 0, "done": [None, None]}
     g = torch.Generator(device=dev).manual_seed(1 + rank)
     H_, W_ = args.height, args.width
     up_color = torch.randn(3, H_, W_, device=dev, generator=g)
@@ -591,7 +601,7 @@ def main():
 
     def drain():
         """Overlap mode: the main stream waits for every pending feature update."""
-        if overlap:
+        if split_opt:
             for ev in pipe["done"]:
                 if ev is not None:
                     torch.cuda.current_stream(dev).wait_event(ev)
@@ -621,9 +631,31 @@ def main():
         pipe["done"][k % 2] = ev
         pipe["k"] = k + 1
 
+    def step_local_overlap(parts):
+        """One rank: the geometry Adam on the main stream, the feature Adam on
+        the side stream behind the next step's projection and binning."""
+        main = torch.cuda.current_stream(dev)
+        bucket.zero_grad()
+        rv = raw_rendervar(params, label, means2D_placeholder) if raw else params2rendervar(params, label)
+        for ras, ups, _ in parts:
+            run_part(ras, ups, rv, ready=pipe["done"][0])
+        opt.step()
+        side.wait_stream(main)
+        fg = params["semantic_feature"].grad
+        with torch.cuda.stream(side):
+            opt_feat.step()
+            ev = torch.cuda.Event()
+            ev.record(side)
+        if fg is not None:  # read on the side stream after the main stream drops it
+            fg.record_stream(side)
+        pipe["done"][0] = ev
+        pipe["k"] += 1
+
     def step_batch(parts=batch_parts):
         if overlap and len(parts) == 1:
             return step_overlap(parts)
+        if local_overlap and len(parts) == 1:
+            return step_local_overlap(parts)
         drain()
         if overlap:
             feat_buckets[0].bind()
@@ -648,6 +680,7 @@ def main():
         opt.step()
         if overlap:
             feat_buckets[0].all_reduce()
+        if split_opt:
             opt_feat.step()
 
     def step(mode=args.mode):
@@ -697,6 +730,7 @@ def main():
         opt.step()
         if overlap:
             feat_buckets[0].all_reduce()
+        if split_opt:
             opt_feat.step()
 
     for _ in range(args.warmup):
@@ -886,7 +920,9 @@ def main():
                    "parallelism": f"camera-sharded dp{world}",
                    "grad_exchange": ("geometry all-reduce before Adam; feature all-reduce + Adam overlapped with the "
                                      "next step's projection and binning" if overlap else
-                                     "one all-reduce before Adam" if world > 1 else "none (one rank)")},
+                                     "one all-reduce before Adam" if world > 1 else
+                                     "none (one rank); the feature Adam step overlapped with the next step's "
+                                     "projection and binning" if local_overlap else "none (one rank)")},
         "roofline": roofline,
         "stages_ms_per_step": {k: round(v, 4) for k, v in stage_ms.items()},
         "split_step": split,
