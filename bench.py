@@ -516,7 +516,8 @@ def main():
     # One rank, no process group: nothing to exchange, but the feature Adam
     # step (32 of the 46 floats per Gaussian) still runs on the side stream
     # behind the next step's projection and binning, gated the same way.
-    local_overlap = (not dist_on and args.features > 0 and args.mode == "batch" and ov_env != "0")
+    local_overlap = (not dist_on and args.features > 0 and args.mode == "batch"
+                     and os.environ.get("GS_BENCH_OVERLAP", "0") == "1")
     split_opt = overlap or local_overlap
     if split_opt:
         opt = make_opt([g_ for g_ in groups if g_["name"] != "semantic_feature"])
