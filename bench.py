@@ -7,9 +7,10 @@ Panoptic-sized scene of 300k Gaussians rendered from a 27-camera rig at
 32-channel semantic features + label), forward AND backward for every camera,
 then ONE flat all-reduce of the per-Gaussian gradients (N > 1) and an Adam
 step -- one step of the per-timestep training loop.  With features (camera
-batch mode) the features' all-reduce (N > 1) and Adam step run on a side
+batch mode, N > 1) the features' all-reduce and Adam step run on a side
 stream behind the next step's projection and binning, whose blend waits for
-them (gs_gaussians.feature_ready; GS_BENCH_OVERLAP=0: in line); the timed
+them (gs_gaussians.feature_ready; GS_BENCH_OVERLAP=0: in line; at one rank
+GS_BENCH_OVERLAP=1 overlaps the feature Adam step the same way); the timed
 region ends after they do.  Data is synthetic (no
 network): seeded Gaussians and cameras (dynamic3dgaussians_amd/scene.py,
 camera.py).
