@@ -39,7 +39,6 @@ VARIANT_FLAGS = {"": [], "stats": ["-DGS_STATS"], "stamps": ["-DGS_STAMPS"],
                  "stamps_fine": ["-DGS_STAMPS", "-DGS_STAMPS_FINE"],
                  "exp_nofeat": ["-DGS_EXP_NO_FEAT_ATOMIC"],
                  "exp_noatomic": ["-DGS_EXP_NO_FEAT_ATOMIC", "-DGS_EXP_NO_ACC_ATOMIC"],
-                 "exp_rot_small_c": ["-DGS_EXP_ROT_SMALL_C"],
                  "ctl": []}  # the product's flags under a variant's (ctypes) binding: the A/B control
 ARCH = os.environ.get("GSPLAT_OFFLOAD_ARCH", "gfx950")
 

@@ -88,14 +88,17 @@ __device__ inline void cam_slot(int bid, int C, int per_cam, int& cam, int& slot
 // kernels.  A (camera, tile) unit is 4 strip workgroups, and those 4 sit on
 // one XCD (one L2 fill of the tile's records and feature rows): units are
 // dealt 8 at a time, one per XCD -- the k-th group of 8 units is blocks
-// 32k .. 32k+31, strip s of its unit j on XCD (j - k) mod 8 (block
-// 32k + 8s + x holds unit 8k + (x + k) mod 8).  Units are ordered by
-// cam_slot (groups of 8 cameras, camera-minor, longest tiles first).  The
-// rotation by k matters at C < 8 (an 8-rank split: 3-4 cameras per rank):
+// 32k .. 32k+31, block 32k + 8s + x holding strip s of unit 8k + (x + r) mod 8
+// on XCD x (r = k at C < 8, else 0: see below).  Units are ordered by
+// cam_slot (groups of 8 cameras, camera-minor, longest tiles first).  At
+// C < 8 (an 8-rank split: 3-4 cameras per rank) the groups are rotated by k:
 // without it XCD x rendered only camera x mod C, and the XCDs holding the
 // heavier cameras finished last (per-XCD work at 4 cameras 698-809 us of
 // the 850 us backward, tools/batch_steps.py --stamps; 4-camera backward
-// 0.785-0.798 vs 0.825-0.832 ms rotated, profiles/r04j/).  The last U % 8
+// 0.785-0.798 vs 0.825-0.832 ms rotated, profiles/r04j/).  At C >= 8 each XCD
+// renders one camera of a group at a time, unrotated: the rotation measured
+// the same there but read 3.6 GB more per 27-camera step (render_fwd 4.25
+// vs 2.56 GB, render_bwd 7.13 vs 5.19; profiles/r04q/).  The last U % 8
 // units keep plain order.
 __device__ inline void strip_of_block(int bid, int C, int num_tiles, int& cam, int& item) {
   const int U = C * num_tiles, full = U & ~7;
@@ -103,11 +106,7 @@ __device__ inline void strip_of_block(int bid, int C, int num_tiles, int& cam, i
   if (bid < 4 * full) {
     const int x = bid & 7, q = bid >> 3, k = q >> 2;
     s = q & 3;
-#ifdef GS_EXP_ROT_SMALL_C
     u = k * 8 + ((x + (C < CAM_GROUP ? k : 0)) & 7);
-#else
-    u = k * 8 + ((x + k) & 7);
-#endif
   } else {
     const int r = bid - 4 * full;
     u = full + (r >> 2);
