@@ -7,8 +7,8 @@
 //  * A 16x16 binning tile is four 8x8 pixel strips (STRIP_W x STRIP_H,
 //    gs_common.h); one wave64 owns a strip (lane = pixel) and walks the
 //    tile's depth-sorted list on its own -- no block barriers, every wave
-//    exits when its own pixels are done.  The forward packs a tile's 4 waves
-//    into one workgroup (WPB_FWD), the backward runs a wave per workgroup.
+//    exits when its own pixels are done.  Both kernels run a wave per
+//    workgroup, a tile's 4 strip workgroups on one XCD (strip_of_block).
 //  * The list is consumed in chunks of 64: lane j gathers the 64-B render
 //    record (gs_common.h R_*) of the chunk's j-th Gaussian (prefetched one
 //    chunk ahead, ids two chunks ahead), tests it against the wave's strip
@@ -382,7 +382,7 @@ constexpr int fwd_waves_per_simd() {
 template <int F, int COMPAT>
 __global__ __launch_bounds__(64 * WPB_FWD) __attribute__((amdgpu_waves_per_eu(fwd_waves_per_simd<F>(), 8))) void render_fwd_kernel(
     RenderArgs a0, CamBatch cb) {
-  // camera c of the batch: workgroups are dealt camera-minor (see cam_slot)
+  // camera and strip of this workgroup (strip_of_block)
   STAMP(ts0);
   RT_STAMP(rt0);
   static_assert(WPB_FWD == 1, "strip_of_block maps one strip per workgroup");
@@ -421,7 +421,7 @@ __global__ __launch_bounds__(64 * WPB_FWD) __attribute__((amdgpu_waves_per_eu(fw
   // batch weights [slot][pixel] (row pad 4: conflict-free writes and reads)
   __shared__ float s_fw[WPB_FWD][MF ? WBF + 1 : 1][68];  // +1: a pair may overfill by one
 
-  // strip item = tile * 4 + wave (dispatch order, see strip_item)
+  // strip item = tile slot * 4 + strip (the tile slot in dispatch order)
   const int lane = threadIdx.x & 63, lw = threadIdx.x >> 6;  // lw: LDS slot of the wave
   const int item = item0 + lw;
   const uint4 trec = tile_rec(order, item >> 2);
@@ -812,7 +812,7 @@ constexpr int bwd_waves_per_simd() {
 template <int F, int COMPAT>
 __global__ __launch_bounds__(64 * WPB_BWD) __attribute__((amdgpu_waves_per_eu(bwd_waves_per_simd<F, COMPAT>(), 8))) void render_bwd_kernel(
     RenderBwdArgs a0, CamBatch cb) {
-  // camera c of the batch: workgroups are dealt camera-minor (see cam_slot)
+  // camera and strip of this workgroup (strip_of_block)
   STAMP(ts0);
   RT_STAMP(rt0);
   static_assert(WPB_BWD == 1, "strip_of_block maps one strip per workgroup");
@@ -864,7 +864,7 @@ __global__ __launch_bounds__(64 * WPB_BWD) __attribute__((amdgpu_waves_per_eu(bw
   __shared__ float s_u[WPB_BWD][WB * 64];
   __shared__ float4 s_slot[WPB_BWD][WB];  // (mean x - cx, mean y - cy, opacity, id bits)
 
-  // strip item = tile * 4 + wave (dispatch order, see strip_item)
+  // strip item = tile slot * 4 + strip (the tile slot in dispatch order)
   const int lane = threadIdx.x & 63, lw = threadIdx.x >> 6;  // lw: LDS slot of the wave
   const int item = strip_item(bslot, WPB_BWD) + lw;
   const uint4 trec = tile_rec(order, item >> 2);
