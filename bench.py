@@ -30,10 +30,10 @@ step time.  `--cams-total T` makes the headline the north star's step split
 across the ranks instead (BASELINE.json configs[3], strong scaling): ONE rig
 of T cameras split over the ranks (--split cameras, the default: camera c on
 rank c mod N, distributed.shard_cameras; --split windows: the first
-N * (T // N) cameras whole, c mod N, the T % N left over cut into N bands of
-tile rows, band k on rank k -- image sharding, gs_camera tile_*,
-distributed.shard_camera_windows; measured slower on the 27-camera rig at
-8 ranks), each rank
+N * (T // N) cameras whole, c mod N, the T % N left over cut into bands of
+tile rows that even out the ranks' work (tile-list instances per row from
+a probe forward of the rig) -- image sharding, gs_camera tile_*,
+distributed.shard_camera_windows), each rank
 renders its share as one batch, then the gradient all-reduce and Adam;
 value = T cameras' pixels / step time.  At N > 1 the weak headline is
 followed by the same measurement of the 27-camera split step, reported as
@@ -184,12 +184,39 @@ def raw_rendervar(params, label, means2D):
     return rv
 
 
-def split_shard(n_cams, rank, world, how, W, H):
+def split_shard(n_cams, rank, world, how, W, H, row_cost=None):
     """[(camera, tile window or None)] of `rank` in a `world`-rank split of an
-    n_cams rig (--split)."""
+    n_cams rig (--split; windows balanced by `row_cost`, rig_row_costs)."""
     if how == "cameras":
         return [(c, None) for c in shard_cameras(n_cams, rank, world)]
-    return shard_camera_windows(n_cams, rank, world, (W + 15) // 16, (H + 15) // 16)
+    return shard_camera_windows(n_cams, rank, world, (W + 15) // 16, (H + 15) // 16, row_cost=row_cost)
+
+
+def rig_row_costs(rig, params, label, args, dev):
+    """The work model of --split windows: per camera of `rig` and tile row,
+    the instances of the row's tile lists (one forward per camera, the tile
+    ranges read back with gs_debug_export).  Every rank computes the same."""
+    from dynamic3dgaussians_amd import _C
+    L_ = _lib.load()
+    W, H = args.width, args.height
+    gx, gy = (W + 15) // 16, (H + 15) // 16
+    P = params["means3D"].shape[0]
+    out = []
+    with torch.no_grad():
+        rv = params2rendervar(params, label)
+        for s in make_settings(rig, dev, args.compat):
+            o = _C.rasterize_gaussians_batch(
+                s.bg, rv["means3D"], rv["colors_precomp"], None, rv["opacities"], rv["scales"], rv["rotations"],
+                1.0, torch.Tensor([]), s.viewmatrix.reshape(1, 16), s.projmatrix.reshape(1, 16), [s.c_x], [s.c_y],
+                [s.tanfovx], [s.tanfovy], H, W, torch.Tensor([]), 0, s.campos.reshape(1, 3), False, False,
+                compat=args.compat)
+            rg = torch.zeros(gx * gy, 2, dtype=torch.int32, device=dev)
+            _lib.check(L_.gs_debug_export(P, W, H, o[6].data_ptr(), None, o[8].data_ptr(), 0, None, None, None,
+                                          None, None, None, rg.data_ptr(), None,
+                                          torch.cuda.current_stream(dev).cuda_stream), "tile ranges")
+            r = rg.cpu().numpy().view(np.uint32).reshape(gy, gx, 2).astype(np.int64)
+            out.append((r[..., 1] - r[..., 0]).sum(1).tolist())
+    return out
 
 
 def make_settings(cams, dev, compat, sink=None, windows=None):
@@ -458,6 +485,7 @@ def main():
 
     strong = args.cams_total > 0
     my_windows = None
+    params, label = make_params(args, dev)
     if args.proxy_world and (world > 1 or not strong):
         raise SystemExit("--proxy-world stands in for one rank of a --cams-total split on ONE process")
     if strong:
@@ -466,7 +494,8 @@ def main():
         if args.split == "cameras" and args.cams_total < s_world:
             raise SystemExit(f"--cams-total {args.cams_total} < {s_world} ranks")
         rig = camera_rig(args.cams_total, args.width, args.height, seed=args.seed)
-        shard = split_shard(args.cams_total, s_rank, s_world, args.split, args.width, args.height)
+        costs = rig_row_costs(rig, params, label, args, dev) if args.split == "windows" else None
+        shard = split_shard(args.cams_total, s_rank, s_world, args.split, args.width, args.height, costs)
         my_cams = [rig[c] for c, _ in shard]
         if any(w is not None for _, w in shard):
             my_windows = [w for _, w in shard]
@@ -480,7 +509,6 @@ def main():
     use_sink = os.environ.get("GS_BENCH_SINK", "1") != "0"
     sink = GradientSink() if use_sink else None
     settings = make_settings(my_cams, dev, args.compat, sink, my_windows)
-    params, label = make_params(args, dev)
     # the CPU-baseline / PSNR leg renders the initial scene (independent of the
     # optimizer steps taken by warmup and timing)
     params0 = {k: v.detach().clone() for k, v in params.items()}
@@ -821,19 +849,21 @@ def main():
     # scaling), measured after a weak-scaling headline at N > 1; at N = 1 it
     # is the headline's own step (27 cameras on one rank).
     split = None
-    sharding_note = ("first N*(T//N) cameras whole, c mod N; the T%N left over in N bands of tile rows "
-                     "(distributed.shard_camera_windows)" if args.split == "windows" else
+    sharding_note = ("first N*(T//N) cameras whole, c mod N; the T%N left over cut into bands of tile rows "
+                     "balancing the ranks' tile-list instances (distributed.shard_camera_windows)"
+                     if args.split == "windows" else
                      "camera c on rank c mod N (distributed.shard_cameras)")
     if not strong and args.mode == "batch":
         n_split = args.cams
         if world > 1:
             rig_s = camera_rig(n_split, args.width, args.height, seed=args.seed)
-            mine = split_shard(n_split, rank, world, args.split, args.width, args.height)
+            costs_s = rig_row_costs(rig_s, params0, label, args, dev) if args.split == "windows" else None
+            mine = split_shard(n_split, rank, world, args.split, args.width, args.height, costs_s)
             wins = [w for _, w in mine] if any(w is not None for _, w in mine) else None
             parts_s = batch_inputs(make_settings([rig_s[c] for c, _ in mine], dev, args.compat, None, wins),
                                    args.sub_batches)
             el_s = timed(lambda: step_batch(parts_s))
-            cams_rank = [len(split_shard(n_split, r, world, args.split, args.width, args.height))
+            cams_rank = [len(split_shard(n_split, r, world, args.split, args.width, args.height, costs_s))
                          for r in range(world)]
             del parts_s
         else:

@@ -22,23 +22,64 @@ def shard_cameras(n_cams: int, rank: int, world: int) -> List[int]:
     return [c for c in range(n_cams) if c % world == rank]
 
 
-def shard_camera_windows(n_cams: int, rank: int, world: int, grid_x: int, grid_y: int
+def shard_camera_windows(n_cams: int, rank: int, world: int, grid_x: int, grid_y: int,
+                         row_cost: Optional[Sequence[Sequence[float]]] = None
                          ) -> List[Tuple[int, Optional[Tuple[int, int, int, int]]]]:
     """Balanced split of an n_cams rig over `world` ranks with image sharding
     (gs_camera tile_*): the first world * (n_cams // world) cameras whole,
-    camera c on rank c mod world, and every one of the n_cams % world left
-    over cameras cut into `world` bands of tile rows, band k on rank k -- so
-    every rank renders n_cams / world cameras' worth of pixels (27 cameras
-    over 8 ranks: 3 whole cameras and 3 eighths, instead of 3 or 4 whole
-    ones).  Returns [(camera, window or None)], window = (x0, y0, x1, y1) in
-    tiles; bands of a grid with fewer tile rows than ranks may be empty and
-    are left out.  The windows of a camera partition its tile grid, so the
-    ranks' gradients sum to the rig's."""
+    camera c on rank c mod world, and the n_cams % world left-over cameras
+    cut into bands of tile rows that even out the ranks' totals.
+
+    The left-over cameras' tile rows are laid end to end (camera-major) and
+    cut into `world` consecutive runs, run k to rank k, each as long as rank
+    k needs to reach the common level of the balanced loads (the mean unless
+    some rank's whole cameras alone exceed it) -- so a rank gets a few bands
+    (one or two on the 27-camera rig over 8 ranks), not a band of every
+    left-over camera.  `row_cost[c][y]` is the work of camera c's tile row y
+    (e.g. its tile-list instances from a previous forward); without it every
+    row of every camera costs the same (the pixel split).  Returns
+    [(camera, window or None)], window = (x0, y0, x1, y1) in tiles, rank-major
+    deterministic (every rank computes the same cut).  The windows of a camera
+    partition its tile grid, so the ranks' gradients sum to the rig's."""
     q, r = divmod(n_cams, world)
+    cost = (lambda c, y: 1.0) if row_cost is None else (lambda c, y: max(float(row_cost[c][y]), 0.0))
     out = [(c, None) for c in range(q * world) if c % world == rank]
-    y0, y1 = rank * grid_y // world, (rank + 1) * grid_y // world
-    if r and y1 > y0:
-        out += [(c, (0, y0, grid_x, y1)) for c in range(q * world, n_cams)]
+    if not r:
+        return out
+    whole = [sum(cost(c, y) for c in range(q * world) if c % world == k for y in range(grid_y))
+             for k in range(world)]
+    seq = [(c, y) for c in range(q * world, n_cams) for y in range(grid_y)]
+    pre = [0.0]
+    for c, y in seq:
+        pre.append(pre[-1] + cost(c, y))
+    left = pre[-1]
+    # water-filling: the level T at which the ranks below it absorb exactly
+    # the left-over work (ranks whose whole cameras exceed T get no rows)
+    lv = sorted(whole)
+    T, acc_w = lv[-1] + left / world, 0.0
+    for j, w in enumerate(lv):
+        acc_w += w
+        t = (acc_w + left) / (j + 1)
+        if j + 1 == world or t <= lv[j + 1]:
+            T = t
+            break
+    need = [max(0.0, T - w) for w in whole]
+    tot_need = sum(need)
+    need = [n * left / tot_need for n in need] if tot_need > 0 else [left / world] * world
+    # run k ends where the cumulative cost comes closest to the cumulative need
+    bounds, acc, i = [0], 0.0, 0
+    for k in range(world - 1):
+        acc += need[k]
+        while i < len(seq) and abs(pre[i + 1] - acc) <= abs(pre[i] - acc):
+            i += 1
+        i = max(i, bounds[-1])
+        bounds.append(i)
+    bounds.append(len(seq))
+    mine = seq[bounds[rank]:bounds[rank + 1]]
+    for c in range(q * world, n_cams):
+        ys = [y for cc, y in mine if cc == c]
+        if ys:
+            out.append((c, (0, ys[0], grid_x, ys[-1] + 1)))
     return out
 
 

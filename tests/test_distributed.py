@@ -296,7 +296,7 @@ def test_bucket_unbinds_parameters_no_rank_reached():
 def test_shard_camera_windows_partition_every_camera(n_cams, world, gx, gy):
     """Image sharding of the rig: every camera's tile grid is covered exactly
     once over the ranks, whole cameras go c mod N, and the ranks' pixel
-    shares differ by at most one band of tile rows per left-over camera."""
+    shares differ by at most one tile row."""
     from dynamic3dgaussians_amd.distributed import shard_camera_windows
     cover = {c: [[0] * gx for _ in range(gy)] for c in range(n_cams)}
     load = []
@@ -314,8 +314,44 @@ def test_shard_camera_windows_partition_every_camera(n_cams, world, gx, gy):
                 assert c % world == r
         load.append(px)
     assert all(v == 1 for c in cover for row in cover[c] for v in row)
-    left = n_cams % world
-    assert max(load) - min(load) <= left * gx * (gy // world + 1)
+    assert max(load) - min(load) <= gx
+
+
+@pytest.mark.parametrize("n_cams,world,gy,seed", [(27, 8, 50, 0), (27, 8, 50, 1), (19, 4, 30, 2), (5, 8, 12, 3)])
+def test_shard_camera_windows_balances_row_costs(n_cams, world, gy, seed):
+    """With per-row work (row_cost) the left-over cameras' rows are cut so
+    every rank's total work is the mean to within one row's cost -- except
+    ranks whose whole cameras alone exceed the mean, which get no rows --
+    and every camera is still covered exactly once."""
+    from dynamic3dgaussians_amd.distributed import shard_camera_windows
+    rng = np.random.default_rng(seed)
+    gx = 7
+    cost = rng.gamma(2.0, 1.0, (n_cams, gy)) * rng.uniform(0.5, 1.5, (n_cams, 1))
+    cover = np.zeros((n_cams, gy), int)
+    tot = []
+    for r in range(world):
+        t = 0.0
+        for c, w in shard_camera_windows(n_cams, r, world, gx, gy, row_cost=cost):
+            y0, y1 = (0, gy) if w is None else (w[1], w[3])
+            if w is not None:
+                assert (w[0], w[2]) == (0, gx)
+            cover[c, y0:y1] += 1
+            t += cost[c, y0:y1].sum()
+        tot.append(t)
+    assert (cover == 1).all()
+    q = n_cams // world
+    whole = np.array([cost[[c for c in range(q * world) if c % world == k]].sum() for k in range(world)])
+    left = cost[q * world:].sum()
+    lo, hi = whole.min(), whole.max() + left  # the balanced level: sum max(0, T - whole) = left
+    for _ in range(200):
+        T = 0.5 * (lo + hi)
+        lo, hi = (T, hi) if np.maximum(0.0, T - whole).sum() < left else (lo, T)
+    for k in range(world):
+        if whole[k] < T - cost.max():
+            assert abs(tot[k] - T) <= cost.max() * 1.0001 + 1e-6, (k, tot[k], T)
+        else:
+            assert tot[k] <= max(whole[k], T) + cost.max() * 1.0001 + 1e-6, (k, tot[k], T)
+    assert max(tot) <= max(whole.max(), T) + cost.max() * 1.0001 + 1e-6
 
 
 def _async_worker(rank, world, port, q):
