@@ -189,7 +189,12 @@ def split_shard(n_cams, rank, world, how, W, H, row_cost=None):
     n_cams rig (--split; windows balanced by `row_cost`, rig_row_costs)."""
     if how == "cameras":
         return [(c, None) for c in shard_cameras(n_cams, rank, world)]
-    return shard_camera_windows(n_cams, rank, world, (W + 15) // 16, (H + 15) // 16, row_cost=row_cost)
+    # one more camera piece costs a rank its projection and binning launches:
+    # about a fifth of a camera's work at the bench scene (per-rank proxies,
+    # DESIGN.md 6.2)
+    piece = 0.0 if row_cost is None else 0.2 * sum(sum(r) for r in row_cost) / len(row_cost)
+    return shard_camera_windows(n_cams, rank, world, (W + 15) // 16, (H + 15) // 16, row_cost=row_cost,
+                                piece_cost=piece)
 
 
 def rig_row_costs(rig, params, label, args, dev):

@@ -23,7 +23,7 @@ def shard_cameras(n_cams: int, rank: int, world: int) -> List[int]:
 
 
 def shard_camera_windows(n_cams: int, rank: int, world: int, grid_x: int, grid_y: int,
-                         row_cost: Optional[Sequence[Sequence[float]]] = None
+                         row_cost: Optional[Sequence[Sequence[float]]] = None, piece_cost: float = 0.0
                          ) -> List[Tuple[int, Optional[Tuple[int, int, int, int]]]]:
     """Balanced split of an n_cams rig over `world` ranks with image sharding
     (gs_camera tile_*): the first world * (n_cams // world) cameras whole,
@@ -37,7 +37,11 @@ def shard_camera_windows(n_cams: int, rank: int, world: int, grid_x: int, grid_y
     (one or two on the 27-camera rig over 8 ranks), not a band of every
     left-over camera.  `row_cost[c][y]` is the work of camera c's tile row y
     (e.g. its tile-list instances from a previous forward); without it every
-    row of every camera costs the same (the pixel split).  Returns
+    row of every camera costs the same (the pixel split).  `piece_cost`: the
+    fixed work of rendering one more camera (its projection and binning
+    launches, in row_cost units): a rank whose run spans two left-over
+    cameras is charged it and given fewer rows (a few refinement passes).
+    Returns
     [(camera, window or None)], window = (x0, y0, x1, y1) in tiles, rank-major
     deterministic (every rank computes the same cut).  The windows of a camera
     partition its tile grid, so the ranks' gradients sum to the rig's."""
@@ -53,28 +57,41 @@ def shard_camera_windows(n_cams: int, rank: int, world: int, grid_x: int, grid_y
     for c, y in seq:
         pre.append(pre[-1] + cost(c, y))
     left = pre[-1]
-    # water-filling: the level T at which the ranks below it absorb exactly
-    # the left-over work (ranks whose whole cameras exceed T get no rows)
-    lv = sorted(whole)
-    T, acc_w = lv[-1] + left / world, 0.0
-    for j, w in enumerate(lv):
-        acc_w += w
-        t = (acc_w + left) / (j + 1)
-        if j + 1 == world or t <= lv[j + 1]:
-            T = t
+
+    def cut(base):
+        # water-filling: the level T at which the ranks below it absorb
+        # exactly the left-over work (ranks already above T get no rows)
+        lv = sorted(base)
+        T, acc_w = lv[-1] + left / world, 0.0
+        for j, w in enumerate(lv):
+            acc_w += w
+            t = (acc_w + left) / (j + 1)
+            if j + 1 == world or t <= lv[j + 1]:
+                T = t
+                break
+        need = [max(0.0, T - w) for w in base]
+        tot_need = sum(need)
+        need = [n * left / tot_need for n in need] if tot_need > 0 else [left / world] * world
+        # run k ends where the cumulative cost comes closest to the cumulative need
+        bounds, acc, i = [0], 0.0, 0
+        for k in range(world - 1):
+            acc += need[k]
+            while i < len(seq) and abs(pre[i + 1] - acc) <= abs(pre[i] - acc):
+                i += 1
+            i = max(i, bounds[-1])
+            bounds.append(i)
+        bounds.append(len(seq))
+        return bounds
+
+    def pieces(bounds, k):
+        return len({c for c, _ in seq[bounds[k]:bounds[k + 1]]})
+
+    bounds = cut(whole)
+    for _ in range(4 if piece_cost > 0 else 0):
+        nb = cut([w + piece_cost * pieces(bounds, k) for k, w in enumerate(whole)])
+        if nb == bounds:
             break
-    need = [max(0.0, T - w) for w in whole]
-    tot_need = sum(need)
-    need = [n * left / tot_need for n in need] if tot_need > 0 else [left / world] * world
-    # run k ends where the cumulative cost comes closest to the cumulative need
-    bounds, acc, i = [0], 0.0, 0
-    for k in range(world - 1):
-        acc += need[k]
-        while i < len(seq) and abs(pre[i + 1] - acc) <= abs(pre[i] - acc):
-            i += 1
-        i = max(i, bounds[-1])
-        bounds.append(i)
-    bounds.append(len(seq))
+        bounds = nb
     mine = seq[bounds[rank]:bounds[rank + 1]]
     for c in range(q * world, n_cams):
         ys = [y for cc, y in mine if cc == c]

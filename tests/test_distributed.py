@@ -352,6 +352,14 @@ def test_shard_camera_windows_balances_row_costs(n_cams, world, gy, seed):
         else:
             assert tot[k] <= max(whole[k], T) + cost.max() * 1.0001 + 1e-6, (k, tot[k], T)
     assert max(tot) <= max(whole.max(), T) + cost.max() * 1.0001 + 1e-6
+    # a fixed per-piece cost (ranks whose run spans two cameras get fewer
+    # rows) keeps the partition
+    cover[:] = 0
+    for r in range(world):
+        sh = shard_camera_windows(n_cams, r, world, gx, gy, row_cost=cost, piece_cost=cost.sum(1).mean() * 0.2)
+        for c, w in sh:
+            cover[c, (0 if w is None else w[1]):(gy if w is None else w[3])] += 1
+    assert (cover == 1).all()
 
 
 def _async_worker(rank, world, port, q):
