@@ -28,12 +28,12 @@ Scaling (headline: weak): every rank renders its own 27 cameras of a 27*N
 camera rig with the full Gaussian set replicated; value = all ranks' pixels /
 step time.  `--cams-total T` makes the headline the north star's step split
 across the ranks instead (BASELINE.json configs[3], strong scaling): ONE rig
-of T cameras split over the ranks (--split cameras, the default: camera c on
-rank c mod N, distributed.shard_cameras; --split windows: the first
+of T cameras split over the ranks (--split windows, the default: the first
 N * (T // N) cameras whole, c mod N, the T % N left over cut into bands of
 tile rows that even out the ranks' work (tile-list instances per row from
-a probe forward of the rig) -- image sharding, gs_camera tile_*,
-distributed.shard_camera_windows), each rank
+a probe forward of the rig, a fixed cost per extra camera piece) -- image
+sharding, gs_camera tile_*, distributed.shard_camera_windows, DESIGN.md 6.2;
+--split cameras: camera c on rank c mod N, distributed.shard_cameras), each rank
 renders its share as one batch, then the gradient all-reduce and Adam;
 value = T cameras' pixels / step time.  At N > 1 the weak headline is
 followed by the same measurement of the 27-camera split step, reported as
@@ -87,9 +87,9 @@ def parse():
     ap.add_argument("--cams", type=int, default=27, help="cameras per rank per step (weak scaling)")
     ap.add_argument("--cams-total", type=int, default=0,
                     help="strong scaling: one rig of this many cameras split over the ranks (see --split)")
-    ap.add_argument("--split", default="cameras", choices=["cameras", "windows"],
-                    help="strong-scaling split: balanced with image sharding of the left-over cameras "
-                         "(windows) or whole cameras c mod N (cameras)")
+    ap.add_argument("--split", default="windows", choices=["cameras", "windows"],
+                    help="strong-scaling split: work-balanced with image sharding of the left-over cameras "
+                         "(windows, the default) or whole cameras c mod N (cameras)")
     ap.add_argument("--proxy-world", type=int, default=0,
                     help="one GPU standing in for rank --proxy-rank of an N-rank --cams-total split: the "
                          "rank's own cameras and windows, no collective (the per-rank shape)")
