@@ -43,7 +43,7 @@ def test_committed_counts_give_possible_fractions(stage):
     with open(os.path.join(REPO, "profiles", "pmc_traffic.json")) as f:
         wl = json.load(f)["workload"]
     pmc = bench.pmc_for(wl)
-    with open(os.path.join(REPO, "profiles", "r04s", "bench.json")) as f:
+    with open(os.path.join(REPO, "profiles", "r04y", "bench.json")) as f:
         line = json.load(f)
     ms = line["stages_ms_per_step"][stage]
     cams = wl["cams_per_launch"]
@@ -65,7 +65,7 @@ def test_committed_bench_line_has_no_fraction_above_one():
                 if k.endswith("frac") and isinstance(v, (int, float)):
                     yield k, v
                 yield from fracs(v)
-    for path in ("r04m/bench.json", "r04m/bench_under_rocprof.json", "r04s/bench.json", "r04s/bench_under_rocprof.json"):
+    for path in ("r04m/bench.json", "r04m/bench_under_rocprof.json", "r04s/bench.json", "r04s/bench_under_rocprof.json", "r04y/bench.json", "r04y/bench_under_rocprof.json"):
         with open(os.path.join(REPO, "profiles", path)) as f:
             line = json.load(f)
         for k, v in fracs(line["roofline"]):
