@@ -16,6 +16,11 @@ from dynamic3dgaussians_amd.camera import setup_camera
 from dynamic3dgaussians_amd.timesteps import params2rendervar
 from oracle import neighbor as onb
 
+# torch's CPU elementwise kernels (exp, sqrt, division) dispatch on the host's
+# vector ISA (AVX2 / AVX512), so results are bit-equal to the fixture only on
+# a host of the fixture's ISA; across hosts they agree to a couple of ulp.
+ULP2 = dict(rtol=2.5e-7, atol=0)
+
 G = np.load(os.path.join(os.path.dirname(__file__), "golden", "train_helpers.npz"))
 
 
@@ -32,12 +37,13 @@ def test_setup_camera_matches_helpers_setup_camera():
         assert c.c_x == float(G["cam_c_x"][i]) and c.c_y == float(G["cam_c_y"][i])
 
 
-def test_params2rendervar_matches_helpers_bit_for_bit():
-    """helpers.py:98-107 on the CPU: normalise / sigmoid / exp."""
+def test_params2rendervar_matches_helpers():
+    """helpers.py:98-107 on the CPU: normalise / sigmoid / exp (the same torch
+    ops, so bit-equal on a host of the fixture's ISA; within 2 ulp on any)."""
     params = {k[2:]: torch.from_numpy(G[k]) for k in G.files if k.startswith("p_")}
     rv = params2rendervar(params)
     for k in ("rotations", "opacities", "scales"):
-        assert torch.equal(rv[k], torch.from_numpy(G[f"rv_{k}"])), k
+        torch.testing.assert_close(rv[k], torch.from_numpy(G[f"rv_{k}"]), **ULP2, msg=k)
 
 
 def test_losses_and_psnr_match_reference():
@@ -62,11 +68,14 @@ def test_neighbour_loss_oracle_matches_reference_composition():
                  "prev_inv_rot_fg": torch.from_numpy(G["nb_prev_inv_rot"]),
                  "prev_offset": torch.from_numpy(G["nb_prev_offset"]),
                  "neighbor_dist": torch.from_numpy(G["nb_dist"])}
-    assert torch.equal(onb._quat_mult(fg_rot, variables["prev_inv_rot_fg"]), torch.from_numpy(G["nb_rel_rot"]))
-    assert torch.equal(onb._build_rotation(torch.from_numpy(G["nb_rel_rot"])), torch.from_numpy(G["nb_rot"]))
+    torch.testing.assert_close(onb._quat_mult(fg_rot, variables["prev_inv_rot_fg"]),
+                               torch.from_numpy(G["nb_rel_rot"]), **ULP2)
+    # build_rotation divides by a sqrt: 2 ulp of the entries' magnitude (<= 1)
+    torch.testing.assert_close(onb._build_rotation(torch.from_numpy(G["nb_rel_rot"])),
+                               torch.from_numpy(G["nb_rot"]), rtol=0, atol=5e-7)
     rigid, rot, iso = onb.torch_reference(fg_pts, fg_rot, variables)
     for got, key in ((rigid, "nb_rigid"), (rot, "nb_rot_loss"), (iso, "nb_iso")):
-        assert got.item() == float(G[key]), (key, got.item(), float(G[key]))
+        assert abs(got.item() - float(G[key])) <= 1e-6 * abs(float(G[key])), (key, got.item(), float(G[key]))
     r64 = onb.numpy_losses(G["nb_fg_pts"], G["nb_fg_rot"], G["nb_indices"], G["nb_weight"], G["nb_dist"],
                            G["nb_prev_offset"], G["nb_prev_inv_rot"])
     for got, key in zip(r64, ("nb_rigid", "nb_rot_loss", "nb_iso")):
