@@ -422,7 +422,8 @@ __global__ __launch_bounds__(64 * WPB_FWD) __attribute__((amdgpu_waves_per_eu(fw
   __shared__ float s_fw[WPB_FWD][MF ? WBF + 1 : 1][68];  // +1: a pair may overfill by one
 
   // strip item = tile slot * 4 + strip (the tile slot in dispatch order)
-  const int lane = threadIdx.x & 63, lw = threadIdx.x >> 6;  // lw: LDS slot of the wave
+  // lw: LDS slot of the wave (a constant 0 at one wave per workgroup)
+  const int lane = threadIdx.x & 63, lw = WPB_FWD == 1 ? 0 : (int)(threadIdx.x >> 6);
   const int item = item0 + lw;
   const uint4 trec = tile_rec(order, item >> 2);
   const int tile = (int)trec.x, wave = item & 3;
@@ -846,9 +847,9 @@ __global__ __launch_bounds__(64 * WPB_BWD) __attribute__((amdgpu_waves_per_eu(bw
   // (F = 36: the host hands a 48-wide scratch, feature_grad_rows copies out)
   constexpr int FS = feature_grad_stride(F);
   constexpr bool FIXED_FEAT = (COMPAT != COMPAT_REFERENCE) && F > 0;
-  // per record: (x, y, -a/2, -b) (-c/2, opacity, r, g) (b, depth, -, -)
-  __shared__ float4 s_rec[WPB_BWD][CHUNK][2];
-  __shared__ float2 s_rec2[WPB_BWD][CHUNK];  // (b, depth)
+  // per record: (x, y, -a/2, -b) (-c/2, opacity, r, g) (b, depth, -, -): one
+  // 48-B row, so a survivor's three reads share one address register
+  __shared__ float4 s_rec[WPB_BWD][CHUNK][3];
   // Colour block operand rows 0..3 (dL/dC_r,g,b, dL/dD) and the FW <= 4
   // feature rows after them, split, in the A layout: [k-step][piece][row]
   // [pixel group of 8].  Kept in LDS (1.5 / 3 KiB) rather than in 24 VGPRs:
@@ -857,15 +858,17 @@ __global__ __launch_bounds__(64 * WPB_BWD) __attribute__((amdgpu_waves_per_eu(bw
   constexpr bool XW_LDS = (FW <= 4);
   constexpr int XR = FW == 0 ? 4 : 8;  // operand rows kept
   __shared__ bf16x8 s_xw[WPB_BWD][XW_LDS ? 2 : 1][NSP][XR][4];
-  // batch weights [slot][pixel]: 64-float rows, 16-B groups XOR-swizzled by
-  // the row (sw_idx) so that the flush's 16-row operand reads and the
-  // per-lane writes are both conflict-free without padding
-  __shared__ float s_w[WPB_BWD][WB * 64];
-  __shared__ float s_u[WPB_BWD][WB * 64];
-  __shared__ float4 s_slot[WPB_BWD][WB];  // (mean x - cx, mean y - cy, opacity, id bits)
+  // batch weights w ([0]) and u ([1]) as [slot][pixel]: 64-float rows, 16-B
+  // groups XOR-swizzled by the row (sw_idx) so that the flush's 16-row operand
+  // reads and the per-lane writes are both conflict-free without padding; one
+  // array, so the u row is the w row's address plus an immediate offset
+  __shared__ float s_wu[WPB_BWD][2][WB * 64];
+  __shared__ float4 s_slot[WPB_BWD][WB];  // (mean x, mean y, opacity, id bits)
 
   // strip item = tile slot * 4 + strip (the tile slot in dispatch order)
-  const int lane = threadIdx.x & 63, lw = threadIdx.x >> 6;  // lw: LDS slot of the wave
+  // lw: LDS slot of the wave (a constant 0 at one wave per workgroup, so LDS
+  // addresses are offsets from scalars rather than from a per-wave register)
+  const int lane = threadIdx.x & 63, lw = WPB_BWD == 1 ? 0 : (int)(threadIdx.x >> 6);
   const int item = strip_item(bslot, WPB_BWD) + lw;
   const uint4 trec = tile_rec(order, item >> 2);
   const int tile = (int)trec.x, wave = item & 3;
@@ -1039,8 +1042,8 @@ __global__ __launch_bounds__(64 * WPB_BWD) __attribute__((amdgpu_waves_per_eu(bw
         bsplit Ws;
         {
           float x[8];
-          const float4 a0 = *reinterpret_cast<const float4*>(&s_w[lw][sw_idx(g, p0)]);
-          const float4 a1 = *reinterpret_cast<const float4*>(&s_w[lw][sw_idx(g, p0 + 4)]);
+          const float4 a0 = *reinterpret_cast<const float4*>(&s_wu[lw][0][sw_idx(g, p0)]);
+          const float4 a1 = *reinterpret_cast<const float4*>(&s_wu[lw][0][sw_idx(g, p0 + 4)]);
           x[0] = a0.x; x[1] = a0.y; x[2] = a0.z; x[3] = a0.w; x[4] = a1.x; x[5] = a1.y; x[6] = a1.z; x[7] = a1.w;
           split_bf16(x, Ws);
         }
@@ -1061,8 +1064,8 @@ __global__ __launch_bounds__(64 * WPB_BWD) __attribute__((amdgpu_waves_per_eu(bw
       bsplit Us;
       {
         float y[8];
-        const float4 b0 = *reinterpret_cast<const float4*>(&s_u[lw][sw_idx(g, p0)]);
-        const float4 b1 = *reinterpret_cast<const float4*>(&s_u[lw][sw_idx(g, p0 + 4)]);
+        const float4 b0 = *reinterpret_cast<const float4*>(&s_wu[lw][1][sw_idx(g, p0)]);
+        const float4 b1 = *reinterpret_cast<const float4*>(&s_wu[lw][1][sw_idx(g, p0 + 4)]);
         y[0] = b0.x; y[1] = b0.y; y[2] = b0.z; y[3] = b0.w; y[4] = b1.x; y[5] = b1.y; y[6] = b1.z; y[7] = b1.w;
         split_bf16(y, Us);
       }
@@ -1102,10 +1105,10 @@ __global__ __launch_bounds__(64 * WPB_BWD) __attribute__((amdgpu_waves_per_eu(bw
     // along as components A_FEAT.. (their target is the feature gradient row,
     // FW contiguous floats: one request per Gaussian instead of one per
     // channel).
-    float* s_out = &s_u[lw][0];
+    float* s_out = &s_wu[lw][1][0];
     if (lane < 16) {
       const float4 sl = s_slot[lw][lane];
-      const float mx = sl.x, my = sl.y, op = sl.z;
+      const float mx = sl.x - cx, my = sl.y - cy, op = sl.z;
       const float S1 = cu[0], Sx = cu[1], Sy = cu[2], Sxx = cu[3];
       // sum u dx = m' S1 - Sx/2, sum u dx^2 = m'^2 S1 - m' Sx + Sxx/4, ...
       const float ux = fmaf(mx, S1, -0.5f * Sx), uy = fmaf(my, S1, -0.5f * Sy);
@@ -1208,11 +1211,12 @@ __global__ __launch_bounds__(64 * WPB_BWD) __attribute__((amdgpu_waves_per_eu(bw
       const float4 h = half_conic(q.q0, q.q1);
       s_rec[lw][lane][0] = make_float4(q.q0.x, q.q0.y, h.x, h.y);
       s_rec[lw][lane][1] = make_float4(h.z, q.q1.y, q.q1.z, q.q1.w);
-      s_rec2[lw][lane] = q.q2;
+      s_rec[lw][lane][2] = make_float4(q.q2.x, q.q2.y, 0.f, 0.f);
     }
     const uint32_t chunk_gid = q.gid;  // lane j: id of the chunk's j-th record
     // chunk entry j is in front of this pixel's last contributor iff j < lrel
-    const int lrel = (int)last - (int)(c0 - range.x);
+    int lrel = (int)last - (int)(c0 - range.x);
+    asm volatile("" : "+v"(lrel));  // kept in a register, not recomputed per survivor
     uint64_t mask = __ballot(keep);
     STAT(8, 1);
     STAT(9, hi - c0);
@@ -1226,9 +1230,11 @@ __global__ __launch_bounds__(64 * WPB_BWD) __attribute__((amdgpu_waves_per_eu(bw
     while (mask) {
       const int j = 63 - __builtin_clzll(mask);
       mask &= ~(1ull << j);
+      // all three fields read up front from one row address (r2 is only used
+      // by blending survivors, but a separate read would need its own address)
       const float4 r0 = s_rec[lw][j][0];
       const float4 r1 = s_rec[lw][j][1];
-      const float2 r2 = s_rec2[lw][j];
+      const float2 r2 = *reinterpret_cast<const float2*>(&s_rec[lw][j][2]);
       const float dx = r0.x - pfx, dy = r0.y - pfy;
       const float op = r1.y;
       const float power = gauss_power(dx, dy, make_float4(r0.z, r0.w, r1.x, 0.f));
@@ -1239,6 +1245,9 @@ __global__ __launch_bounds__(64 * WPB_BWD) __attribute__((amdgpu_waves_per_eu(bw
       STAT_INC(st_it);
       STAT(12, wave_any(valid));
       STAT(13, __builtin_popcountll(__ballot(valid)));
+      // r2 read with r0 / r1 (not sunk into the branch below, where its own
+      // address would cost a vector instruction)
+      asm volatile("" ::"v"(r2.x), "v"(r2.y));
       if (!wave_any(valid)) continue;
       // Invalid lanes park w = u = 0, which zeroes their contributions.
       float w = 0.f, u = 0.f;
@@ -1262,10 +1271,26 @@ __global__ __launch_bounds__(64 * WPB_BWD) __attribute__((amdgpu_waves_per_eu(bw
         la = alpha;
         u = G * dL_dopa;
       }
-      s_w[lw][sw_idx(nb, lane)] = w;
-      s_u[lw][sw_idx(nb, lane)] = u;
-      if (lane == 0)
-        s_slot[lw][nb] = make_float4(r0.x - cx, r0.y - cy, op, bits_f(__builtin_amdgcn_readlane(chunk_gid, j)));
+      {
+        // sw_idx(nb, lane) in bytes is ((4 lane) ^ (nb << 4)) + 256 nb (nb < 16):
+        // one v_xad_u32 for both rows instead of four address instructions
+        char* const wu = reinterpret_cast<char*>(&s_wu[lw][0][0]);
+        const uint32_t off = (((uint32_t)lane << 2) ^ ((uint32_t)nb << 4)) + ((uint32_t)nb << 8);
+        *reinterpret_cast<float*>(wu + off) = w;
+        *reinterpret_cast<float*>(wu + off + WB * 64 * 4) = u;
+      }
+      // the slot record from lane j, which holds the record's id: no
+      // readlane, and the centring on the strip is left to the flush
+      if (lane == j) {
+        // three stores straight from the registers the fields sit in (one
+        // 16-B store would need them moved into four consecutive registers)
+        float* const sl = reinterpret_cast<float*>(&s_slot[lw][nb]);
+        *reinterpret_cast<float2*>(sl) = make_float2(r0.x, r0.y);
+        asm volatile("" ::: "memory");
+        sl[2] = op;
+        asm volatile("" ::: "memory");
+        sl[3] = bits_f(chunk_gid);
+      }
       if (++nb == WB) {
         flush(WB);
         nb = 0;
