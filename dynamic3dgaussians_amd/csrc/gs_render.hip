@@ -420,6 +420,7 @@ __global__ __launch_bounds__(64 * WPB_FWD) __attribute__((amdgpu_waves_per_eu(fw
   __shared__ float4 s_rec[WPB_FWD][CHUNK][3];
   // batch weights [slot][pixel] (row pad 4: conflict-free writes and reads)
   __shared__ float s_fw[WPB_FWD][MF ? WBF + 1 : 1][68];  // +1: a pair may overfill by one
+  __shared__ __attribute__((aligned(16))) uint32_t s_gid[WPB_FWD][MF ? WBF + 4 : 1];  // batch ids (+ the overfill)
 
   // strip item = tile slot * 4 + strip (the tile slot in dispatch order)
   // lw: LDS slot of the wave (a constant 0 at one wave per workgroup)
@@ -465,15 +466,20 @@ __global__ __launch_bounds__(64 * WPB_FWD) __attribute__((amdgpu_waves_per_eu(fw
   // that it lives in a VGPR instead of exec-mask bookkeeping across the loops
   uint32_t live = inside ? 1u : 0u;
   int nb = 0;          // batch fill
-  uint32_t gidv = 0;   // lane k < nb: id of the batch's k-th Gaussian
 
   // Contract the batch's nb Gaussians.  A[ch][k] = feat[gid_k][32 fb + ch]
   // (lane l: channel l&31, k = 8(l>>5) + j), B[k][pix] = w[k][pix] (lane l:
   // pixel (l&31) + 32 blk); slots k >= nb are zeroed on both sides.
-  // Park Gaussian g's feature rows as batch slot k: remember the id for the
-  // flush's gather.  (Copying the rows to LDS by LDS-DMA at park time was
-  // measured slower: DESIGN.md section 4.)
-  auto park_row = [&](uint32_t g, int k) { gidv = lane == k ? g : gidv; };
+  // Park record j's Gaussian as batch slot k: the lane holding the chunk's
+  // j-th id stores it to the batch's id row, which the flush reads back with
+  // two broadcast 16-B reads per lane (instead of a readlane and a lane
+  // select per park and 8 lane shuffles per flush).  (Copying the feature
+  // rows to LDS by LDS-DMA at park time was measured slower: DESIGN.md
+  // section 4.)
+  if (MF && lane < WBF + 4) s_gid[lw][lane] = 0u;  // stale slots gather row 0
+  auto park_row = [&](uint32_t chunk_gid, int j, int k) {
+    if (lane == j) s_gid[lw][k] = chunk_gid;
+  };
   // feature rows addressed by unsigned 32-bit byte offsets through a buffer
   // resource over the P x F table (the host refuses tables over 4 GiB): 64-bit
   // pointer arithmetic per row cost 3 more vector instructions per row and
@@ -497,10 +503,13 @@ __global__ __launch_bounds__(64 * WPB_FWD) __attribute__((amdgpu_waves_per_eu(fw
         float fa[8];
         // 32-bit row offsets through a buffer resource: one address
         // instruction per row instead of 64-bit pointer arithmetic
+        const uint4 ga = *reinterpret_cast<const uint4*>(&s_gid[lw][8 * h]);
+        const uint4 gb = *reinterpret_cast<const uint4*>(&s_gid[lw][8 * h + 4]);
+        const uint32_t gk[8] = {ga.x, ga.y, ga.z, ga.w, gb.x, gb.y, gb.z, gb.w};
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int k = 8 * h + j;
-          const uint32_t g = (uint32_t)__shfl((int)gidv, k, 64);
+          const uint32_t g = gk[j];
           const uint32_t off = (g * (uint32_t)F + (uint32_t)(fb * 32 + (ln & 31))) * 4u;
           const float v = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(frsrc, (int)off, 0, 0));
           fa[j] = k < n ? v : 0.f;
@@ -582,7 +591,7 @@ __global__ __launch_bounds__(64 * WPB_FWD) __attribute__((amdgpu_waves_per_eu(fw
         if constexpr (MF) {
           if (wave_any(blend)) {  // park it; the batch is flushed after the pair
             s_fw[lw][nb][lane] = w;  // 0 on non-blending lanes
-            park_row(__builtin_amdgcn_readlane(chunk_gid, j), nb);
+            park_row(chunk_gid, j, nb);
             ++nb;
           }
         }
@@ -617,8 +626,7 @@ __global__ __launch_bounds__(64 * WPB_FWD) __attribute__((amdgpu_waves_per_eu(fw
             flush(WBF);
             if (nb > WBF) {
               s_fw[lw][0][lane] = s_fw[lw][WBF][lane];
-              const uint32_t g16 = __builtin_amdgcn_readlane(gidv, WBF);
-              gidv = lane == 0 ? g16 : gidv;
+              if (lane == 0) s_gid[lw][0] = s_gid[lw][WBF];
             }
             nb -= WBF;
           }
@@ -675,7 +683,7 @@ __global__ __launch_bounds__(64 * WPB_FWD) __attribute__((amdgpu_waves_per_eu(fw
       if (F > 0 && wave_any(blend)) {
         if constexpr (MF) {
           s_fw[lw][nb][lane] = w;  // 0 on non-blending lanes
-          park_row(__builtin_amdgcn_readlane(chunk_gid, j), nb);
+          park_row(chunk_gid, j, nb);
           if (++nb == WBF) {
             flush(WBF);
             nb = 0;
