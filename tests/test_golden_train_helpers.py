@@ -49,9 +49,12 @@ def test_params2rendervar_matches_helpers():
 def test_losses_and_psnr_match_reference():
     from bench import calc_psnr
     x, y, w = (torch.from_numpy(G[k]) for k in ("loss_x", "loss_y", "loss_w"))
-    assert torch.abs(x - y).mean().item() == float(G["l1_v1"])          # helpers.py:110-111
-    assert onb._wl2_v1(x, y, w).item() == float(G["wl2_v1"])            # helpers.py:117-118
-    assert onb._wl2_v2(x, y, w[:, 0]).item() == float(G["wl2_v2"])      # helpers.py:121-122
+    # reductions: bit-equal on the fixture's host ISA, 1e-6 relative on any
+    def close(got, key):
+        return abs(got - float(G[key])) <= 1e-6 * abs(float(G[key]))
+    assert close(torch.abs(x - y).mean().item(), "l1_v1")          # helpers.py:110-111
+    assert close(onb._wl2_v1(x, y, w).item(), "wl2_v1")            # helpers.py:117-118
+    assert close(onb._wl2_v2(x, y, w[:, 0]).item(), "wl2_v2")      # helpers.py:121-122
     # bench.py's PSNR: external.py:85-87 per channel, averaged over the channels
     ref = np.asarray(G["psnr"], np.float64).reshape(-1)
     assert abs(calc_psnr(G["psnr_img1"], G["psnr_img2"]) - ref.mean()) < 1e-4
