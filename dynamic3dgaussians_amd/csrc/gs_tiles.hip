@@ -468,7 +468,8 @@ __device__ inline uint64_t match_digit8(uint32_t d, uint64_t valid) {
 // Bucket bits of the MSD sort: 2^10 buckets, 2^11 for the longer length
 // classes of long-tile scenes (tile_sort_launches).
 constexpr int BS_BITS = 10, BS_BITS_LONG = 11;
-constexpr int BS_KPT = 8;  // keys per thread held in registers
+constexpr int BS_KPT = 8;       // keys per thread held in registers (up to 8 NT keys per tile)
+constexpr int BS_KPT_LONG = 16;  // for launches whose tiles exceed 8 NT keys
 constexpr int BS_RUN_MAX = 48;  // longest per-thread run handed to the insertion sort
 
 template <int NT, int BINS>
@@ -604,7 +605,7 @@ __device__ __attribute__((always_inline)) KP tile_radix_sort(KP A, KP B, int n, 
 // hold or some thread's run is longer than BS_RUN_MAX (depths crowded into
 // few buckets): the caller then runs the radix sort.
 
-template <int NT, int BITS>
+template <int NT, int BITS, int BS_KPT>
 __device__ __attribute__((always_inline)) bool tile_bucket_sort(const uint64_t* A, uint64_t* B, int n,
                                                                 RadixSmem<NT, (1 << BITS)>& sm) {
   constexpr int BS_BINS = 1 << BITS;
@@ -710,11 +711,15 @@ extern "C" int gs_sort_stats_read(unsigned long long* out) {
 #endif
 
 // One tile per workgroup of NT threads (tiles of length lo < n <= hi; the
-// others exit).  Keys sorted in LDS up to `cap` (the launch's dynamic LDS),
-// in global memory beyond.
-template <int NT, int BITS>
+// others exit).  Keys bucket-sorted in place in LDS up to `cap` (the launch's
+// dynamic LDS: one buffer -- every key is in registers before the scatter
+// writes over the staging copy, so the tile needs cap keys of LDS, not two
+// buffers, and twice the workgroups fit a CU); a tile the bucket sort hands
+// back (crowded depths, or more than KPT keys per thread) and one longer than
+// cap are radix-sorted in global memory.
+template <int NT, int BITS, int KPT>
 __global__ __launch_bounds__(NT) void tile_sort_kernel(TileArgs a0, CamBatch cb, int cap, int lo, int hi, int ofs) {
-  extern __shared__ uint64_t s_key[];  // 2 x cap keys
+  extern __shared__ uint64_t s_key[];  // cap keys
   __shared__ RadixSmem<NT, (1 << BITS)> sm;
   const TileArgs ta = cam_tile_args(a0, cb, blockIdx.y);
   uint64_t* __restrict__ keys = ta.keys;
@@ -732,13 +737,15 @@ __global__ __launch_bounds__(NT) void tile_sort_kernel(TileArgs a0, CamBatch cb,
     for (int i = threadIdx.x; i < n; i += NT) s_key[i] = keys[r.x + i];
     __syncthreads();
     const uint64_t* out;
-    if (tile_bucket_sort<NT, BITS>(s_key, s_key + cap, n, sm)) {
-      out = s_key + cap;
+    if (tile_bucket_sort<NT, BITS, KPT>(s_key, s_key, n, sm)) {
+      out = s_key;
     } else {
 #ifdef GS_STATS
       if (threadIdx.x == 0) atomicAdd(&g_sort_stats[1], 1ull);
 #endif
-      out = tile_radix_sort<uint64_t*, NT, (1 << BITS)>(s_key, s_key + cap, n, sm);
+      // the staging copy is intact (the bucket sort gives up before its
+      // scatter); the radix passes need a second buffer: global memory
+      out = tile_radix_sort<uint64_t*, NT, (1 << BITS)>(keys + r.x, keys2 + r.x, n, sm);
     }
 #ifdef GS_STATS
     if (threadIdx.x == 0) atomicAdd(&g_sort_stats[0], 1ull);
@@ -811,12 +818,21 @@ static void tile_sort_launches(const TileArgs& a, const CamBatch& cb, int64_t ma
   auto launch = [&](int cap, int lo, int hi, int ofs, int n) {
     if (n <= 0) return;
     const dim3 grid(n, cb.C);
-    if (lo == 0 || !long_bits)
-      hipLaunchKernelGGL((tile_sort_kernel<NT, BS_BITS>), grid, block, 2 * sizeof(uint64_t) * (cap > 0 ? cap : 1), s,
-                         a, cb, cap > 0 ? cap : 1, lo, hi, ofs);
-    else
-      hipLaunchKernelGGL((tile_sort_kernel<NT, BS_BITS_LONG>), grid, block,
-                         2 * sizeof(uint64_t) * (cap > 0 ? cap : 1), s, a, cb, cap > 0 ? cap : 1, lo, hi, ofs);
+    const int c = cap > 0 ? cap : 1;
+    const size_t lds = sizeof(uint64_t) * (size_t)c;
+    const bool wide = c > BS_KPT * NT;  // keys per thread of the bucket sort
+    if (lo == 0 || !long_bits) {
+      if (wide)
+        hipLaunchKernelGGL((tile_sort_kernel<NT, BS_BITS, BS_KPT_LONG>), grid, block, lds, s, a, cb, c, lo, hi, ofs);
+      else
+        hipLaunchKernelGGL((tile_sort_kernel<NT, BS_BITS, BS_KPT>), grid, block, lds, s, a, cb, c, lo, hi, ofs);
+    } else {
+      if (wide)
+        hipLaunchKernelGGL((tile_sort_kernel<NT, BS_BITS_LONG, BS_KPT_LONG>), grid, block, lds, s, a, cb, c, lo, hi,
+                           ofs);
+      else
+        hipLaunchKernelGGL((tile_sort_kernel<NT, BS_BITS_LONG, BS_KPT>), grid, block, lds, s, a, cb, c, lo, hi, ofs);
+    }
   };
   const int T = a.num_tiles;
   if (max_len < 0) {  // unknown lengths: the LDS classes and the global-memory class
