@@ -469,7 +469,7 @@ __device__ inline uint64_t match_digit8(uint32_t d, uint64_t valid) {
 // classes of long-tile scenes (tile_sort_launches).
 constexpr int BS_BITS = 10, BS_BITS_LONG = 11;
 constexpr int BS_KPT = 8;       // keys per thread held in registers (up to 8 NT keys per tile)
-constexpr int BS_KPT_LONG = 16;  // for launches whose tiles exceed 8 NT keys
+constexpr int BS_KPT_LONG = 16;  // for launches whose tiles exceed 8 NT keys (20 / 24 measured slower)
 constexpr int BS_RUN_MAX = 48;  // longest per-thread run handed to the insertion sort
 
 template <int NT, int BINS>
