@@ -28,14 +28,16 @@
 //     the full key.  Common case, an MSD bucket sort: the top bits of the
 //     tile's depth-bit span pick one of 1,024 buckets (LDS atomics give each
 //     key its slot), one scan, one scatter, then every thread insertion-sorts
-//     its contiguous run of buckets by the full key.  Tiles whose keys crowd
-//     into few buckets fall back to an LSD radix sort (wave-owned quarters,
-//     ballot-matched stable scatter, skipped constant-digit passes, equal
-//     depths ordered by id).  Keys are unique, so either way the list is
-//     exactly the reference's stable order.  Length classes (short / up to
-//     TS_CAP in LDS / up to TS_CAP_LONG in a one-per-CU launch / beyond in
-//     global memory) run as separate launches over their prefix of the
-//     longest-first dispatch order (P1, Q1, P2 in the header).
+//     its contiguous run of buckets by the full key -- in place, in one LDS
+//     buffer (every key sits in registers before the scatter).  Tiles whose
+//     keys crowd into few buckets fall back to an LSD radix sort in global
+//     memory (wave-owned quarters, ballot-matched stable scatter, skipped
+//     constant-digit passes, equal depths ordered by id).  Keys are unique,
+//     so either way the list is exactly the reference's stable order.
+//     Length classes (short / up to TS_CAP / up to TS_CAP_LONG, two
+//     workgroups per CU / beyond in global memory) run as separate launches
+//     over their prefix of the longest-first dispatch order (P1, Q1, P2 in
+//     the header).
 // Integer work, HBM- and latency-bound; 5 launches instead of the
 // reference's scan + 6-pass 64-bit radix sort + ranges.
 #include "gs_common.h"
@@ -802,7 +804,9 @@ void launch_tile_bucket(const TileArgs& a, const CamBatch& cb, hipStream_t s) {
 // ~660 keys on the bench camera) get their own launch with small LDS and many
 // workgroups per CU, the long ones follow with LDS for their length (and
 // global memory beyond TS_CAP_LONG).  Bench batch (27 cameras): sort 0.94 ->
-// 0.80 ms per step with the small class at 1024 keys.
+// 0.80 ms per step with the small class at 1024 keys; one in-place buffer
+// instead of two (twice the long-class workgroups per CU): 0.52 -> 0.47 ms,
+// configs[4] 0.82 -> 0.51 ms with the LDS class up to 4096 keys.
 template <int NT>
 static void tile_sort_launches(const TileArgs& a, const CamBatch& cb, int64_t max_len, const SortClasses& sc,
                                hipStream_t s) {
