@@ -28,8 +28,8 @@
 //     the full key.  Common case, an MSD bucket sort: the top bits of the
 //     tile's depth-bit span pick one of 1,024 buckets (LDS atomics give each
 //     key its slot), one scan, one scatter, then every thread insertion-sorts
-//     its contiguous run of buckets by the full key -- in place, in one LDS
-//     buffer (every key sits in registers before the scatter).  Tiles whose
+//     its contiguous run of buckets by the full key -- the keys go from
+//     global memory to registers to one LDS buffer (the scatter target).  Tiles whose
 //     keys crowd into few buckets fall back to an LSD radix sort in global
 //     memory (wave-owned quarters, ballot-matched stable scatter, skipped
 //     constant-digit passes, equal depths ordered by id).  Keys are unique,
@@ -713,12 +713,12 @@ extern "C" int gs_sort_stats_read(unsigned long long* out) {
 #endif
 
 // One tile per workgroup of NT threads (tiles of length lo < n <= hi; the
-// others exit).  Keys bucket-sorted in place in LDS up to `cap` (the launch's
-// dynamic LDS: one buffer -- every key is in registers before the scatter
-// writes over the staging copy, so the tile needs cap keys of LDS, not two
-// buffers, and twice the workgroups fit a CU); a tile the bucket sort hands
-// back (crowded depths, or more than KPT keys per thread) and one longer than
-// cap are radix-sorted in global memory.
+// others exit).  Keys bucket-sorted up to `cap` (the launch's dynamic LDS):
+// loaded from global memory straight into registers and scattered into one
+// LDS buffer of cap keys, where the insertion sorts run (no staging copy and
+// no second buffer: twice the workgroups per CU of the two-buffer sort); a
+// tile the bucket sort hands back (crowded depths, or more than KPT keys per
+// thread) and one longer than cap are radix-sorted in global memory.
 template <int NT, int BITS, int KPT>
 __global__ __launch_bounds__(NT) void tile_sort_kernel(TileArgs a0, CamBatch cb, int cap, int lo, int hi, int ofs) {
   extern __shared__ uint64_t s_key[];  // cap keys
@@ -736,17 +736,17 @@ __global__ __launch_bounds__(NT) void tile_sort_kernel(TileArgs a0, CamBatch cb,
     return;
   }
   if (n <= cap) {
-    for (int i = threadIdx.x; i < n; i += NT) s_key[i] = keys[r.x + i];
-    __syncthreads();
+    // keys straight from global memory into the bucket sort's registers
+    // (no LDS staging copy: sort 0.457-0.462 vs 0.470-0.471 ms per bench step)
     const uint64_t* out;
-    if (tile_bucket_sort<NT, BITS, KPT>(s_key, s_key, n, sm)) {
+    if (tile_bucket_sort<NT, BITS, KPT>(keys + r.x, s_key, n, sm)) {
       out = s_key;
     } else {
 #ifdef GS_STATS
       if (threadIdx.x == 0) atomicAdd(&g_sort_stats[1], 1ull);
 #endif
-      // the staging copy is intact (the bucket sort gives up before its
-      // scatter); the radix passes need a second buffer: global memory
+      // the keys in global memory are untouched (the bucket sort gives up
+      // before its scatter); the radix passes run there with the twin buffer
       out = tile_radix_sort<uint64_t*, NT, (1 << BITS)>(keys + r.x, keys2 + r.x, n, sm);
     }
 #ifdef GS_STATS
