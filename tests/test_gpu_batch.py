@@ -227,7 +227,7 @@ def test_camera_shards_sum_to_the_full_batch(world, P=15000, W=128, H=96, C=27):
 def test_batch_sort_classes_with_long_and_short_cameras(P=20000, W=160, H=128):
     """The batch merges the cameras' tile-sort class extents (gs_api.hip: max
     of the long-class prefixes, min of the short-class one): a camera with
-    tiles longer than GS_SORT_SMALL (1024) and TS_CAP (3584) next to cameras
+    tiles longer than SORT_SMALL (1024) and TS_CAP (4096) next to cameras
     whose tiles are all short must still sort every list.  A dense cluster of
     Gaussians just in front of camera 0 makes its long tiles; the batch's
     outputs must be bit-identical to the per-camera calls."""
@@ -256,7 +256,7 @@ def test_batch_sort_classes_with_long_and_short_cameras(P=20000, W=160, H=128):
         st = Hh.export_state(P, W, H, out)
         rg = st["ranges"].reshape(-1, 2).astype(np.int64)
         maxlen.append(int((rg[:, 1] - rg[:, 0]).max()))
-    assert maxlen[0] > 3584, maxlen
+    assert maxlen[0] > 4096, maxlen
     assert min(maxlen[1:]) <= 1024, maxlen
     bat = GaussianRasterizerBatch(sets)(means2D=torch.zeros(P, 3, device=DEV), label=label, **src)
     for c in range(len(sets)):
