@@ -799,58 +799,63 @@ void launch_tile_bucket(const TileArgs& a, const CamBatch& cb, hipStream_t s) {
   }
 }
 
+// One class launch of NT-thread workgroups over the dispatch-order positions
+// [ofs, ofs + n) (SortClasses), LDS for `cap` keys, BITS / BITS_LONG bucket
+// bits (lo == 0: the short class).
+template <int NT, bool LONG_BITS>
+static void tile_sort_class(const TileArgs& a, const CamBatch& cb, int cap, int lo, int hi, int ofs, int n,
+                            hipStream_t s) {
+  if (n <= 0) return;
+  const dim3 grid(n, cb.C), block(NT);
+  const int c = cap > 0 ? cap : 1;
+  const size_t lds = sizeof(uint64_t) * (size_t)c;
+  const bool wide = c > BS_KPT * NT;  // keys per thread of the bucket sort
+  constexpr int B = LONG_BITS ? BS_BITS_LONG : BS_BITS;
+  if (lo == 0 || !LONG_BITS) {
+    if (wide) hipLaunchKernelGGL((tile_sort_kernel<NT, BS_BITS, BS_KPT_LONG>), grid, block, lds, s, a, cb, c, lo, hi, ofs);
+    else hipLaunchKernelGGL((tile_sort_kernel<NT, BS_BITS, BS_KPT>), grid, block, lds, s, a, cb, c, lo, hi, ofs);
+  } else {
+    if (wide) hipLaunchKernelGGL((tile_sort_kernel<NT, B, BS_KPT_LONG>), grid, block, lds, s, a, cb, c, lo, hi, ofs);
+    else hipLaunchKernelGGL((tile_sort_kernel<NT, B, BS_KPT>), grid, block, lds, s, a, cb, c, lo, hi, ofs);
+  }
+}
+
 // Tile-length classes of the sort launches.  The LDS of a launch is sized to
 // its longest tile, and the occupancy with it: the short tiles (most of them:
 // ~660 keys on the bench camera) get their own launch with small LDS and many
 // workgroups per CU, the long ones follow with LDS for their length (and
 // global memory beyond TS_CAP_LONG).  Bench batch (27 cameras): sort 0.94 ->
-// 0.80 ms per step with the small class at 1024 keys; one in-place buffer
-// instead of two (twice the long-class workgroups per CU): 0.52 -> 0.47 ms,
-// configs[4] 0.82 -> 0.51 ms with the LDS class up to 4096 keys.
+// 0.80 ms per step with the small class at 1024 keys; one LDS buffer instead
+// of two (twice the long-class workgroups per CU): 0.52 -> 0.47 ms, configs[4]
+// 0.82 -> 0.51 ms with the LDS class up to 4096 keys; the classes past the
+// short one with 512-thread workgroups at every scene: 0.46 -> 0.44 ms.
+// NT: the short class's workgroup size (launch_tile_sort).
 template <int NT>
 static void tile_sort_launches(const TileArgs& a, const CamBatch& cb, int64_t max_len, const SortClasses& sc,
                                hipStream_t s) {
-  const dim3 block(NT);
   const int big = 0x7FFFFFFF;
   // the short class sorts with BS_BITS bucket bits; the longer classes of the
-  // wide (512-thread, long-tile) launches with BS_BITS_LONG.  Measured: 1080p /
-  // 1M Gaussians sort 1.02 -> 0.85 ms per 4 cameras at 11 bits; the bench
-  // scene's few longer tiles (256-thread launches) are faster at 10 bits
+  // long-tile scenes (512-thread short class, mean tile >= TS_WIDE_MEAN) with
+  // BS_BITS_LONG.  Measured: 1080p / 1M Gaussians sort 1.02 -> 0.85 ms per 4
+  // cameras at 11 bits; the bench scene's longer tiles are faster at 10 bits
   // (0.54 vs 0.60 ms per step).
   constexpr bool long_bits = NT >= 512 && BS_BITS_LONG != BS_BITS;
-  // a class covers the dispatch-order positions [ofs, ofs + n) (SortClasses)
-  auto launch = [&](int cap, int lo, int hi, int ofs, int n) {
-    if (n <= 0) return;
-    const dim3 grid(n, cb.C);
-    const int c = cap > 0 ? cap : 1;
-    const size_t lds = sizeof(uint64_t) * (size_t)c;
-    const bool wide = c > BS_KPT * NT;  // keys per thread of the bucket sort
-    if (lo == 0 || !long_bits) {
-      if (wide)
-        hipLaunchKernelGGL((tile_sort_kernel<NT, BS_BITS, BS_KPT_LONG>), grid, block, lds, s, a, cb, c, lo, hi, ofs);
-      else
-        hipLaunchKernelGGL((tile_sort_kernel<NT, BS_BITS, BS_KPT>), grid, block, lds, s, a, cb, c, lo, hi, ofs);
-    } else {
-      if (wide)
-        hipLaunchKernelGGL((tile_sort_kernel<NT, BS_BITS_LONG, BS_KPT_LONG>), grid, block, lds, s, a, cb, c, lo, hi,
-                           ofs);
-      else
-        hipLaunchKernelGGL((tile_sort_kernel<NT, BS_BITS_LONG, BS_KPT>), grid, block, lds, s, a, cb, c, lo, hi, ofs);
-    }
-  };
   const int T = a.num_tiles;
   if (max_len < 0) {  // unknown lengths: the LDS classes and the global-memory class
-    launch(TS_CAP, 0, TS_CAP, 0, T);
-    launch(TS_CAP_LONG, TS_CAP, big, 0, T);
+    tile_sort_class<512, long_bits>(a, cb, TS_CAP, 0, TS_CAP, 0, T, s);
+    tile_sort_class<512, long_bits>(a, cb, TS_CAP_LONG, TS_CAP, big, 0, T, s);
     return;
   }
   const int64_t small = SORT_SMALL;
   const bool known = sc.valid;
   const int q1 = known ? sc.q1 : 0;
-  launch((int)(max_len < small ? max_len : small), 0, (int)small, q1, T - q1);
-  if (max_len > small) launch((int)(max_len < TS_CAP ? max_len : TS_CAP), (int)small, TS_CAP, 0, known ? sc.p1 : T);
+  tile_sort_class<NT, long_bits>(a, cb, (int)(max_len < small ? max_len : small), 0, (int)small, q1, T - q1, s);
+  if (max_len > small)
+    tile_sort_class<512, long_bits>(a, cb, (int)(max_len < TS_CAP ? max_len : TS_CAP), (int)small, TS_CAP, 0,
+                                    known ? sc.p1 : T, s);
   if (max_len > TS_CAP)
-    launch((int)(max_len < TS_CAP_LONG ? max_len : TS_CAP_LONG), TS_CAP, big, 0, known ? sc.p2 : T);
+    tile_sort_class<512, long_bits>(a, cb, (int)(max_len < TS_CAP_LONG ? max_len : TS_CAP_LONG), TS_CAP, big, 0,
+                                    known ? sc.p2 : T, s);
 }
 
 void launch_tile_sort(const TileArgs& a, const CamBatch& cb, int64_t max_len, int64_t L, const SortClasses& sc,
