@@ -472,7 +472,7 @@ __device__ inline uint64_t match_digit8(uint32_t d, uint64_t valid) {
 constexpr int BS_BITS = 10, BS_BITS_LONG = 11;
 constexpr int BS_KPT = 8;       // keys per thread held in registers (up to 8 NT keys per tile)
 constexpr int BS_KPT_LONG = 16;  // for launches whose tiles exceed 8 NT keys (20 / 24 measured slower)
-constexpr int BS_RUN_MAX = 48;  // longest per-thread run handed to the insertion sort
+constexpr int BS_RUN_MAX = 48;  // longest per-thread run handed to the insertion sort (64: no change)
 
 template <int NT, int BINS>
 struct RadixSmem {
@@ -834,12 +834,12 @@ template <int NT>
 static void tile_sort_launches(const TileArgs& a, const CamBatch& cb, int64_t max_len, const SortClasses& sc,
                                hipStream_t s) {
   const int big = 0x7FFFFFFF;
-  // the short class sorts with BS_BITS bucket bits; the longer classes of the
-  // long-tile scenes (512-thread short class, mean tile >= TS_WIDE_MEAN) with
-  // BS_BITS_LONG.  Measured: 1080p / 1M Gaussians sort 1.02 -> 0.85 ms per 4
-  // cameras at 11 bits; the bench scene's longer tiles are faster at 10 bits
-  // (0.54 vs 0.60 ms per step).
-  constexpr bool long_bits = NT >= 512 && BS_BITS_LONG != BS_BITS;
+  // the short class sorts with BS_BITS bucket bits, the longer (512-thread)
+  // classes with BS_BITS_LONG.  Measured: 1080p / 1M Gaussians sort 1.02 ->
+  // 0.85 ms per 4 cameras at 11 bits; the bench scene's longer tiles, once
+  // they too ran 512-thread workgroups: 0.435-0.437 -> 0.416-0.420 ms per step
+  // (with 256 threads they had been faster at 10 bits).
+  constexpr bool long_bits = BS_BITS_LONG != BS_BITS;
   const int T = a.num_tiles;
   if (max_len < 0) {  // unknown lengths: the LDS classes and the global-memory class
     tile_sort_class<512, long_bits>(a, cb, TS_CAP, 0, TS_CAP, 0, T, s);
