@@ -454,10 +454,47 @@ def _windows_arg(windows, C):
     return [[0, 0, 0, 0] if w is None else [int(v) for v in w] for w in windows]
 
 
+class BinningPlan:
+    """State of the sync-free batch forward (gs_forward_batch, ABI 11) over
+    the calls of one camera set: per camera the binning buffer's capacity
+    (the last call's exact list instances x (1 + margin) + slack) and the
+    previous plan's sort extents (gs_batch_hint).  The first call has no
+    capacity: it runs with capacity 0, which never fits, and takes the retry
+    with the exact lengths -- one forward in the two-phase path's cost.
+    `calls`, `retries` (attempts that did not fit after the first call) and
+    `num_instances` (exact, last call) are for the caller to inspect;
+    `force_capacity` (tests) replaces the computed capacities once."""
+
+    def __init__(self, margin: float = 0.125, slack: int = 4096):
+        self.margin, self.slack = float(margin), int(slack)
+        self.capacity = None
+        self.hint = [0, 0, 0, 0, 0, 0]  # gs_batch_hint {valid, p1, q1, p2, max_len, total}
+        self.num_instances = None
+        self.calls = 0
+        self.retries = 0
+        self.force_capacity = None
+
+    def next_capacity(self, C):
+        if self.force_capacity is not None:
+            cap, self.force_capacity = [int(x) for x in self.force_capacity], None
+            return cap
+        if self.capacity is None or len(self.capacity) != C:
+            return [0] * C
+        return list(self.capacity)
+
+    def update(self, num_instances, hint, fitted, first):
+        self.calls += 1
+        if not fitted and not first:
+            self.retries += 1
+        self.num_instances = [int(x) for x in num_instances]
+        self.capacity = [int(n * (1.0 + self.margin)) + self.slack for n in self.num_instances]
+        self.hint = [int(x) for x in hint]
+
+
 def rasterize_gaussians_batch(background, means3D, colors, semantic_feature, opacity, scales, rotations,
                               scale_modifier, cov3D_precomp, viewmatrices, projmatrices, c_x, c_y, tan_fovx,
                               tan_fovy, image_height, image_width, sh, degree, campos, prefiltered, debug,
-                              *, compat=None, activate=False, windows=None, feature_ready=None):
+                              *, compat=None, activate=False, windows=None, feature_ready=None, plan_state=None):
     """The forward of C cameras at once (gs_forward_plan_batch +
     gs_forward_render_batch): the arguments of rasterize_gaussians with
     per-camera matrices stacked ([C,4,4] or [C,16], campos [C,3]) and the
@@ -469,8 +506,16 @@ def rasterize_gaussians_batch(background, means3D, colors, semantic_feature, opa
     (logit, log, unnormalised; GS_FLAG_ACTIVATE).  `windows`: per camera a
     tile window (x0, y0, x1, y1) or None (gs_camera tile_*).  `feature_ready`:
     a torch.cuda.Event (recorded) the blend waits for before reading the
-    features (gs_gaussians.feature_ready), or None."""
+    features (gs_gaussians.feature_ready), or None.  `plan_state`: a
+    BinningPlan -- the sync-free forward (gs_forward_batch): no host round
+    trip between the plan and the render stages, the binning buffer sized
+    from the previous call and re-rendered with the exact lengths when it
+    does not fit (bit-identical outputs either way).  The returned
+    num_instances is then the per-camera length the binning buffer is laid
+    out with (what the backward takes); the exact counts are in
+    plan_state.num_instances."""
     L_ = _lib.load()
+    sync_free = plan_state is not None and not debug
     cm = _compat_code(compat)
     if feature_ready is not None and _present(semantic_feature):
         sf = semantic_feature
@@ -482,17 +527,25 @@ def rasterize_gaussians_batch(background, means3D, colors, semantic_feature, opa
             feature_ready = None
     nat = _native_mod()
     if nat is not None and means3D.is_cuda and means3D.dim() == 2 and means3D.size(0) > 0:
+        C_ = len(c_x)
+        cap = plan_state.next_capacity(C_) if sync_free else []
         try:
-            return nat.forward_batch(background, means3D, _opt(colors), _opt(semantic_feature), _opt(opacity),
-                                     _opt(scales), _opt(rotations), float(scale_modifier), _opt(cov3D_precomp),
-                                     viewmatrices, projmatrices, [float(x) for x in c_x], [float(x) for x in c_y],
-                                     [float(x) for x in tan_fovx], [float(x) for x in tan_fovy], int(image_height),
-                                     int(image_width), _opt(sh), int(degree), campos, bool(prefiltered),
-                                     bool(debug), cm, bool(activate), _windows_arg(windows, len(c_x)),
-                                     _event_handle(feature_ready),
-                                     torch.cuda.current_stream(means3D.device).cuda_stream)
+            out = nat.forward_batch(background, means3D, _opt(colors), _opt(semantic_feature), _opt(opacity),
+                                    _opt(scales), _opt(rotations), float(scale_modifier), _opt(cov3D_precomp),
+                                    viewmatrices, projmatrices, [float(x) for x in c_x], [float(x) for x in c_y],
+                                    [float(x) for x in tan_fovx], [float(x) for x in tan_fovy], int(image_height),
+                                    int(image_width), _opt(sh), int(degree), campos, bool(prefiltered),
+                                    bool(debug), cm, bool(activate), _windows_arg(windows, C_),
+                                    _event_handle(feature_ready), cap,
+                                    plan_state.hint if sync_free else [],
+                                    torch.cuda.current_stream(means3D.device).cuda_stream)
         except RuntimeError as ex:
             raise _lib.GsplatError(str(ex)) from None
+        NR, color, fmap, depth, alpha, radii, geom, binning, img, NI, layout, hint, fitted = out
+        if sync_free:
+            plan_state.update(NI, hint, fitted, first=not any(cap))
+            return (NR, color, fmap, depth, alpha, radii, geom, binning, img, layout)
+        return (NR, color, fmap, depth, alpha, radii, geom, binning, img, NI)
     inp = _Inputs(means3D, colors, semantic_feature, opacity, scales, rotations, scale_modifier,
                   cov3D_precomp, sh, degree)
     dev, P = inp.device, inp.P
@@ -518,18 +571,38 @@ def rasterize_gaussians_batch(background, means3D, colors, semantic_feature, opa
     stream = _stream(dev)
     NR = (ctypes.c_int64 * C)()
     NI = (ctypes.c_int64 * C)()
-    check(L_.gs_forward_plan_batch(ctypes.byref(g), cams, C, int(bool(prefiltered)), int(bool(debug)), cm,
-                                   geom.data_ptr(), img.data_ptr(), radii.data_ptr(), NR, NI, stream),
-          "rasterize_gaussians_batch (preprocess)")
-    binning = torch.empty(max(1, L_.gs_batch_binning_buffer_bytes(C, NI)), **u8)
-    check(L_.gs_forward_render_batch(ctypes.byref(g), cams, C, int(bool(debug)), cm, geom.data_ptr(),
-                                     binning.data_ptr(), img.data_ptr(), NI, radii.data_ptr(),
-                                     out_color.data_ptr(), out_feature.data_ptr() if inp.F else None,
-                                     out_depth.data_ptr(), out_alpha.data_ptr(), stream),
-          "rasterize_gaussians_batch (render)")
+    outs = (out_color.data_ptr(), out_feature.data_ptr() if inp.F else None, out_depth.data_ptr(),
+            out_alpha.data_ptr())
+    fitted = False
+    if sync_free:
+        cap_list = plan_state.next_capacity(C)
+        cap = (ctypes.c_int64 * C)(*cap_list)
+        hint = _lib.GsBatchHint(*plan_state.hint)
+        binning = torch.empty(max(1, L_.gs_batch_binning_buffer_bytes(C, cap)), **u8)
+        fits = ctypes.c_int32(0)
+        check(L_.gs_forward_batch(ctypes.byref(g), cams, C, int(bool(prefiltered)), cm, geom.data_ptr(),
+                                  img.data_ptr(), binning.data_ptr(), cap, ctypes.byref(hint), radii.data_ptr(),
+                                  NR, NI, ctypes.byref(fits), *outs, stream),
+              "rasterize_gaussians_batch (sync-free forward)")
+        fitted = bool(fits.value)
+    else:
+        check(L_.gs_forward_plan_batch(ctypes.byref(g), cams, C, int(bool(prefiltered)), int(bool(debug)), cm,
+                                       geom.data_ptr(), img.data_ptr(), radii.data_ptr(), NR, NI, stream),
+              "rasterize_gaussians_batch (preprocess)")
+    layout = list(NI)
+    if fitted:
+        layout = cap_list
+    else:
+        binning = torch.empty(max(1, L_.gs_batch_binning_buffer_bytes(C, NI)), **u8)
+        check(L_.gs_forward_render_batch(ctypes.byref(g), cams, C, int(bool(debug)), cm, geom.data_ptr(),
+                                         binning.data_ptr(), img.data_ptr(), NI, radii.data_ptr(), *outs, stream),
+              "rasterize_gaussians_batch (render)")
+    if sync_free:
+        plan_state.update(list(NI), [hint.valid, hint.p1, hint.q1, hint.p2, hint.max_len, hint.total], fitted,
+                          first=not any(cap_list))
     del keep
     feature_map = out_feature[:, :inp.F_user] if inp.F_user != inp.F else out_feature
-    return (list(NR), out_color, feature_map, out_depth, out_alpha, radii, geom, binning, img, list(NI))
+    return (list(NR), out_color, feature_map, out_depth, out_alpha, radii, geom, binning, img, layout)
 
 
 def rasterize_gaussians_batch_backward(background, means3D, radii, colors, semantic_feature, scales,

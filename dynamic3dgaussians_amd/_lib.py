@@ -16,7 +16,7 @@ _lock = threading.Lock()
 _lib = None
 
 c_void_p = ctypes.c_void_p
-ABI_VERSION = 10  # include/gsplat_hip.h GS_ABI_VERSION
+ABI_VERSION = 11  # include/gsplat_hip.h GS_ABI_VERSION
 GS_FLAG_ACCUMULATE = 1  # include/gsplat_hip.h
 GS_FLAG_ACTIVATE = 2  # include/gsplat_hip.h: raw opacity / scale / rotation parameters
 c_int32, c_int64, c_float, c_size_t = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_size_t
@@ -68,6 +68,13 @@ class GsDensifyStats(ctypes.Structure):
                 ("grad_accum", c_void_p), ("denom", c_void_p)]
 
 
+class GsBatchHint(ctypes.Structure):
+    """include/gsplat_hip.h gs_batch_hint (ABI 11): the previous plan's sort
+    extents, written back by gs_forward_batch."""
+    _fields_ = [("valid", c_int32), ("p1", c_int32), ("q1", c_int32), ("p2", c_int32),
+                ("max_len", c_int64), ("total", c_int64)]
+
+
 P_G = ctypes.POINTER(GsGaussians)
 P_NG = ctypes.POINTER(GsNeighborGraph)
 P_C = ctypes.POINTER(GsCamera)
@@ -100,6 +107,10 @@ PROTOTYPES = {
     "gs_forward_render_batch": (ctypes.c_int, [P_G, P_C, c_int32, ctypes.c_int, ctypes.c_int, c_void_p,
                                                c_void_p, c_void_p, ctypes.POINTER(c_int64), c_void_p, c_void_p,
                                                c_void_p, c_void_p, c_void_p, c_void_p]),
+    "gs_forward_batch": (ctypes.c_int, [P_G, P_C, c_int32, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p,
+                                        c_void_p, ctypes.POINTER(c_int64), ctypes.POINTER(GsBatchHint), c_void_p,
+                                        ctypes.POINTER(c_int64), ctypes.POINTER(c_int64), ctypes.POINTER(c_int32),
+                                        c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "gs_backward_batch": (ctypes.c_int, [P_G, P_C, c_int32, c_void_p, ctypes.c_int, ctypes.c_int, c_void_p,
                                          c_void_p, c_void_p, ctypes.POINTER(c_int64), c_void_p, c_void_p,
                                          c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -7,6 +7,7 @@
 // backward's per-call cudaMalloc/cudaFree (:408-409, :436) is gone.
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <mutex>
@@ -102,29 +103,51 @@ hipEvent_t pool_get() {
     g_pool.pop_back();
     return e;
   }
+  // device-scope release: no system-scope cache writeback when the stream
+  // reaches the event (hipEventReleaseToDevice), so timing a kernel does not
+  // add that to the step it is timed in
   hipEvent_t e = nullptr;
-  (void)hipEventCreate(&e);
+  if (hipEventCreateWithFlags(&e, hipEventReleaseToDevice) != hipSuccess) (void)hipEventCreate(&e);
   return e;
 }
 
+// attach = true: a one-kernel stage whose launch goes through timed_launch
+// (gs_kernels.h): the events ride on the dispatch instead of marker packets.
 struct StageTimer {
   hipStream_t s;
   int kind;
+  bool attach;
   hipEvent_t a = nullptr, b = nullptr;
-  StageTimer(hipStream_t s_, int kind_) : s(s_), kind(kind_) {
+  StageTimer(hipStream_t s_, int kind_, bool attach_ = false) : s(s_), kind(kind_), attach(attach_) {
     std::lock_guard<std::mutex> lk(g_tmu);
     if (!g_timing || !((g_timing_mask >> kind) & 1u)) return;
     a = pool_get();
     b = pool_get();
-    (void)hipEventRecord(a, s);
+    if (attach) launch_events() = LaunchEvents{a, b};
+    else (void)hipEventRecord(a, s);
   }
   ~StageTimer() {
     if (!a) return;
-    (void)hipEventRecord(b, s);
+    if (!attach) {
+      (void)hipEventRecord(b, s);
+    } else if (launch_events().start) {  // nothing was launched: an empty interval
+      launch_events() = LaunchEvents{};
+      (void)hipEventRecord(a, s);
+      (void)hipEventRecord(b, s);
+    }
     std::lock_guard<std::mutex> lk(g_tmu);
     g_events.push_back({a, b, kind});
   }
 };
+}  // namespace
+namespace gs {
+LaunchEvents& launch_events() {
+  thread_local LaunchEvents e;
+  return e;
+}
+}  // namespace gs
+namespace {
+
 // The plan's header as read back by gs_forward_plan, remembered per thread so
 // that gs_forward_render can size its sort launch without another readback.
 struct PlanInfo {
@@ -136,18 +159,93 @@ struct PlanInfo {
 };
 thread_local PlanInfo g_plan;
 
-// Page-locked host landing area of the plan headers (GS_MAX_CAMS x M_WORDS
-// words, 2 KiB per calling thread, allocated on first use and never freed:
-// freeing it from a thread-exit destructor could run after the HIP runtime
-// is gone): a device->host copy into pageable memory is staged through a
-// driver bounce buffer, an extra copy on the forward's one host round trip.
-// Host memory: the library still allocates no device memory.
-thread_local uint32_t* g_hdr = nullptr;
-static uint32_t* pinned_headers() {
-  if (!g_hdr && hipHostMalloc(reinterpret_cast<void**>(&g_hdr), sizeof(uint32_t) * GS_MAX_CAMS * M_WORDS,
-                              hipHostMallocDefault) != hipSuccess)
-    g_hdr = nullptr;
-  return g_hdr;
+// Host landing areas of the plan headers (GS_MAX_CAMS x M_WORDS words each):
+// page-locked, device-mapped, coherent host memory that tile_offsets_kernel
+// writes directly, plus an event recorded behind the plan kernels.  Leased
+// per call from a process-wide pool, so the number of buffers is bounded by
+// the number of concurrent callers (not by the threads that ever called:
+// thread pools and autograd workers would otherwise each pin one for good).
+// Never freed: a pool destructor could run after the HIP runtime is gone.
+// Env GS_HEADER_COPY=1 (A/B of the header path): a hipMemcpy2DAsync of the
+// device headers in the stream instead of tile_offsets_kernel's stores to
+// mapped host memory.
+bool header_copy() {
+  static const bool v = [] {
+    const char* e = getenv("GS_HEADER_COPY");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
+struct HeaderSlot {
+  uint32_t* host = nullptr;  // host pointer
+  uint32_t* dev = nullptr;   // the same memory as the kernels address it
+  hipEvent_t ev = nullptr;
+};
+std::mutex g_hmu;
+std::vector<HeaderSlot> g_hfree;
+
+struct HeaderLease {
+  HeaderSlot s;
+  HeaderLease() {
+    {
+      std::lock_guard<std::mutex> lk(g_hmu);
+      if (!g_hfree.empty()) {
+        s = g_hfree.back();
+        g_hfree.pop_back();
+        return;
+      }
+    }
+    void* h = nullptr;
+    if (hipHostMalloc(&h, sizeof(uint32_t) * GS_MAX_CAMS * M_WORDS,
+                      hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+      return;
+    void* d = nullptr;
+    // device-scope release: tile_offsets_kernel's stores to this host memory
+    // are system-scope atomics behind a system fence of their own
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess ||
+        hipEventCreateWithFlags(&s.ev, header_copy() ? hipEventDisableTiming : hipEventReleaseToDevice) !=
+            hipSuccess) {
+      (void)hipHostFree(h);
+      s = HeaderSlot{};
+      return;
+    }
+    s.host = static_cast<uint32_t*>(h);
+    s.dev = static_cast<uint32_t*>(d);
+  }
+  ~HeaderLease() {
+    if (!s.host) return;
+    std::lock_guard<std::mutex> lk(g_hmu);
+    g_hfree.push_back(s);
+  }
+  bool ok() const { return s.host != nullptr; }
+};
+
+// The tile sort's launch extents: the plan's longest tile and class prefixes
+// (exact, from the header; or a previous plan's with margins, whose coverage
+// the caller checks against the header afterwards), or unknown (every class
+// launch covers all tiles).
+struct SortPlan {
+  int64_t max_len = -1;  // -1: unknown
+  int64_t total = -1;    // instances of the batch (the short class's workgroup size)
+  SortClasses sc;
+  bool hinted = false;   // extents from an earlier plan (gs_batch_hint): coverage checked
+};
+
+// What launch_tile_sort(max_len, sc) covers (tile_sort_launches' class
+// decisions): nothing to check with unknown extents (every class launch
+// covers all tiles) or when exact (they came from this very plan).
+SortCover sort_cover(const SortPlan& sp, int64_t tiles) {
+  SortCover cv;
+  if (sp.max_len < 0 || !sp.sc.valid || !sp.hinted) return cv;
+  cv.on = 1;
+  cv.q1 = sp.sc.q1;
+  cv.p1 = sp.sc.p1;
+  cv.p2 = sp.sc.p2;
+  cv.mid = sp.max_len > SORT_SMALL;
+  cv.lng = sp.max_len > TS_CAP;
+  (void)tiles;
+  return cv;
 }
 
 TileArgs tile_args(int P, int W, int H, void* geom, void* image) {
@@ -344,21 +442,13 @@ static int debug_check_lists(const TileArgs& ta, const CamBatch& cb, const void*
   return 0;
 }
 
-static int plan_impl(const gs_gaussians* g, const gs_camera* cams, int C, int prefiltered, int debug, int compat,
-                     void* geom, void* image, int32_t* radii, int64_t* num_rendered, int64_t* num_instances,
-                     hipStream_t s) {
-  if (int e = check_gaussians(g, cams, true)) return e;
-  if (!num_rendered) return fail(-1, "num_rendered is null");
-  for (int c = 0; c < C; ++c) {
-    num_rendered[c] = 0;
-    if (num_instances) num_instances[c] = 0;
-  }
-  g_plan = PlanInfo{};
+// The plan's kernels (preprocess, tile histogram, column scan, offsets), the
+// headers published to hdr_dev (mapped host memory) by the last of them.
+static int plan_enqueue(const gs_gaussians* g, const gs_camera* cams, int C, int prefiltered, int debug, void* geom,
+                        void* image, int32_t* radii, uint32_t* hdr_dev, hipEvent_t done, CamBatch& cb,
+                        hipStream_t s) {
   const int P = g->P;
-  if (P == 0) return 0;
-  if (!geom || !image || !radii) return fail(-1, "geom buffer, image buffer and radii are required");
   const int W = cams[0].image_width, H = cams[0].image_height;
-  CamBatch cb;
   if (int e = make_batch(cams, C, P, W, H, cb)) return e;
   const GeomLayout gl(P);
   const TileArgs ta = tile_args(P, W, H, geom, image);
@@ -386,26 +476,22 @@ static int plan_impl(const gs_gaussians* g, const gs_camera* cams, int C, int pr
   if (int e = check("preprocess", debug, s)) return e;
   {
     StageTimer t(s, GS_STAGE_SCAN);
-    launch_tile_plan(ta, cb, prefiltered, s);
+    launch_tile_plan(ta, cb, prefiltered, hdr_dev, done, s);
   }
-  if (int e = check("tile plan", debug, s)) return e;
-  // The one host read of the forward (CR/rasterizer_impl.cu:287), one for
-  // the whole batch: the list instance counts size the binning buffer; the
-  // reference's counts and the rest of the headers ride along.
-  uint32_t stack_hdr[GS_MAX_CAMS][M_WORDS];
-  uint32_t* pin = pinned_headers();
-  uint32_t(*host)[M_WORDS] = pin ? reinterpret_cast<uint32_t(*)[M_WORDS]>(pin) : stack_hdr;
-  hipError_t he = hipMemcpy2DAsync(host, sizeof(uint32_t) * M_WORDS, ta.meta, (size_t)cb.img_stride,
-                                   sizeof(uint32_t) * M_WORDS, C, hipMemcpyDeviceToHost, s);
-  if (he == hipSuccess) he = hipStreamSynchronize(s);
-  if (he != hipSuccess) return fail((int)he, "num_rendered readback: %s", hipGetErrorString(he));
+  return check("tile plan", debug, s);
+}
+
+// The host's reading of the C plan headers: the reference's counts, the list
+// instances, the sort extents (PlanInfo), status checks.
+static int plan_read(const uint32_t (*host)[M_WORDS], int C, int prefiltered, int debug, int64_t tiles,
+                     int64_t* num_rendered, int64_t* num_instances, PlanInfo& info) {
   int64_t max_len = 0, total = 0;
   SortClasses sc;
   sc.valid = true;
   sc.q1 = 0x7FFFFFFF;
   for (int c = 0; c < C; ++c) {
     if (debug)
-      if (int e = gs_check_plan_header(host[c], (int64_t)ta.grid_x * ta.grid_y)) return e;
+      if (int e = gs_check_plan_header(host[c], tiles)) return e;
     sc.p1 = (int)host[c][M_SORT_P1] > sc.p1 ? (int)host[c][M_SORT_P1] : sc.p1;
     sc.p2 = (int)host[c][M_SORT_P2] > sc.p2 ? (int)host[c][M_SORT_P2] : sc.p2;
     sc.q1 = (int)host[c][M_SORT_Q1] < sc.q1 ? (int)host[c][M_SORT_Q1] : sc.q1;
@@ -417,18 +503,88 @@ static int plan_impl(const gs_gaussians* g, const gs_camera* cams, int C, int pr
     max_len = host[c][M_MAXN] > max_len ? host[c][M_MAXN] : max_len;
     total += host[c][M_L];
   }
-  g_plan.image = image;
-  g_plan.C = C;
-  g_plan.L = total;
-  g_plan.max_len = max_len;
-  g_plan.sort = C > 0 ? sc : SortClasses{};
+  info.C = C;
+  info.L = total;
+  info.max_len = max_len;
+  info.sort = C > 0 ? sc : SortClasses{};
+  return 0;
+}
+
+// The headers' way to the host after plan_enqueue: in the default path
+// tile_offsets_kernel stored them and its dispatch records hl's event; with
+// GS_HEADER_COPY=1 a copy command and an event marker follow it here.
+// record_only: do not wait yet.
+static int publish_wait(HeaderLease& hl, const TileArgs& ta, const CamBatch& cb, int C, hipStream_t s,
+                        bool record_only) {
+  hipError_t he = hipSuccess;
+  if (header_copy()) {
+    he = hipMemcpy2DAsync(hl.s.host, sizeof(uint32_t) * M_WORDS, ta.meta, (size_t)cb.img_stride,
+                          sizeof(uint32_t) * M_WORDS, C, hipMemcpyDeviceToHost, s);
+    if (he == hipSuccess) he = hipEventRecord(hl.s.ev, s);
+  }
+  if (he == hipSuccess && !record_only) he = hipEventSynchronize(hl.s.ev);
+  if (he == hipSuccess && !record_only) {
+    // every header's last word is 0 once written (header_sentinel): an event
+    // that did not cover the header's kernel must not hand back stale words
+    bool stale = false;
+    for (int c = 0; c < C; ++c) stale = stale || hl.s.host[c * M_WORDS + M_WORDS - 1] != 0u;
+    if (stale) {
+      he = hipStreamSynchronize(s);
+      for (int c = 0; c < C && he == hipSuccess; ++c)
+        if (hl.s.host[c * M_WORDS + M_WORDS - 1] != 0u)
+          return fail(-4, "plan header of camera %d was not written (event / header path)", c);
+    }
+  }
+  if (he != hipSuccess) return fail((int)he, "num_rendered readback: %s", hipGetErrorString(he));
+  return 0;
+}
+
+// Mark the leased header words unwritten before the plan that fills them.
+static void header_sentinel(HeaderLease& hl, int C) {
+  for (int c = 0; c < C; ++c) hl.s.host[c * M_WORDS + M_WORDS - 1] = 0xFFFFFFFFu;
+}
+
+static int plan_impl(const gs_gaussians* g, const gs_camera* cams, int C, int prefiltered, int debug, int compat,
+                     void* geom, void* image, int32_t* radii, int64_t* num_rendered, int64_t* num_instances,
+                     hipStream_t s) {
+  if (int e = check_gaussians(g, cams, true)) return e;
+  if (!num_rendered) return fail(-1, "num_rendered is null");
+  for (int c = 0; c < C; ++c) {
+    num_rendered[c] = 0;
+    if (num_instances) num_instances[c] = 0;
+  }
+  g_plan = PlanInfo{};
+  const int P = g->P;
+  if (P == 0) return 0;
+  if (!geom || !image || !radii) return fail(-1, "geom buffer, image buffer and radii are required");
+  HeaderLease hl;
+  if (!hl.ok()) return fail((int)hipErrorOutOfMemory, "cannot allocate the page-locked plan header buffer");
+  header_sentinel(hl, C);
+  CamBatch cb;
+  if (int e = plan_enqueue(g, cams, C, prefiltered, debug, geom, image, radii, header_copy() ? nullptr : hl.s.dev,
+                           header_copy() ? nullptr : hl.s.ev,
+                           cb, s))
+    return e;
+  // The one host read of the forward (CR/rasterizer_impl.cu:287), one for
+  // the whole batch: the list instance counts size the binning buffer; the
+  // reference's counts and the rest of the headers ride along.
+  const TileArgs ta = tile_args(P, cams[0].image_width, cams[0].image_height, geom, image);
+  if (int e = publish_wait(hl, ta, cb, C, s, false)) return e;
+  PlanInfo info;
+  if (int e = plan_read(reinterpret_cast<const uint32_t(*)[M_WORDS]>(hl.s.host), C, prefiltered, debug,
+                        (int64_t)ta.grid_x * ta.grid_y, num_rendered, num_instances, info))
+    return e;
+  info.image = image;
+  g_plan = info;
   (void)compat;
   return 0;
 }
 
+// L[c]: the instances camera c's binning buffer is laid out for (its list
+// length, or gs_forward_batch's capacity); sp: the sort launch extents.
 static int render_impl(const gs_gaussians* g, const gs_camera* cams, int C, int debug, int compat, void* geom,
                        void* binning, void* image, const int64_t* L, const int32_t* radii, float* out_color,
-                       float* out_feature, float* out_depth, float* out_alpha, hipStream_t s) {
+                       float* out_feature, float* out_depth, float* out_alpha, const SortPlan& sp, hipStream_t s) {
   if (int e = check_gaussians(g, cams, true)) return e;
   const int P = g->P;
   if (P == 0) return 0;  // the reference leaves the zero-filled outputs untouched
@@ -451,7 +607,7 @@ static int render_impl(const gs_gaussians* g, const gs_camera* cams, int C, int 
     // the dispatch order (longest list first) from the ranges: the stage the
     // reference's identifyTileRanges occupies
     StageTimer t(s, GS_STAGE_RANGES);
-    launch_tile_order(ta, cb, s);
+    launch_tile_order(ta, cb, sort_cover(sp, gx * gy), s);
   }
   if (total > 0) {
     {
@@ -459,14 +615,14 @@ static int render_impl(const gs_gaussians* g, const gs_camera* cams, int C, int 
       launch_tile_bucket(ta, cb, s);
     }
     if (int e = check("duplicateWithKeys", debug, s)) return e;
-    const bool known = g_plan.image == image && g_plan.C == C && g_plan.L == total;
     {
       StageTimer t(s, GS_STAGE_SORT);
-      launch_tile_sort(ta, cb, known ? g_plan.max_len : -1, total, known ? g_plan.sort : SortClasses{}, s);
+      launch_tile_sort(ta, cb, sp.max_len, sp.total >= 0 ? sp.total : total,
+                       sp.max_len >= 0 ? sp.sc : SortClasses{}, s);
     }
     if (int e = check("tile sort", debug, s)) return e;
     if (debug)
-      if (int e = debug_check_lists(ta, cb, binning, L, P, (int64_t)gx * gy, known ? g_plan.max_len : -1, s))
+      if (int e = debug_check_lists(ta, cb, binning, L, P, (int64_t)gx * gy, sp.max_len, s))
         return e;
   }
   RenderArgs ra{};
@@ -486,7 +642,7 @@ static int render_impl(const gs_gaussians* g, const gs_camera* cams, int C, int 
     if (e != hipSuccess) return fail((int)e, "waiting for feature_ready: %s", hipGetErrorString(e));
   }
   {
-    StageTimer t(s, GS_STAGE_RENDER_FWD);
+    StageTimer t(s, GS_STAGE_RENDER_FWD, true);
     if (!launch_render_fwd(ra, cb, s)) return fail(-1, "unsupported feature width %d", g->F);
   }
   return check("render", debug, s);
@@ -543,7 +699,7 @@ static int backward_impl(const gs_gaussians* g, const gs_camera* cams, int C, co
   ra.dL_dpix = dL_dout_color; ra.dL_dfeat = dL_dout_feature; ra.dL_ddepth = dL_dout_depth;
   ra.dL_dalpha = dL_dout_alpha; ra.acc = acc; ra.dsem = dsem_pad ? dsem_pad : dL_dsemantic;
   {
-    StageTimer t(s, GS_STAGE_RENDER_BWD);
+    StageTimer t(s, GS_STAGE_RENDER_BWD, true);
     if (!launch_render_bwd(ra, cb, s)) return fail(-1, "unsupported feature width %d", g->F);
     if (dsem_pad) launch_feature_grad_rows(dsem_pad, dL_dsemantic, P, g->F, accumulate ? 1 : 0, s);
   }
@@ -572,6 +728,20 @@ static int backward_impl(const gs_gaussians* g, const gs_camera* cams, int C, co
   return check("preprocess backward", debug, s);
 }
 
+// The sort extents of the last plan of this thread when the render belongs
+// to it (same image buffer, cameras and list lengths), else unknown.
+static SortPlan exact_sort_plan(const void* image, int C, const int64_t* L) {
+  SortPlan sp;
+  int64_t total = 0;
+  for (int c = 0; c < C; ++c) total += L[c] > 0 ? L[c] : 0;
+  if (g_plan.image == image && g_plan.C == C && g_plan.L == total) {
+    sp.max_len = g_plan.max_len;
+    sp.total = total;
+    sp.sc = g_plan.sort;
+  }
+  return sp;
+}
+
 int gs_forward_plan(const gs_gaussians* g, const gs_camera* cam, int prefiltered, int debug, int compat,
                     void* geom, void* image, int32_t* radii, int64_t* num_rendered, int64_t* num_instances,
                     gs_stream_t stream) {
@@ -585,7 +755,7 @@ int gs_forward_render(const gs_gaussians* g, const gs_camera* cam, int debug, in
                       float* out_feature, float* out_depth, float* out_alpha, gs_stream_t stream) {
   if (!cam) return fail(-1, "null argument block");
   return render_impl(g, cam, 1, debug, compat, geom, binning, image, &L, radii, out_color, out_feature, out_depth,
-                     out_alpha, (hipStream_t)stream);
+                     out_alpha, exact_sort_plan(image, 1, &L), (hipStream_t)stream);
 }
 
 int gs_backward(const gs_gaussians* g, const gs_camera* cam, const int32_t* radii, int debug, int compat,
@@ -630,7 +800,108 @@ int gs_forward_render_batch(const gs_gaussians* g, const gs_camera* cams, int32_
   if (!cams || !num_instances) return fail(-1, "null argument block");
   if (C < 1 || C > GS_MAX_CAMS) return fail(-1, "camera batch size %d outside 1..%d", C, GS_MAX_CAMS);
   return render_impl(g, cams, C, debug, compat, geom, binning, image, num_instances, radii, out_color,
-                     out_feature, out_depth, out_alpha, (hipStream_t)stream);
+                     out_feature, out_depth, out_alpha, exact_sort_plan(image, C, num_instances),
+                     (hipStream_t)stream);
+}
+
+// ---- sync-free batch forward (ABI 11)
+
+// Launch extents from a previous plan (gs_batch_hint), widened by margins;
+// tile_sort_launches launches the class above SORT_SMALL keys when max_len
+// exceeds it and the one above TS_CAP likewise.
+static SortPlan hinted_sort_plan(const gs_batch_hint* h, int64_t tiles) {
+  SortPlan sp;
+  if (!h || !h->valid) return sp;  // unknown: every class launch covers all tiles
+  auto grow = [&](int64_t v) { return v + (v / 8 > 16 ? v / 8 : 16); };
+  sp.max_len = grow(h->max_len > 0 ? h->max_len : 1);
+  sp.total = h->total > 0 ? h->total : 0;
+  sp.sc.valid = true;
+  const int64_t q = h->q1 - (h->q1 / 8 > 16 ? h->q1 / 8 : 16);
+  sp.sc.q1 = (int)(q < 0 ? 0 : (q > tiles ? tiles : q));
+  sp.hinted = true;
+  sp.sc.p1 = (int)(grow(h->p1) < tiles ? grow(h->p1) : tiles);
+  sp.sc.p2 = (int)(grow(h->p2) < tiles ? grow(h->p2) : tiles);
+  return sp;
+}
+
+// Did the sort launches of `sp` cover every tile of the plan `a`?  (Class
+// extents are positions in the dispatch order: the short class [q1, T), the
+// classes above SORT_SMALL / TS_CAP keys [0, p1) / [0, p2).)
+// The batch-wide form of tile_order_kernel's per-camera test (q1 the least
+// over the cameras, p1 / p2 / max_len the largest): false iff some camera
+// was rendered empty.
+static bool sort_covered(const SortCover& cv, const PlanInfo& a) {
+  if (!cv.on) return true;
+  if (a.sort.q1 < cv.q1) return false;
+  if (a.max_len > SORT_SMALL && (!cv.mid || a.sort.p1 > cv.p1)) return false;
+  if (a.max_len > TS_CAP && (!cv.lng || a.sort.p2 > cv.p2)) return false;
+  return true;
+}
+
+int gs_forward_batch(const gs_gaussians* g, const gs_camera* cams, int32_t C, int prefiltered, int compat,
+                     void* geom, void* image, void* binning, const int64_t* capacity, gs_batch_hint* hint,
+                     int32_t* radii, int64_t* num_rendered, int64_t* num_instances, int32_t* fits,
+                     float* out_color, float* out_feature, float* out_depth, float* out_alpha, gs_stream_t stream) {
+  if (!cams || !capacity || !num_rendered || !num_instances || !fits) return fail(-1, "null argument block");
+  if (C < 1 || C > GS_MAX_CAMS) return fail(-1, "camera batch size %d outside 1..%d", C, GS_MAX_CAMS);
+  if (int e = check_gaussians(g, cams, true)) return e;
+  *fits = 1;
+  for (int c = 0; c < C; ++c) {
+    num_rendered[c] = 0;
+    num_instances[c] = 0;
+    if (capacity[c] < 0) return fail(-1, "capacity[%d] = %lld < 0", c, (long long)capacity[c]);
+  }
+  g_plan = PlanInfo{};
+  const int P = g->P;
+  if (P == 0) return 0;  // the reference leaves the zero-filled outputs untouched
+  if (!geom || !image || !radii) return fail(-1, "geom buffer, image buffer and radii are required");
+  int64_t cap_total = 0;
+  for (int c = 0; c < C; ++c) cap_total += capacity[c];
+  if (cap_total > 0 && !binning) return fail(-1, "binning buffer is null");
+  if (!out_color || !out_depth || (g->F > 0 && !out_feature) || (compat != COMPAT_REFERENCE && !out_alpha))
+    return fail(-1, "output image pointers are required");
+  HeaderLease hl;
+  if (!hl.ok()) return fail((int)hipErrorOutOfMemory, "cannot allocate the page-locked plan header buffer");
+  header_sentinel(hl, C);
+  hipStream_t s = (hipStream_t)stream;
+  CamBatch cb;
+  if (int e = plan_enqueue(g, cams, C, prefiltered, 0, geom, image, radii, header_copy() ? nullptr : hl.s.dev,
+                           header_copy() ? nullptr : hl.s.ev, cb,
+                           s))
+    return e;
+  const int W = cams[0].image_width, H = cams[0].image_height;
+  const TileArgs ta = tile_args(P, W, H, geom, image);
+  const int64_t tiles = (int64_t)ta.grid_x * ta.grid_y;
+  if (int e = publish_wait(hl, ta, cb, C, s, true)) return e;
+  // Every stage behind the plan is enqueued before the host looks at the
+  // headers: the GPU goes on from the plan to the bucket, sort and blend
+  // launches while the host waits for the event.
+  const SortPlan sp = hinted_sort_plan(hint, tiles);
+  if (int e = render_impl(g, cams, C, 0, compat, geom, binning, image, capacity, radii, out_color, out_feature,
+                          out_depth, out_alpha, sp, s))
+    return e;
+  {
+    const hipError_t he = hipEventSynchronize(hl.s.ev);
+    if (he != hipSuccess) return fail((int)he, "num_rendered readback: %s", hipGetErrorString(he));
+  }
+  PlanInfo info;
+  if (int e = plan_read(reinterpret_cast<const uint32_t(*)[M_WORDS]>(hl.s.host), C, prefiltered, 0, tiles,
+                        num_rendered, num_instances, info))
+    return e;
+  info.image = image;
+  g_plan = info;  // a follow-up gs_forward_render_batch with the exact lengths uses the exact extents
+  bool ok = sort_covered(sort_cover(sp, tiles), info);
+  for (int c = 0; c < C; ++c) ok = ok && num_instances[c] <= capacity[c];
+  *fits = ok ? 1 : 0;
+  if (hint) {
+    hint->valid = 1;
+    hint->max_len = info.max_len;
+    hint->total = info.L;
+    hint->p1 = info.sort.p1;
+    hint->q1 = info.sort.q1;
+    hint->p2 = info.sort.p2;
+  }
+  return 0;
 }
 
 int gs_backward_batch(const gs_gaussians* g, const gs_camera* cams, int32_t C, const int32_t* radii, int debug,

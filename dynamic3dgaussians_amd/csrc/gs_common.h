@@ -82,6 +82,7 @@ __host__ __device__ inline int64_t sort_blocks(int64_t n) {
 constexpr int TB_BLOCKS = 128;  // per camera; a multiple of 64 (tile_rowscan_kernel, tile_offsets_kernel)
 constexpr int TB_THREADS = 1024;
 constexpr int TB_BINS = 16384;    // LDS tile bins per pass (64 KiB)
+constexpr int SORT_SMALL = 1024;  // tile length up to which the tile sort runs in its short (small-LDS) class
 constexpr int TS_CAP = 4096;      // per-tile LDS sort capacity (32 KiB of u64 keys, sorted in place)
 constexpr int TS_CAP_LONG = 9600; // long-tile launch: 75 KiB (+ 8 KiB radix state), two workgroups per CU
 constexpr int TS_WIDE_MEAN = 1024; // mean tile length from which the sort uses 512-thread workgroups

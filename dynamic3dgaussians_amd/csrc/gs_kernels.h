@@ -1,6 +1,7 @@
 // gs_kernels.h -- kernel argument blocks and host launchers (internal).
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include "../../include/gs_optim.h"
@@ -112,6 +113,28 @@ struct RenderBwdArgs {
   float* dsem;  // P x F semantic-feature gradients (the output), zeroed (or holding earlier sums) by the caller
 };
 
+// Live stage timing of a one-kernel stage (gs_timing_*, gs_api.hip): the
+// stage's event pair travels to its kernel launch (thread-local, consumed by
+// timed_launch) and is attached to the dispatch itself through
+// hipExtLaunchKernel -- the kernel's own start / end timestamps, no marker
+// packets in the stream between it and its neighbours (a marker pair cost the
+// timed step ~12 us of idle GPU: profiles/r05sf2, tools/step_gaps.py).
+struct LaunchEvents {
+  hipEvent_t start = nullptr, stop = nullptr;
+};
+LaunchEvents& launch_events();
+template <class K, class... A>
+inline void timed_launch(K kernel, dim3 grid, dim3 block, uint32_t lds, hipStream_t s, A... args) {
+  LaunchEvents& e = launch_events();
+  if (e.start) {
+    const LaunchEvents ev = e;
+    e = LaunchEvents{};
+    hipExtLaunchKernelGGL(kernel, grid, block, lds, s, ev.start, ev.stop, 0u, args...);
+  } else {
+    hipLaunchKernelGGL(kernel, grid, block, lds, s, args...);
+  }
+}
+
 void launch_preprocess_fwd(const PreprocessArgs& a, const CamBatch& cb, hipStream_t s);
 void launch_preprocess_bwd(const PreprocessBwdArgs& a, const CamBatch& cb, hipStream_t s);
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t s);
@@ -162,12 +185,28 @@ __host__ __device__ inline TileArgs cam_tile_args(const TileArgs& a0, const CamB
   return a;
 }
 // plan: per-block tile histograms, tile totals and offsets, ranges, header
-void launch_tile_plan(const TileArgs& a, const CamBatch& cb, int prefiltered, hipStream_t s);
+// (also stored to hdr_host[c * M_WORDS ..] when non-null: mapped host memory;
+// `done`, when non-null, is recorded by the dispatch of the header's kernel)
+void launch_tile_plan(const TileArgs& a, const CamBatch& cb, int prefiltered, uint32_t* hdr_host, hipEvent_t done,
+                      hipStream_t s);
 // render: bucket the instances by tile, then sort every tile by (depth, id).
 // max_len = the plan header's longest tile (host copy), or -1 if unknown.
 void launch_tile_bucket(const TileArgs& a, const CamBatch& cb, hipStream_t s);
+// What the tile sort launches of a render cover (tile_sort_launches): on = 0
+// every tile (the exact or unknown extents); else the short class the
+// dispatch positions [q1, T), the class above SORT_SMALL keys (if mid) [0,
+// p1), the one above TS_CAP (if lng) [0, p2).  A camera whose plan puts a
+// tile outside them (gs_forward_batch's hinted extents gone stale) gets empty
+// dispatch records, like one over its binning capacity: its lists are never
+// read unsorted, and the host, checking the same condition on the headers,
+// renders it again.
+struct SortCover {
+  int on = 0;
+  int q1 = 0, p1 = 0, p2 = 0;
+  int mid = 0, lng = 0;
+};
 // dispatch order of the blend / sort kernels (tiles by descending list length)
-void launch_tile_order(const TileArgs& a, const CamBatch& cb, hipStream_t s);
+void launch_tile_order(const TileArgs& a, const CamBatch& cb, const SortCover& cv, hipStream_t s);
 // max_len: the longest tile over the batch (-1: unknown); L: the batch's total instances
 // Dispatch-order extents of the sort's length classes over the batch (plan
 // header M_SORT_*: p1 / p2 = max over cameras of the prefixes holding every

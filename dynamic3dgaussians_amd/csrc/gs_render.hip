@@ -1348,18 +1348,18 @@ template <int F>
 static void fwd_f(const RenderArgs& a, const CamBatch& cb, hipStream_t s) {
   dim3 grid(a.num_tiles * (4 / WPB_FWD) * cb.C), block(64 * WPB_FWD);
   if (a.compat == COMPAT_REFERENCE)
-    hipLaunchKernelGGL((render_fwd_kernel<F, COMPAT_REFERENCE>), grid, block, 0, s, a, cb);
+    timed_launch(render_fwd_kernel<F, COMPAT_REFERENCE>, grid, block, 0, s, a, cb);
   else
-    hipLaunchKernelGGL((render_fwd_kernel<F, COMPAT_FIXED>), grid, block, 0, s, a, cb);
+    timed_launch(render_fwd_kernel<F, COMPAT_FIXED>, grid, block, 0, s, a, cb);
 }
 
 template <int F>
 static void bwd_f(const RenderBwdArgs& a, const CamBatch& cb, hipStream_t s) {
   dim3 grid(a.num_tiles * (4 / WPB_BWD) * cb.C), block(64 * WPB_BWD);
   if (a.compat == COMPAT_REFERENCE)
-    hipLaunchKernelGGL((render_bwd_kernel<F, COMPAT_REFERENCE>), grid, block, 0, s, a, cb);
+    timed_launch(render_bwd_kernel<F, COMPAT_REFERENCE>, grid, block, 0, s, a, cb);
   else
-    hipLaunchKernelGGL((render_bwd_kernel<F, COMPAT_FIXED>), grid, block, 0, s, a, cb);
+    timed_launch(render_bwd_kernel<F, COMPAT_FIXED>, grid, block, 0, s, a, cb);
 }
 
 bool launch_render_fwd(const RenderArgs& a, const CamBatch& cb, hipStream_t s) {

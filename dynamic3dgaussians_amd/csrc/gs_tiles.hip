@@ -45,9 +45,6 @@
 
 namespace gs {
 
-// tile length up to which the tile sort runs in its short (small-LDS) class
-constexpr int SORT_SMALL = 1024;
-
 // Instances of one rect handled by one lane; larger rects are spread over the
 // wave (a full-screen Gaussian must not serialize its wave for 2,500 tiles).
 constexpr int LANE_TILES = 16;
@@ -60,6 +57,9 @@ constexpr int LANE_TILES = 16;
 template <bool WRITE>
 __global__ __launch_bounds__(TB_THREADS) void tile_hist_kernel(TileArgs a0, CamBatch cb, int t0, int nt) {
   const TileArgs a = cam_tile_args(a0, cb, blockIdx.y);
+  // a binning buffer laid out for fewer instances than the plan counted
+  // (gs_forward_batch's capacity): store nothing, the caller renders again
+  if (WRITE && a.meta[M_L] > (uint64_t)cb.bin_L[blockIdx.y]) return;
   extern __shared__ uint32_t s_bin[];  // nt counters (hist) or cursors (bucket)
   __shared__ uint32_t s_rect[TB_THREADS / 64];
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
@@ -139,6 +139,7 @@ __global__ __launch_bounds__(TB_THREADS) void tile_hist_kernel(TileArgs a0, CamB
 // before.
 __global__ __launch_bounds__(TB_THREADS) void tile_bucket_kernel(TileArgs a0, CamBatch cb, int t0, int nt, int cap) {
   const TileArgs a = cam_tile_args(a0, cb, blockIdx.y);
+  if (a.meta[M_L] > (uint64_t)cb.bin_L[blockIdx.y]) return;  // over capacity (tile_hist_kernel<true>)
   extern __shared__ uint64_t s_dyn64[];
   uint64_t* s_key = s_dyn64;                                    // cap keys
   uint32_t* s_cur = reinterpret_cast<uint32_t*>(s_key + cap);   // nt run cursors (local, or global if direct)
@@ -306,7 +307,7 @@ __global__ __launch_bounds__(OFF_T) void tile_offsets_kernel(const uint32_t* __r
                                                              const uint32_t* __restrict__ bsum0,
                                                              uint2* __restrict__ ranges0,
                                                              uint32_t* __restrict__ meta0, int prefiltered,
-                                                             CamBatch cb) {
+                                                             CamBatch cb, uint32_t* __restrict__ hdr_host) {
   const int64_t io = blockIdx.x * cb.img_stride;  // one workgroup per camera
   const uint32_t* __restrict__ ttotal = shift_bytes(ttotal0, io);
   const uint32_t* __restrict__ bsum = shift_bytes(bsum0, io);
@@ -380,16 +381,29 @@ __global__ __launch_bounds__(OFF_T) void tile_offsets_kernel(const uint32_t* __r
   }
   __syncthreads();
   if (tid == 0) {
-    meta[M_SORT_P1] = s_cnt[0];
-    meta[M_SORT_Q1] = s_cnt[1];
-    meta[M_SORT_P2] = s_cnt[2];
     const unsigned long long lref = s_lref;
     // ranges are 32-bit, as in the reference
     const uint32_t ovf = (total > 0xFFFFFFFFull || lref > 0xFFFFFFFFull) ? 2u : 0u;
-    meta[M_L] = (uint32_t)total;
-    meta[M_MAXN] = s_max;
-    meta[M_LREF] = (uint32_t)lref;
-    meta[M_STATUS] = prefiltered ? (meta[M_STATUS] | ovf) : ovf;
+    uint32_t h[M_WORDS] = {0u};
+    h[M_L] = (uint32_t)total;
+    h[M_MAXN] = s_max;
+    h[M_LREF] = (uint32_t)lref;
+    h[M_STATUS] = prefiltered ? (meta[M_STATUS] | ovf) : ovf;
+    h[M_SORT_P1] = s_cnt[0];
+    h[M_SORT_Q1] = s_cnt[1];
+    h[M_SORT_P2] = s_cnt[2];
+#pragma unroll
+    for (int w = 0; w < M_WORDS; ++w) meta[w] = h[w];
+    // The host's copy of the header: page-locked, device-mapped, coherent
+    // host memory written here directly (vector stores at system scope), so
+    // no copy command sits in the stream between the plan and the render
+    // launches; the host reads it after an event recorded behind this kernel.
+    if (hdr_host) {
+      uint32_t* o = hdr_host + (size_t)blockIdx.x * M_WORDS;
+#pragma unroll
+      for (int w = 0; w < M_WORDS; ++w) __hip_atomic_store(o + w, h[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __threadfence_system();
+    }
   }
 }
 
@@ -404,7 +418,7 @@ __global__ __launch_bounds__(OFF_T) void tile_offsets_kernel(const uint32_t* __r
 __global__ __launch_bounds__(OFF_T) void tile_order_kernel(const uint32_t* __restrict__ ttotal0, int T,
                                                            const uint32_t* __restrict__ meta0,
                                                            const uint2* __restrict__ ranges0,
-                                                           uint4* __restrict__ order0, CamBatch cb) {
+                                                           uint4* __restrict__ order0, CamBatch cb, SortCover cv) {
   const int64_t io = blockIdx.x * cb.img_stride;  // one workgroup per camera
   const uint32_t* __restrict__ ttotal = shift_bytes(ttotal0, io);
   const uint32_t* __restrict__ meta = shift_bytes(meta0, io);
@@ -418,6 +432,16 @@ __global__ __launch_bounds__(OFF_T) void tile_order_kernel(const uint32_t* __res
   s_obin[tid] = 0;
   __syncthreads();
   const uint32_t mxl = meta[M_MAXN];
+  // a camera whose lists exceed its binning buffer (gs_forward_batch's
+  // capacity) gets empty dispatch records: the sort and blend kernels then
+  // read nothing from that buffer, and the caller renders again
+  bool over = meta[M_L] > (uint64_t)cb.bin_L[blockIdx.x];
+  if (cv.on) {  // a tile outside the sort launches (SortCover): render nothing either
+    const bool covered = meta[M_SORT_Q1] >= (uint32_t)cv.q1 &&
+                         (mxl <= (uint32_t)SORT_SMALL || (cv.mid && meta[M_SORT_P1] <= (uint32_t)cv.p1)) &&
+                         (mxl <= (uint32_t)TS_CAP || (cv.lng && meta[M_SORT_P2] <= (uint32_t)cv.p2));
+    over = over || !covered;
+  }
   const int sh = mxl >= OFF_T ? (32 - __builtin_clz(mxl)) - 10 : 0;
   for (int t = a0; t < a1; ++t) atomicAdd(&s_obin[OFF_T - 1 - min(ttotal[t] >> sh, (uint32_t)(OFF_T - 1))], 1u);
   __syncthreads();
@@ -437,7 +461,7 @@ __global__ __launch_bounds__(OFF_T) void tile_order_kernel(const uint32_t* __res
   for (int t = a0; t < a1; ++t) {
     const uint2 r = ranges[t];
     order[atomicAdd(&s_obin[OFF_T - 1 - min(ttotal[t] >> sh, (uint32_t)(OFF_T - 1))], 1u)] =
-        make_uint4((uint32_t)t, r.x, r.y, 0u);
+        over ? make_uint4((uint32_t)t, 0u, 0u, 0u) : make_uint4((uint32_t)t, r.x, r.y, 0u);
   }
 }
 
@@ -761,7 +785,8 @@ __global__ __launch_bounds__(NT) void tile_sort_kernel(TileArgs a0, CamBatch cb,
 
 // ------------------------------------------------------------------ launchers
 
-void launch_tile_plan(const TileArgs& a, const CamBatch& cb, int prefiltered, hipStream_t s) {
+void launch_tile_plan(const TileArgs& a, const CamBatch& cb, int prefiltered, uint32_t* hdr_host, hipEvent_t done,
+                      hipStream_t s) {
   const int T = a.num_tiles;
   for (int t0 = 0; t0 < T; t0 += TB_BINS) {
     const int nt = min(TB_BINS, T - t0);
@@ -770,13 +795,19 @@ void launch_tile_plan(const TileArgs& a, const CamBatch& cb, int prefiltered, hi
   }
   hipLaunchKernelGGL(tile_rowscan_kernel, dim3((T + RS_T - 1) / RS_T, cb.C), dim3(RS_THREADS), 0, s, a.thist, a.ttotal, T,
                      cb);
-  hipLaunchKernelGGL(tile_offsets_kernel, dim3(cb.C), dim3(OFF_T), 0, s, a.ttotal, T, a.bsum, a.ranges, a.meta,
-                     prefiltered, cb);
+  // the host waits for `done`: an event of this dispatch itself, not a
+  // marker packet between it and the render launches behind it
+  if (done)
+    hipExtLaunchKernelGGL(tile_offsets_kernel, dim3(cb.C), dim3(OFF_T), 0, s, nullptr, done, 0u, a.ttotal, T, a.bsum,
+                          a.ranges, a.meta, prefiltered, cb, hdr_host);
+  else
+    hipLaunchKernelGGL(tile_offsets_kernel, dim3(cb.C), dim3(OFF_T), 0, s, a.ttotal, T, a.bsum, a.ranges, a.meta,
+                       prefiltered, cb, hdr_host);
 }
 
-void launch_tile_order(const TileArgs& a, const CamBatch& cb, hipStream_t s) {
+void launch_tile_order(const TileArgs& a, const CamBatch& cb, const SortCover& cv, hipStream_t s) {
   hipLaunchKernelGGL(tile_order_kernel, dim3(cb.C), dim3(OFF_T), 0, s, a.ttotal, a.num_tiles, a.meta, a.ranges, a.order,
-                     cb);
+                     cb, cv);
 }
 
 void launch_tile_bucket(const TileArgs& a, const CamBatch& cb, hipStream_t s) {

@@ -278,13 +278,22 @@ struct Cameras {
   }
 };
 
-std::tuple<std::vector<int64_t>, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, std::vector<int64_t>>
+// capacity: empty = the two-phase path (plan, host read, render); else the
+// sync-free gs_forward_batch with a binning buffer of capacity[c] instances
+// per camera and `hint` (gs_batch_hint as {valid, p1, q1, p2, max_len,
+// total}), retried with the exact lengths when they do not fit.  Returns the
+// reference's counts, the images and state, the exact num_instances, the
+// per-camera lengths the binning buffer is laid out with (what the backward
+// takes), the updated hint and whether the first attempt fitted.
+std::tuple<std::vector<int64_t>, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, std::vector<int64_t>,
+           std::vector<int64_t>, std::vector<int64_t>, bool>
 forward_batch(const Tensor& bg, const Tensor& means3D, const OptT& colors, const OptT& sem, const OptT& opacity,
               const OptT& scales, const OptT& rotations, double scale_modifier, const OptT& cov3D, const Tensor& views,
               const Tensor& projs, const std::vector<double>& cx, const std::vector<double>& cy,
               const std::vector<double>& tx, const std::vector<double>& ty, int64_t H, int64_t W, const OptT& sh,
               int64_t degree, const Tensor& campos, bool prefiltered, bool debug, int64_t compat, bool activate,
-              const std::vector<std::vector<int64_t>>& windows, int64_t feature_ready, int64_t stream) {
+              const std::vector<std::vector<int64_t>>& windows, int64_t feature_ready,
+              const std::vector<int64_t>& capacity, const std::vector<int64_t>& hint, int64_t stream) {
   Inputs in(means3D, colors, sem, opacity, scales, rotations, scale_modifier, cov3D, sh, degree);
   if (activate) in.g.flags |= GS_FLAG_ACTIVATE;
   in.g.feature_ready = reinterpret_cast<gs_event_t>(feature_ready);
@@ -301,18 +310,51 @@ forward_batch(const Tensor& bg, const Tensor& means3D, const OptT& colors, const
   Tensor img = at::empty({(int64_t)gs_batch_image_buffer_bytes((int32_t)W, (int32_t)H, C)}, u8);
   std::vector<int64_t> NR(C, 0), NI(C, 0);
   gs_stream_t s = reinterpret_cast<gs_stream_t>(stream);
-  check(gs_forward_plan_batch(&in.g, k.cams.data(), C, prefiltered ? 1 : 0, debug ? 1 : 0, (int)compat,
-                              geom.data_ptr(), img.data_ptr(), radii.data_ptr<int32_t>(), NR.data(), NI.data(), s),
-        "rasterize_gaussians_batch (preprocess)");
-  const int64_t nb = (int64_t)gs_batch_binning_buffer_bytes(C, NI.data());
-  Tensor binning = at::empty({nb > 1 ? nb : 1}, u8);
-  check(gs_forward_render_batch(&in.g, k.cams.data(), C, debug ? 1 : 0, (int)compat, geom.data_ptr(),
-                                binning.data_ptr(), img.data_ptr(), NI.data(), radii.data_ptr<int32_t>(),
-                                out_color.data_ptr<float>(), in.F ? out_feature.data_ptr<float>() : nullptr,
-                                out_depth.data_ptr<float>(), out_alpha.data_ptr<float>(), s),
-        "rasterize_gaussians_batch (render)");
+  float* oc = out_color.data_ptr<float>();
+  float* of = in.F ? out_feature.data_ptr<float>() : nullptr;
+  float* od = out_depth.data_ptr<float>();
+  float* oa = out_alpha.data_ptr<float>();
+  Tensor binning;
+  bool fitted = false;
+  gs_batch_hint h{};
+  if (!capacity.empty() && !debug) {
+    if ((int64_t)capacity.size() != C) throw std::runtime_error("capacity must have C entries");
+    if (hint.size() == 6) {
+      h.valid = (int32_t)hint[0];
+      h.p1 = (int32_t)hint[1];
+      h.q1 = (int32_t)hint[2];
+      h.p2 = (int32_t)hint[3];
+      h.max_len = hint[4];
+      h.total = hint[5];
+    }
+    const int64_t nb = (int64_t)gs_batch_binning_buffer_bytes(C, capacity.data());
+    binning = at::empty({nb > 1 ? nb : 1}, u8);
+    int32_t fits = 0;
+    check(gs_forward_batch(&in.g, k.cams.data(), C, prefiltered ? 1 : 0, (int)compat, geom.data_ptr(),
+                           img.data_ptr(), binning.data_ptr(), capacity.data(), &h, radii.data_ptr<int32_t>(),
+                           NR.data(), NI.data(), &fits, oc, of, od, oa, s),
+          "rasterize_gaussians_batch (sync-free forward)");
+    fitted = fits != 0;
+  } else {
+    check(gs_forward_plan_batch(&in.g, k.cams.data(), C, prefiltered ? 1 : 0, debug ? 1 : 0, (int)compat,
+                                geom.data_ptr(), img.data_ptr(), radii.data_ptr<int32_t>(), NR.data(), NI.data(), s),
+          "rasterize_gaussians_batch (preprocess)");
+  }
+  std::vector<int64_t> layout = NI;
+  if (fitted) {
+    layout = capacity;
+  } else {
+    // two-phase, or the sync-free attempt's retry with the exact lengths
+    const int64_t nb = (int64_t)gs_batch_binning_buffer_bytes(C, NI.data());
+    binning = at::empty({nb > 1 ? nb : 1}, u8);
+    check(gs_forward_render_batch(&in.g, k.cams.data(), C, debug ? 1 : 0, (int)compat, geom.data_ptr(),
+                                  binning.data_ptr(), img.data_ptr(), NI.data(), radii.data_ptr<int32_t>(), oc, of, od,
+                                  oa, s),
+          "rasterize_gaussians_batch (render)");
+  }
   Tensor feature_map = in.F_user != in.F ? out_feature.narrow(1, 0, in.F_user) : out_feature;
-  return {NR, out_color, feature_map, out_depth, out_alpha, radii, geom, binning, img, NI};
+  std::vector<int64_t> hint_out = {h.valid, h.p1, h.q1, h.p2, h.max_len, h.total};
+  return {NR, out_color, feature_map, out_depth, out_alpha, radii, geom, binning, img, NI, layout, hint_out, fitted};
 }
 
 // [C, ch, H, W] fp32 of an upstream gradient (channels zero-padded to ch), or undefined

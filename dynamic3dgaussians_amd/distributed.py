@@ -11,6 +11,7 @@ all_reduce (train.py:288-290, external.py:136-140).
 """
 from __future__ import annotations
 
+import weakref
 from typing import Dict, Iterable, List, Mapping, Optional, Sequence, Tuple
 
 import torch
@@ -147,7 +148,11 @@ class GradBucket:
     each rank which parameters autograd accumulated into (post-accumulate
     hooks), sums those flags over the ranks in the same all_reduce, and after
     it sets .grad = None on the parameters no rank reached (one small
-    device->host read of the flags); zero_grad() binds them again.
+    device->host read of the flags); zero_grad() binds them again.  The
+    hooks hold the bucket only weakly and close() removes them: a parameter
+    that survives a densification (e.g. the reference's cam_m / cam_c) must
+    not keep every replaced bucket -- and its flat buffer -- alive, nor run
+    their stale hooks in every later backward.
     """
 
     def __init__(self, params: Iterable[torch.Tensor] | Mapping[str, torch.Tensor],
@@ -195,9 +200,27 @@ class GradBucket:
         self.resync()
 
     def _hook(self, i):
+        ref = weakref.ref(self)
+
         def mark(_p):
-            self._reached[i] = True
+            b = ref()
+            if b is not None:
+                b._reached[i] = True
         return mark
+
+    def close(self) -> None:
+        """Remove the reach-tracking hooks from the parameters (idempotent).
+        Call it when the bucket is replaced (a new bucket per timestep or
+        after a densification); a closed bucket no longer tracks reach."""
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
     # ---------------------------------------------------------------- checks
     def check_live(self) -> None:

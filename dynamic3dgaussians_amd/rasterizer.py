@@ -432,7 +432,7 @@ class _RasterizeGaussiansBatch(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, means3D, means2D, sh, colors_precomp, semantic_feature, opacities, scales, rotations,
-                cov3Ds_precomp, cams, label, densify_out, raw_params=False, feature_ready=None):
+                cov3Ds_precomp, cams, label, densify_out, raw_params=False, feature_ready=None, plan_state=None):
         if not isinstance(cams, _BatchCameras):
             cams = _BatchCameras(cams)
         rs0 = cams.rs0
@@ -449,7 +449,7 @@ class _RasterizeGaussiansBatch(torch.autograd.Function):
             rs0.bg, means3D, colors_precomp, semantic_feature, opacities, scales, rotations, rs0.scale_modifier,
             cov3Ds_precomp, views, projs, [p[0] for p in pp], [p[1] for p in pp], tx, ty, rs0.image_height,
             rs0.image_width, sh, rs0.sh_degree, cpos, rs0.prefiltered, rs0.debug, compat=compat,
-            activate=raw_params, windows=cams.windows, feature_ready=feature_ready)
+            activate=raw_params, windows=cams.windows, feature_ready=feature_ready, plan_state=plan_state)
         num_rendered, color, feature_map, depth, alpha, radii, geom, binning, img, num_instances = out
         ctx.rs0 = rs0
         ctx.cams = (views, projs, cpos, pp, tx, ty, cams.windows)
@@ -504,13 +504,14 @@ class _RasterizeGaussiansBatch(torch.autograd.Function):
             grad_rotations = grad_rotations * lab
             grad_cov3Ds_precomp = grad_cov3Ds_precomp * lab
         grads = (grad_means3D, grad_means2D, grad_sh, grad_colors_precomp, grad_semantic_feature,
-                 grad_opacities, grad_scales, grad_rotations, grad_cov3Ds_precomp, None, None, None, None, None)
+                 grad_opacities, grad_scales, grad_rotations, grad_cov3Ds_precomp, None, None, None, None, None,
+                 None)
         return tuple(g if need else None for g, need in zip(grads, ctx.needs_input_grad))
 
 
 def rasterize_gaussians_batch(means3D, means2D, sh, colors_precomp, semantic_feature, opacities, scales,
                               rotations, cov3Ds_precomp, settings_list, label=None, densify_out=None,
-                              raw_params=False, feature_ready=None):
+                              raw_params=False, feature_ready=None, plan_state=None):
     """rasterize_gaussians over a list of camera settings; outputs [C, ...]
     (color, radii, feature_map, depth, alpha).  `densify_out`: optional
     (accum, denom, max_radius) fp32 [P] tensors the backward fills with the
@@ -520,11 +521,12 @@ def rasterize_gaussians_batch(means3D, means2D, sh, colors_precomp, semantic_fea
     kernels apply sigmoid / exp / normalize and return their gradients.
     `feature_ready`: a recorded torch.cuda.Event the blend waits for before it
     reads semantic_feature (an overlapped optimizer update of the features on
-    another stream; gs_gaussians.feature_ready)."""
+    another stream; gs_gaussians.feature_ready).  `plan_state`: a
+    _C.BinningPlan for the sync-free forward (gs_forward_batch)."""
     cams = settings_list if isinstance(settings_list, _BatchCameras) else _BatchCameras(list(settings_list))
     return _RasterizeGaussiansBatch.apply(means3D, means2D, sh, colors_precomp, semantic_feature, opacities,
                                           scales, rotations, cov3Ds_precomp, cams, label, densify_out,
-                                          bool(raw_params), feature_ready)
+                                          bool(raw_params), feature_ready, plan_state)
 
 
 class GaussianRasterizerBatch(nn.Module):
@@ -543,11 +545,20 @@ class GaussianRasterizerBatch(nn.Module):
     unnorm_rotations: helpers.py:98-107 params2rendervar) and applies the
     activations -- sigmoid, exp, F.normalize -- inside the preprocess kernels,
     forward and backward (GS_FLAG_ACTIVATE): the same step without the ~20
-    elementwise launches of the activations and their autograd backward."""
+    elementwise launches of the activations and their autograd backward.
 
-    def __init__(self, settings_list, track_densify=False, raw_params=False):
+    `sync_free=True` (the default): the forward does not wait for the host
+    between the plan and the render stages (gs_forward_batch, ABI 11): the
+    binning buffer is sized from the previous call's list lengths (a
+    _C.BinningPlan kept in `self.plan`) and the headers are read after every
+    stage is enqueued; a call whose lists outgrow it is rendered again with
+    the exact lengths.  Outputs and gradients are bit-identical to
+    sync_free=False (the reference's two-phase order)."""
+
+    def __init__(self, settings_list, track_densify=False, raw_params=False, sync_free=True):
         super().__init__()
         self.settings_list = list(settings_list)
+        self.plan = _C.BinningPlan() if sync_free else None
         self._cams = _BatchCameras(self.settings_list)
         if track_densify and self._cams.windows is not None:
             raise ValueError("densification statistics need whole-image cameras: a tile window counts a "
@@ -581,7 +592,7 @@ class GaussianRasterizerBatch(nn.Module):
             self.densify_stats = {"means2D_gradient_accum": dens[0], "denom": dens[1], "max_2D_radius": dens[2]}
         color, radii, feature_map, depth, alpha = rasterize_gaussians_batch(
             means3D, means2D, shs, colors_precomp, semantic_feature, opacities, scales, rotations,
-            cov3D_precomp, self._cams, lab, dens, self.raw_params, feature_ready)
+            cov3D_precomp, self._cams, lab, dens, self.raw_params, feature_ready, self.plan)
         has_sem = semantic_feature is not None
         if has_label and has_sem:      # G3
             return color, radii, feature_map, depth, alpha

@@ -173,19 +173,27 @@ class TimestepDriver:
 
     Densification statistics: the loss divides every camera's image loss by
     n_cams (the rig's mean), so each camera's means2D gradient is 1/n_cams of
-    the reference's one-camera-per-step gradient (train.py:422-425); the
-    statistic external.py:136-140 accumulates is the NORM of that gradient
-    (compared with an absolute threshold, external.py:247-259), so the
-    driver scales the increments back by n_cams: means2D_gradient_accum
-    holds the reference's per-view norms (the image loss being the only
-    term that reaches means2D, as in train.py's get_loss)."""
+    a one-camera-per-step gradient (train.py:422-425); the statistic
+    external.py:136-140 accumulates is the NORM of that gradient (compared
+    with an absolute threshold, external.py:247-259), so the driver scales
+    the increments by `stat_scale` (default n_cams): means2D_gradient_accum
+    then holds per-view norms of an image loss of weight 1 that is the only
+    term reaching means2D -- the loss of dyn_train.py (loss_weights['im'] =
+    1).  The shipped train.py differs: it sets loss_weights['im'] = 0.0
+    (train.py:284), and its means2D gradient comes from stat_im (weight
+    0.01, averaged over the stat cameras sharing one means2D,
+    train.py:186-243) plus depth; a caller reproducing that weighting
+    passes its own `stat_scale`.  That train.py variant is parity unpinned:
+    the reference ships no fixture of its statistics."""
 
     def __init__(self, params: dict, variables: dict, optimizer, n_cams: int, render: Callable,
                  rank: int = 0, world: int = 1, group=None,
                  image_loss: Callable = l1_image_loss, extra_loss: Optional[Callable] = None,
-                 densify: Optional[Callable] = None, targets_sharded: bool = False):
+                 densify: Optional[Callable] = None, targets_sharded: bool = False,
+                 stat_scale: Optional[float] = None):
         self.params, self.variables, self.optimizer = params, variables, optimizer
         self.n_cams = n_cams
+        self.stat_scale = float(n_cams if stat_scale is None else stat_scale)
         self.targets_sharded = targets_sharded
         self.cams = shard_cameras(n_cams, rank, world)
         self.rank, self.world, self.group = rank, world, group
@@ -200,6 +208,10 @@ class TimestepDriver:
         self._new_bucket()
 
     def _new_bucket(self):
+        # the replaced bucket's reach hooks come off the parameters that
+        # survive (GradBucket.close)
+        if self.bucket is not None:
+            self.bucket.close()
         # the optimizer's parameters (seg_colors and other constants stay out)
         names = {g.get("name") for g in self.optimizer.param_groups}
         keys = [k for k in self.params if k in names]
@@ -242,7 +254,7 @@ class TimestepDriver:
             if stats is not None:
                 # this rank's cameras' statistics (external.py:136-140,
                 # train.py:288-290); the bucket sums the increments
-                v["means2D_gradient_accum"] += stats["means2D_gradient_accum"] * float(self.n_cams)
+                v["means2D_gradient_accum"] += stats["means2D_gradient_accum"] * self.stat_scale
                 v["denom"] += stats["denom"]
                 torch.maximum(v["max_2D_radius"], stats["max_2D_radius"], out=v["max_2D_radius"])
             bucket.all_reduce(self.group)

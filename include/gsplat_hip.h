@@ -22,7 +22,8 @@
  *    (DGR/rasterize_points.h); the Python layer decides what it passes.
  *  - All work is enqueued on `stream`; gs_forward_plan performs the one
  *    device->host read the reference also performs (num_rendered,
- *    CR/rasterizer_impl.cu:287).
+ *    CR/rasterizer_impl.cu:287).  gs_forward_batch (ABI 11) performs it after
+ *    every forward stage is enqueued, so the GPU does not wait for the host.
  */
 #ifndef GSPLAT_HIP_H
 #define GSPLAT_HIP_H
@@ -34,7 +35,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 10
+#define GS_ABI_VERSION 11
 
 /* compat modes: numerics of the as-shipped reference vs corrected ones */
 #define GS_COMPAT_REFERENCE 0
@@ -243,6 +244,46 @@ int gs_backward_batch(const gs_gaussians *g, const gs_camera *cams, int32_t C,
                       float *dL_dmeans2D, float *dL_dcolors, float *dL_dsemantic,
                       float *dL_dopacity, float *dL_dmeans3D, float *dL_dcov3D, float *dL_dsh,
                       float *dL_dscales, float *dL_drotations, gs_stream_t stream);
+
+/* ---- sync-free batch forward (ABI 11; no reference analogue).
+ * gs_forward_plan_batch + gs_forward_render_batch in one call without the
+ * host round trip between them (the reference reads num_rendered back before
+ * it can size the binning buffer, CR/rasterizer_impl.cu:283-287, and the GPU
+ * idles while the host does):
+ *  - the binning buffer is laid out for capacity[c] instances of camera c
+ *    (gs_batch_binning_buffer_bytes(C, capacity)), e.g. the previous step's
+ *    num_instances with a margin;
+ *  - the tile sort's launches are sized from *hint (the previous call's plan,
+ *    written back by this call; hint->valid = 0 or hint = NULL: launches
+ *    that cover every tile);
+ *  - the plan headers reach page-locked host memory behind the plan kernels
+ *    and the call waits for them only after the bucket, sort and blend
+ *    launches are enqueued.
+ * On return *fits = 1: every camera's lists fit its capacity and every tile
+ * was sorted -- the outputs are complete and bit-identical to the two-phase
+ * path's, num_rendered / num_instances as from gs_forward_plan_batch.
+ * *fits = 0: some camera's lists exceed its capacity (or a tile lay outside
+ * the hinted sort launches); the kernels stored nothing into the binning
+ * buffer beyond it and the outputs are NOT valid.  num_instances holds the
+ * exact counts and the plan stays valid: size a binning buffer with
+ * gs_batch_binning_buffer_bytes(C, num_instances) and call
+ * gs_forward_render_batch with it and num_instances (the retry; its outputs
+ * are those of the two-phase path).  The backward takes the per-camera
+ * lengths the binning buffer of the forward it follows was laid out with
+ * (capacity when *fits = 1, num_instances after a retry). */
+typedef struct gs_batch_hint {
+  int32_t valid;                /* 0 until a call wrote it */
+  int32_t p1, q1, p2;           /* the plan's sort-class extents (opaque) */
+  int64_t max_len;              /* the longest tile list */
+  int64_t total;                /* the batch's list instances */
+} gs_batch_hint;
+
+int gs_forward_batch(const gs_gaussians *g, const gs_camera *cams, int32_t C, int prefiltered,
+                     int compat, void *geom_buffer, void *image_buffer, void *binning_buffer,
+                     const int64_t *capacity, gs_batch_hint *hint, int32_t *radii,
+                     int64_t *num_rendered, int64_t *num_instances, int32_t *fits,
+                     float *out_color, float *out_feature, float *out_depth, float *out_alpha,
+                     gs_stream_t stream);
 
 /* markVisible -- replaces DGR/rasterize_points.cu:227-246 and
  * CR/rasterizer_impl.cu:141-153 (checkFrustum).  present[P] is 0/1 bytes. */

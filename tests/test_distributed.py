@@ -409,3 +409,38 @@ def test_bucket_async_all_reduce_on_alternating_buffers():
         assert len(res[r]) == 4
         for s_, g in enumerate(res[r]):
             np.testing.assert_array_equal(g, np.full(21, 3.0 + 2 * s_, np.float32))
+
+
+def test_replaced_bucket_releases_surviving_parameters_hooks():
+    """with track_reached, each parameter carries a post-accumulate
+    hook.  A parameter that survives a densification (the reference keeps
+    cam_m / cam_c, external.py:185,253,263) must not keep the replaced bucket
+    and its flat buffer alive, nor run its stale hook in later backwards:
+    TimestepDriver closes the old bucket, and the hooks hold it weakly."""
+    import gc
+    import weakref
+
+    from dynamic3dgaussians_amd.timesteps import TimestepDriver
+
+    P = 64
+    params = {"means3D": torch.nn.Parameter(torch.randn(P, 3)), "cam_m": torch.nn.Parameter(torch.zeros(1, 3))}
+    opt = torch.optim.Adam([{"params": [v], "name": k, "lr": 1e-3} for k, v in params.items()])
+    drv = TimestepDriver(params, {}, opt, 1, render=lambda rv, cams: (None, None), world=2)
+    old = weakref.ref(drv.bucket)
+    # densification: means3D replaced, cam_m survives
+    params["means3D"] = torch.nn.Parameter(torch.randn(2 * P, 3))
+    opt.param_groups[0]["params"][0] = params["means3D"]
+    drv._live_bucket()  # stale -> a new bucket
+    gc.collect()
+    assert old() is None, "the replaced bucket is still referenced (a surviving parameter's hook?)"
+    # exactly one live hook on the surviving parameter: the new bucket's
+    drv.bucket.zero_grad()
+    (params["cam_m"].sum() * 2 + params["means3D"].sum()).backward()
+    assert drv.bucket._reached == [True, True]
+    n_hooks = len(params["cam_m"]._post_accumulate_grad_hooks or {})
+    assert n_hooks == 1, n_hooks
+    # a bucket closed by hand stops tracking; close() is idempotent
+    b = GradBucket({"cam_m": params["cam_m"]}, bind_grads=True, track_reached=True)
+    b.close()
+    b.close()
+    assert len(params["cam_m"]._post_accumulate_grad_hooks or {}) == 1

@@ -64,8 +64,19 @@ def test_window_pixels_equal_the_whole_render(compat, P=20000, W=200, H=152, F=3
             assert not torch.any(t[k][:, ~m]), k
 
 
-def test_window_gradients_sum_to_the_whole_camera(P=20000, W=200, H=152, F=32):
+@pytest.mark.parametrize("raw_params", [False, True])
+@pytest.mark.parametrize("compat", ["reference", "fixed"])
+def test_window_gradients_sum_to_the_whole_camera(compat, raw_params, P=20000, W=200, H=152, F=32):
+    """Both numerics (fixed mode's per-pixel T_final * bg term and its f.dL/dF
+    feeding dL/dalpha) and the raw parameters (GS_FLAG_ACTIVATE): the
+    bench's window split runs the latter."""
     src = _scene(P, F, seed=3)
+    if raw_params:
+        # params2rendervar's inputs (helpers.py:98-107): logit, log, an
+        # unnormalised quaternion
+        src["opacities"] = torch.logit(src["opacities"])
+        src["scales"] = torch.log(src["scales"])
+        src["rotations"] = src["rotations"] * 1.7
     cams = camera_rig(5, W, H)
     gx, gy = (W + 15) // 16, (H + 15) // 16
     # camera 1 whole, camera 3 as a partition of 4 windows (row bands and a split band)
@@ -76,11 +87,11 @@ def test_window_gradients_sum_to_the_whole_camera(P=20000, W=200, H=152, F=32):
     lab = torch.ones(P, device=DEV)
 
     def grads(entries):
-        sets = _settings([cams[c] for c, _ in entries], W, H, [w for _, w in entries])
+        sets = _settings([cams[c] for c, _ in entries], W, H, [w for _, w in entries], compat)
         leaves = {k: v.clone().requires_grad_(True) for k, v in src.items()}
         n = len(entries)
-        im, _, feat, depth, _ = GaussianRasterizerBatch(sets)(means2D=torch.zeros(P, 3, device=DEV), label=lab,
-                                                             **leaves)
+        im, _, feat, depth, _ = GaussianRasterizerBatch(sets, raw_params=raw_params)(
+            means2D=torch.zeros(P, 3, device=DEV), label=lab, **leaves)
         torch.autograd.backward([im, depth, feat], [u.expand(n, -1, -1, -1) for u in up])
         return {k: v.grad for k, v in leaves.items()}
 
