@@ -184,17 +184,38 @@ def raw_rendervar(params, label, means2D):
     return rv
 
 
-def split_shard(n_cams, rank, world, how, W, H, row_cost=None):
+# One more camera piece costs a rank its projection and binning launches and
+# launch tails.  Measured in isolation (tools/piece_cost.py: the same pixels
+# of one camera as 1 / 2 / 3 pieces): 0.152 of a camera's step time (51 vs
+# 337 us; profiles/r05pc/piece_cost.json).  In the split itself the ranks
+# holding a second left-over camera's piece ran 0.058 ms above the others at
+# equal modelled load (the second piece is another camera's projection and
+# plan; profiles/r05px: 1.403-1.406 vs 1.30-1.38 ms), i.e. about 0.32 of a
+# camera per piece: the model charges that.  (A model of every camera's
+# measured one-camera step instead of its tile-list instances did not predict
+# the batched ranks better, 1.30-1.45 ms, and varied run to run:
+# profiles/r05px2.)
+PIECE_FRACTION = 0.32
+
+
+def split_shard(n_cams, rank, world, how, W, H, costs=None):
     """[(camera, tile window or None)] of `rank` in a `world`-rank split of an
-    n_cams rig (--split; windows balanced by `row_cost`, rig_row_costs)."""
+    n_cams rig (--split; windows balanced by `costs` = (row_cost, piece_cost),
+    rig_costs)."""
     if how == "cameras":
         return [(c, None) for c in shard_cameras(n_cams, rank, world)]
-    # one more camera piece costs a rank its projection and binning launches:
-    # about a fifth of a camera's work at the bench scene (per-rank proxies,
-    # DESIGN.md 6.2)
-    piece = 0.0 if row_cost is None else 0.2 * sum(sum(r) for r in row_cost) / len(row_cost)
+    row_cost, piece = costs if costs is not None else (None, 0.0)
     return shard_camera_windows(n_cams, rank, world, (W + 15) // 16, (H + 15) // 16, row_cost=row_cost,
                                 piece_cost=piece)
+
+
+def rig_costs(rig, params, label, args, dev):
+    """The work model of --split windows: per camera and tile row the
+    instances of the row's tile lists (rig_row_costs), and the fixed cost of
+    one more camera piece, PIECE_FRACTION of a mean camera's instances.
+    Returns (row_cost, piece_cost)."""
+    rows = rig_row_costs(rig, params, label, args, dev)
+    return rows, PIECE_FRACTION * sum(sum(r) for r in rows) / len(rows)
 
 
 def rig_row_costs(rig, params, label, args, dev):
@@ -499,7 +520,7 @@ def main():
         if args.split == "cameras" and args.cams_total < s_world:
             raise SystemExit(f"--cams-total {args.cams_total} < {s_world} ranks")
         rig = camera_rig(args.cams_total, args.width, args.height, seed=args.seed)
-        costs = rig_row_costs(rig, params, label, args, dev) if args.split == "windows" else None
+        costs = rig_costs(rig, params, label, args, dev) if args.split == "windows" else None
         shard = split_shard(args.cams_total, s_rank, s_world, args.split, args.width, args.height, costs)
         my_cams = [rig[c] for c, _ in shard]
         if any(w is not None for _, w in shard):
@@ -862,7 +883,7 @@ def main():
         n_split = args.cams
         if world > 1:
             rig_s = camera_rig(n_split, args.width, args.height, seed=args.seed)
-            costs_s = rig_row_costs(rig_s, params0, label, args, dev) if args.split == "windows" else None
+            costs_s = rig_costs(rig_s, params0, label, args, dev) if args.split == "windows" else None
             mine = split_shard(n_split, rank, world, args.split, args.width, args.height, costs_s)
             wins = [w for _, w in mine] if any(w is not None for _, w in mine) else None
             parts_s = batch_inputs(make_settings([rig_s[c] for c, _ in mine], dev, args.compat, None, wins),
@@ -970,6 +991,24 @@ def main():
         "instances_per_cam": int(np.mean([L for L, _, _ in inst])),
         "num_rendered_per_cam": int(np.mean([R for _, _, R in inst])),
     }
+    if strong:
+        # the split's work model: every rank's pieces and modelled load
+        # (row_cost instances + PIECE_FRACTION x a mean camera per piece)
+        s_world = args.proxy_world if args.proxy_world else world
+        gx_, gy_ = (W_ + 15) // 16, (H_ + 15) // 16
+        model = []
+        rc_, pc_ = costs if costs is not None else (None, 0.0)
+        for r_ in range(s_world):
+            sh_ = split_shard(args.cams_total, r_, s_world, args.split, W_, H_, costs)
+            load = 0.0
+            for c_, w_ in sh_:
+                rows = range(gy_) if w_ is None else range(w_[1], w_[3])
+                load += (sum(rc_[c_][y] for y in rows) + pc_) if rc_ is not None else 0.0
+            model.append({"rank": r_, "pieces": len(sh_), "model_ms": round(load, 4),
+                          "shard": [[c_, w_] for c_, w_ in sh_]})
+        result["split_model"] = {"piece_fraction": PIECE_FRACTION, "piece_ms": round(pc_, 4),
+                                 "camera_ms": [round(sum(r) + pc_, 4) for r in rc_] if rc_ else None,
+                                 "ranks": model}
     if args.step_times:
         result["host_step_ms"] = [round((b - a) * 1e3, 3) for a, b in zip([t0] + host_marks, host_marks)]
         result["tail_ms"] = round((t0 + elapsed - host_marks[-1]) * 1e3, 3) if world == 1 else None

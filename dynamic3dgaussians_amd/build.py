@@ -53,6 +53,7 @@ SOURCES = {
     "gs_optim.hip": ["-ffp-contract=off"],
     "gs_knn.hip": ["-ffp-contract=off"],
     "gs_api.hip": [],
+    "gs_host.cpp": [],  # host-only C++ (also built by oracle/Makefile's sanitizer target)
 }
 COMMON = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall",
           "-Wno-unused-function", "-I", CSRC, "-I", INCLUDE]
@@ -95,8 +96,12 @@ def build(force: bool = False, verbose: bool = False) -> str:
 
     def compile_one(item):
         src, extra = item
-        obj = os.path.join(BUILD_DIR, src.replace(".hip", ".o"))
-        cmd = [cc, *COMMON, *VARIANT_FLAGS[VARIANT], *extra, "-c", os.path.join(CSRC, src), "-o", obj]
+        obj = os.path.join(BUILD_DIR, os.path.splitext(src)[0] + ".o")
+        if src.endswith(".cpp"):  # host-only translation unit
+            cmd = [cc, "-x", "c++", "-O3", "-std=c++17", "-fPIC", "-Wall", "-I", CSRC, "-I", INCLUDE, *extra,
+                   "-c", os.path.join(CSRC, src), "-o", obj]
+        else:
+            cmd = [cc, *COMMON, *VARIANT_FLAGS[VARIANT], *extra, "-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)

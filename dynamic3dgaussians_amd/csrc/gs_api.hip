@@ -24,18 +24,8 @@
 using namespace gs;
 
 namespace {
-thread_local std::string g_err;
-
-int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
-int fail(int code, const char* fmt, ...) {
-  char buf[512];
-  va_list ap;
-  va_start(ap, fmt);
-  vsnprintf(buf, sizeof(buf), fmt, ap);
-  va_end(ap);
-  g_err = buf;
-  return code;
-}
+// the thread's error message (gs_host.cpp: gs_last_error)
+#define fail gs_set_error
 
 // Post-launch check: always catch launch errors; with `debug`, also
 // synchronise and surface asynchronous faults (the reference's CHECK_CUDA
@@ -300,7 +290,6 @@ int gs_timing_read(double* ms, int64_t* count, int n_kinds) {
 }
 
 int gs_version(void) { return GS_ABI_VERSION; }
-const char* gs_last_error(void) { return g_err.c_str(); }
 
 size_t gs_geom_buffer_bytes(int64_t P) { return GeomLayout(P > 0 ? P : 0).total; }
 size_t gs_binning_buffer_bytes(int64_t L) { return BinLayout(L > 0 ? L : 0).total; }
@@ -373,54 +362,8 @@ static size_t feat_pad_bytes(int64_t P, int32_t F) {
 }
 
 // ---------------------------------------------------------------- debug checks
-// Host-side validation of the forward's state under `debug` (gsplat_hip.h).
-
-extern "C" int gs_check_plan_header(const uint32_t* hdr, int64_t tiles) {
-  if (!hdr) return fail(-1, "plan header: null");
-  const uint64_t L = hdr[M_L], maxn = hdr[M_MAXN], lref = hdr[M_LREF], st = hdr[M_STATUS];
-  const uint64_t p1 = hdr[M_SORT_P1], q1 = hdr[M_SORT_Q1], p2 = hdr[M_SORT_P2];
-  if (st > 3u) return fail(-3, "plan header: status word %llu has unknown bits", (unsigned long long)st);
-  if (L > lref)
-    return fail(-3, "plan header: %llu list instances exceed the %llu bounding-rect instances",
-                (unsigned long long)L, (unsigned long long)lref);
-  if (maxn > L)
-    return fail(-3, "plan header: longest tile %llu > %llu instances", (unsigned long long)maxn,
-                (unsigned long long)L);
-  if (p1 > (uint64_t)tiles || p2 > p1 || q1 > p1)
-    return fail(-3, "plan header: sort-class prefixes p1=%llu q1=%llu p2=%llu inconsistent with %lld tiles",
-                (unsigned long long)p1, (unsigned long long)q1, (unsigned long long)p2, (long long)tiles);
-  return 0;
-}
-
-extern "C" int gs_check_ranges(const uint32_t* ranges, int64_t tiles, int64_t L, int64_t max_len) {
-  if (!ranges && tiles > 0) return fail(-1, "ranges: null");
-  int64_t next = 0;
-  for (int64_t t = 0; t < tiles; ++t) {
-    const int64_t a = ranges[2 * t], b = ranges[2 * t + 1];
-    if (b < a || b > L)
-      return fail(-3, "ranges: tile %lld has [%lld, %lld) outside [0, %lld]", (long long)t, (long long)a,
-                  (long long)b, (long long)L);
-    if (b > a) {
-      if (a != next)
-        return fail(-3, "ranges: tile %lld starts at %lld, expected %lld (lists not contiguous)", (long long)t,
-                    (long long)a, (long long)next);
-      if (max_len >= 0 && b - a > max_len)
-        return fail(-3, "ranges: tile %lld holds %lld instances > the planned longest %lld", (long long)t,
-                    (long long)(b - a), (long long)max_len);
-      next = b;
-    }
-  }
-  if (next != L) return fail(-3, "ranges: lists cover %lld of %lld instances", (long long)next, (long long)L);
-  return 0;
-}
-
-extern "C" int gs_check_point_list(const uint32_t* ids, int64_t L, int64_t P) {
-  if (!ids && L > 0) return fail(-1, "point list: null");
-  for (int64_t i = 0; i < L; ++i)
-    if ((int64_t)ids[i] >= P)
-      return fail(-3, "point list: entry %lld holds Gaussian id %u >= P = %lld", (long long)i, ids[i], (long long)P);
-  return 0;
-}
+// Host-side validation of the forward's state under `debug` (gsplat_hip.h):
+// gs_check_plan_header / gs_check_ranges / gs_check_point_list, gs_host.cpp.
 
 // debug mode, after the sort: every camera's ranges and list ids, read back
 static int debug_check_lists(const TileArgs& ta, const CamBatch& cb, const void* binning, const int64_t* L,

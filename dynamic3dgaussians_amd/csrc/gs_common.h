@@ -7,6 +7,8 @@
 
 #include <type_traits>
 
+#include "gs_meta.h"
+
 namespace gs {
 
 // Binning tile = 16x16 pixels, identical to the reference (CR/config.h:18-19)
@@ -132,13 +134,8 @@ struct SortLayout {
 };
 
 // Image buffer (per pixel / per tile), also the binning plan: per-block tile
-// histograms (turned into per-block offsets), tile totals and a 4-word
-// header {L, max tile length, -, status}.
-// header: M_L = list instances (after the exact tile test), M_LREF = the
-// reference's num_rendered (bounding-rect instances), longest tile, status
-enum ImgMeta { M_L = 0, M_MAXN = 1, M_LREF = 2, M_STATUS = 3,
-               // tile-order prefixes for the sort launches (tile_offsets_kernel)
-               M_SORT_P1 = 4, M_SORT_Q1 = 5, M_SORT_P2 = 6, M_WORDS = 8 };
+// histograms (turned into per-block offsets), tile totals and the 8-word
+// header (gs_meta.h).
 struct ImgLayout {
   size_t ranges, n_contrib, thist, ttotal, bsum, meta, order, smax, total;
   int64_t tiles;
