@@ -236,3 +236,50 @@ def test_flat_backward_buffers_carving(P, F, M):
     ov = _C.carve_buffers(other, offs)
     for k in views:
         torch.testing.assert_close(summed[k], views[k] + ov[k], rtol=0, atol=0)
+
+
+def _header_struct_fields(name):
+    """Field names of `typedef struct <name> { ... } <name>;` in include/gsplat_hip.h, in order."""
+    import re
+    src = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include",
+                            "gsplat_hip.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (name, name), src, flags=re.S).group(1)
+    names = []
+    for decl in body.split(";"):
+        decl = decl.strip()
+        if not decl:
+            continue
+        # "float c_x, c_y, tan_fovx" / "const float *means3D" / "int32_t tile_x0, tile_y0"
+        first, *rest = [p.strip() for p in decl.split(",")]
+        names.append(re.findall(r"[A-Za-z_]\w*", first)[-1])
+        names += [re.findall(r"[A-Za-z_]\w*", p)[-1] for p in rest]
+    return names
+
+
+@pytest.mark.parametrize("struct,mirror", [("gs_gaussians", "GsGaussians"), ("gs_camera", "GsCamera"),
+                                           ("gs_batch_hint", "GsBatchHint")])
+def test_ctypes_structs_mirror_the_header(struct, mirror):
+    """The ctypes mirrors name the header's fields in order (ctypes would
+    silently accept a stale keyword as a plain attribute)."""
+    fields = [f for f, _ in getattr(_lib, mirror)._fields_]
+    assert fields == _header_struct_fields(struct)
+
+
+def test_integration_stub_uses_real_field_names():
+    """INTEGRATION.md's ctypes stub passes only field names of the structs."""
+    import re
+    doc = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "INTEGRATION.md")).read()
+    for mirror in ("GsGaussians", "GsCamera"):
+        fields = {f for f, _ in getattr(_lib, mirror)._fields_}
+        calls = []
+        for m in re.finditer(r"%s\(" % mirror, doc):
+            depth, i = 1, m.end()
+            while depth:
+                depth += {"(": 1, ")": -1}.get(doc[i], 0)
+                i += 1
+            calls.append(re.sub(r"#[^\n]*", "", doc[m.end():i - 1]))
+        assert calls, mirror
+        for call in calls:
+            for kw in re.findall(r"(\w+)=", call):
+                assert kw in fields, (mirror, kw)
