@@ -41,8 +41,6 @@ VARIANT_FLAGS = {"": [], "stats": ["-DGS_STATS"], "stamps": ["-DGS_STAMPS"],
                  "exp_noatomic": ["-DGS_EXP_NO_FEAT_ATOMIC", "-DGS_EXP_NO_ACC_ATOMIC"],
                  "exp_fwd_nofeatst": ["-DGS_EXP_FWD_NO_FEAT_STORE"],  # traffic of the feature planes
                  "exp_fwd_featnt": ["-DGS_EXP_FWD_FEAT_NT"],
-                 "exp_bwd_nosmask": ["-DGS_EXP_BWD_NO_SMASK"],  # the round-4 backward (strip tests)
-                 "exp_bwd_mloads": ["-DGS_EXP_BWD_MASKED_LOADS"],  # only the survivors' records fetched
                  "ctl": []}  # the product's flags under a variant's (ctypes) binding: the A/B control
 ARCH = os.environ.get("GSPLAT_OFFLOAD_ARCH", "gfx950")
 

@@ -119,18 +119,6 @@ struct BinLayout {
   }
 };
 
-// Per-(strip, chunk) survivor masks of the forward blend: the ballot of a
-// strip's strip_culled tests over a 64-entry chunk of its tile's list,
-// handed to the backward (which then skips the test and the culled records)
-// in the binning buffer's key areas -- dead once the tile sort has written
-// the id lists.  Chunk k of tile t (list range [x, y)) has slot
-// x / 64 + t + k, unique per tile (a later tile's first slot is past this
-// tile's last: floor((x + n) / 64) + 2 > floor(x / 64) + ceil(n / 64)), 4
-// strips per slot: 32 B x (L / 64 + T + 1) in the 16 B x L of keys + keys2.
-// A layout too small for that (tiny lists over many tiles) keeps no masks:
-// the backward tests every record itself, with the same result.
-__host__ __device__ inline bool smask_fits(int64_t L, int64_t T) { return 16 * L >= 32 * (L / 64 + T + 1); }
-
 // Scratch of the standalone radix sort entry point (gs_sort_pairs).
 struct SortLayout {
   size_t keys1, vals1, hist, rowtot, total;

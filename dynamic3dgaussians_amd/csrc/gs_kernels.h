@@ -76,7 +76,6 @@ struct RenderArgs {
   const float* rec;
   const float* feats;  // P x F
   uint32_t* smax;      // 4 x num_tiles: per strip item (dispatch order) the longest pixel walk (max n_contrib)
-  uint64_t* smask;     // per (tile chunk slot, strip) survivor masks for the backward, or null (smask_fits)
   const float* bg;     // 3
   float* out_color;
   float* out_feature;
@@ -104,7 +103,6 @@ struct RenderBwdArgs {
   const float* feats;
   const float* bg;
   const uint32_t* smax;  // 4 x num_tiles: the forward's per-strip walk lengths
-  const uint64_t* smask; // the forward's per-(chunk slot, strip) survivor masks, or null
   const float* alphas;
   const uint32_t* n_contrib;
   const float* dL_dpix;
@@ -233,9 +231,6 @@ __host__ __device__ inline RenderArgs cam_render_args(const RenderArgs& a0, cons
   a.n_contrib = shift_bytes(a0.n_contrib, io);
   a.rec = shift_bytes(a0.rec, go);
   a.point_list = shift_bytes(a0.point_list, cb.bin_off[c]);
-  a.smask = a.point_list && smask_fits(cb.bin_L[c], a0.num_tiles)
-                ? reinterpret_cast<uint64_t*>(reinterpret_cast<uintptr_t>(a.point_list) + BinLayout(cb.bin_L[c]).keys)
-                : nullptr;
   a.out_color = a0.out_color ? a0.out_color + c * 3 * hw : nullptr;
   a.out_feature = a0.out_feature ? a0.out_feature + c * a0.F * hw : nullptr;
   a.out_depth = a0.out_depth ? a0.out_depth + c * hw : nullptr;
@@ -251,14 +246,6 @@ __host__ __device__ inline RenderBwdArgs cam_render_bwd_args(const RenderBwdArgs
   a.n_contrib = shift_bytes(a0.n_contrib, io);
   a.rec = shift_bytes(a0.rec, go);
   a.point_list = shift_bytes(a0.point_list, cb.bin_off[c]);
-#ifdef GS_EXP_BWD_NO_SMASK  // the round-4 backward: every record tested again
-  a.smask = nullptr;
-#else
-  a.smask = a.point_list && smask_fits(cb.bin_L[c], a0.num_tiles)
-                ? reinterpret_cast<const uint64_t*>(reinterpret_cast<uintptr_t>(a.point_list) +
-                                                    BinLayout(cb.bin_L[c]).keys)
-                : nullptr;
-#endif
   a.alphas = a0.alphas ? a0.alphas + c * hw : nullptr;
   a.dL_dpix = a0.dL_dpix ? a0.dL_dpix + c * 3 * hw : nullptr;
   a.dL_dfeat = a0.dL_dfeat ? a0.dL_dfeat + c * a0.F * hw : nullptr;

@@ -533,8 +533,6 @@ __global__ __launch_bounds__(64 * WPB_FWD) __attribute__((amdgpu_waves_per_eu(fw
   };
 
   const uint32_t lastv = range.y > range.x ? range.y - 1 : range.x;
-  uint64_t* __restrict__ smask = ca.smask;
-  const uint32_t mbase = range.x / CHUNK + (uint32_t)tile;  // the tile's first survivor-mask slot
   // Records are prefetched one chunk ahead and their list ids two chunks
   // ahead, so the id -> record dependent load never waits inside a chunk.
   RecRegs q;
@@ -560,8 +558,6 @@ __global__ __launch_bounds__(64 * WPB_FWD) __attribute__((amdgpu_waves_per_eu(fw
     }
     const uint32_t chunk_gid = q.gid;  // lane j: id of the chunk's j-th record
     uint64_t mask = __ballot(keep);
-    // the backward's survivors of this chunk (gs_common.h smask_fits)
-    if (smask && lane == 0) smask[4 * (mbase + (c0 - range.x) / CHUNK) + wave] = mask;
     const uint32_t lbase = c0 - range.x + 1;
     STAT(0, 1);
     STAT(1, range.y - c0 < CHUNK ? range.y - c0 : CHUNK);
@@ -1208,42 +1204,14 @@ __global__ __launch_bounds__(64 * WPB_BWD) __attribute__((amdgpu_waves_per_eu(bw
   STAT(14, 1);
   STAT(15, wmax);
   STAT_DECL(st_it);
-  // The walk goes down the list in the forward's chunks (aligned to the
-  // list's start), so each chunk's survivors are the forward's ballot
-  // (smask): no strip test here, the same survivors in the same order.
-  const uint64_t* __restrict__ smask = ca.smask;
-  const uint32_t mbase = range.x / CHUNK + (uint32_t)tile;
-  const int kfirst = wmax > 0 ? (int)((wmax - 1) / CHUNK) : -1;  // the top chunk
-  // The survivor masks of up to 64 chunks in one vector load (lane i: chunk
-  // kbase - i), read out per chunk with v_readlane: per-chunk scalar loads
-  // were waited for at every chunk top (scalar loads complete out of order,
-  // so each use waits for all of them): render_bwd 5.22-5.36 vs 5.02-5.05 ms
-  // without masks (profiles/r05/).
-  uint32_t mlo = 0u, mhi = 0u;
-  int kbase = kfirst;
-  auto load_masks = [&](int kb) {
-    const int k = kb - lane;
-    if (smask && k >= 0) {
-      const uint64_t m = smask[4 * (mbase + (uint32_t)k) + wave];
-      mlo = (uint32_t)m;
-      mhi = (uint32_t)(m >> 32);
-    }
-  };
-  load_masks(kbase);
-  auto mask_at = [&](int kk) -> uint64_t {
-    const int i = kbase - kk;
-    return ((uint64_t)__builtin_amdgcn_readlane(mhi, i) << 32) | (uint64_t)__builtin_amdgcn_readlane(mlo, i);
-  };
-  uint64_t mcur = smask && kfirst >= 0 ? mask_at(kfirst) : 0ull;
+  // records one chunk ahead, list ids two chunks ahead (see the forward)
   RecRegs q;
   uint32_t gnext = 0;
-  if (kfirst >= 0) {
-    const uint32_t c0 = range.x + (uint32_t)kfirst * CHUNK;
-#ifdef GS_EXP_BWD_MASKED_LOADS
-    if (!smask || ((mcur >> lane) & 1ull))
-#endif
-      q = load_rec(point_list, rec, c0 + lane, top - 1);
-    gnext = load_gid(point_list, (kfirst >= 1 ? c0 - CHUNK : range.x) + lane, top - 1);
+  if (top > range.x) {
+    const uint32_t c0 = top > range.x + CHUNK ? top - CHUNK : range.x;
+    q = load_rec(point_list, rec, c0 + lane, top - 1);
+    const uint32_t n0 = c0 > range.x + CHUNK ? c0 - CHUNK : range.x;
+    gnext = load_gid(point_list, n0 + lane, top - 1);
   }
 #ifdef GS_STAMPS
 #ifdef GS_STAMPS_FINE
@@ -1252,23 +1220,9 @@ __global__ __launch_bounds__(64 * WPB_BWD) __attribute__((amdgpu_waves_per_eu(bw
   FINE_STAMP(tD);
   const unsigned long long ts1 = stamp();
 #endif
-  for (int kk = kfirst; kk >= 0; --kk) {
-    const uint32_t c0 = range.x + (uint32_t)kk * CHUNK;
-    const uint32_t hi = top < c0 + CHUNK ? top : c0 + CHUNK;
-    const uint32_t nin = hi - c0;  // 1 .. 64 entries of the chunk below the walk's top
-    uint64_t mask;
-    if (smask) {
-      mask = mcur & (nin >= 64 ? ~0ull : ((1ull << nin) - 1ull));
-      if (kk >= 1) {
-        if (kbase - (kk - 1) >= 64) {  // past the loaded 64 chunks (tiles over 4096 entries)
-          kbase = kk - 1;
-          load_masks(kbase);
-        }
-        mcur = mask_at(kk - 1);  // the next chunk's (masked record loads below)
-      }
-    } else {
-      mask = __ballot((c0 + lane < hi) && !strip_culled(q, sx0, sx1, sy0, sy1));
-    }
+  for (uint32_t hi = top; hi > range.x;) {
+    const uint32_t c0 = hi > range.x + CHUNK ? hi - CHUNK : range.x;
+    const bool keep = (c0 + lane < hi) && !strip_culled(q, sx0, sx1, sy0, sy1);
     {
       const float4 h = half_conic(q.q0, q.q1);
       s_rec[lw][lane][0] = make_float4(q.q0.x, q.q0.y, h.x, h.y);
@@ -1279,16 +1233,14 @@ __global__ __launch_bounds__(64 * WPB_BWD) __attribute__((amdgpu_waves_per_eu(bw
     // chunk entry j is in front of this pixel's last contributor iff j < lrel
     int lrel = (int)last - (int)(c0 - range.x);
     asm volatile("" : "+v"(lrel));  // kept in a register, not recomputed per survivor
+    uint64_t mask = __ballot(keep);
     STAT(8, 1);
     STAT(9, hi - c0);
     STAT(10, __builtin_popcountll(mask));
     {
-      const uint32_t nn0 = kk >= 2 ? c0 - 2 * CHUNK : range.x;
-#ifdef GS_EXP_BWD_MASKED_LOADS
-      // only the next chunk's survivors fetch their records (mcur: its mask)
-      if (!smask || ((mcur >> lane) & 1ull))
-#endif
-        q = load_rec_gid(rec, gnext);                      // the next (lower) chunk
+      const uint32_t n0 = c0 > range.x + CHUNK ? c0 - CHUNK : range.x;
+      const uint32_t nn0 = n0 > range.x + CHUNK ? n0 - CHUNK : range.x;
+      q = load_rec_gid(rec, gnext);                        // the next (lower) chunk
       gnext = load_gid(point_list, nn0 + lane, top - 1);   // the one after
     }
     while (mask) {
@@ -1360,6 +1312,7 @@ __global__ __launch_bounds__(64 * WPB_BWD) __attribute__((amdgpu_waves_per_eu(bw
         nb = 0;
       }
     }
+    hi = c0;
   }
   STAT_WAVE(17, 25, st_it);
   STAMP(ts2);
