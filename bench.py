@@ -68,7 +68,8 @@ sys.path.insert(0, REPO)
 
 from dynamic3dgaussians_amd import _lib  # noqa: E402
 from dynamic3dgaussians_amd.camera import camera_rig  # noqa: E402
-from dynamic3dgaussians_amd.distributed import GradBucket, shard_camera_windows, shard_cameras  # noqa: E402
+from dynamic3dgaussians_amd.distributed import (GradBucket, rank_load_scale, shard_camera_windows,  # noqa: E402
+                                                shard_cameras)
 from dynamic3dgaussians_amd.optim import FusedAdam  # noqa: E402
 from dynamic3dgaussians_amd.rasterizer import (GaussianRasterizationSettings,  # noqa: E402
                                                GaussianRasterizer, GaussianRasterizerBatch, GradientSink)
@@ -90,6 +91,12 @@ def parse():
     ap.add_argument("--split", default="windows", choices=["cameras", "windows"],
                     help="strong-scaling split: work-balanced with image sharding of the left-over cameras "
                          "(windows, the default) or whole cameras c mod N (cameras)")
+    ap.add_argument("--balance", default="measured", choices=["model", "measured"],
+                    help="window split: cut by the work model alone, or re-cut once from every rank's measured "
+                         "step per modelled unit (distributed.rank_load_scale)")
+    ap.add_argument("--whole-scale", default="",
+                    help="comma-separated measured-feedback factors (a split_model.whole_scale of an earlier run): "
+                         "use them instead of measuring, so every proxy rank cuts the same windows")
     ap.add_argument("--proxy-world", type=int, default=0,
                     help="one GPU standing in for rank --proxy-rank of an N-rank --cams-total split: the "
                          "rank's own cameras and windows, no collective (the per-rank shape)")
@@ -198,15 +205,81 @@ def raw_rendervar(params, label, means2D):
 PIECE_FRACTION = 0.32
 
 
-def split_shard(n_cams, rank, world, how, W, H, costs=None):
+def split_shard(n_cams, rank, world, how, W, H, costs=None, whole_scale=None):
     """[(camera, tile window or None)] of `rank` in a `world`-rank split of an
     n_cams rig (--split; windows balanced by `costs` = (row_cost, piece_cost),
-    rig_costs)."""
+    rig_costs, and the measured-feedback factors `whole_scale`)."""
     if how == "cameras":
         return [(c, None) for c in shard_cameras(n_cams, rank, world)]
     row_cost, piece = costs if costs is not None else (None, 0.0)
     return shard_camera_windows(n_cams, rank, world, (W + 15) // 16, (H + 15) // 16, row_cost=row_cost,
-                                piece_cost=piece)
+                                piece_cost=piece, whole_scale=whole_scale)
+
+
+def shard_model_load(shard, costs, gy):
+    """The modelled load of a rank's shard in row_cost units (its rows plus
+    the fixed cost of every piece)."""
+    row_cost, piece = costs
+    load = 0.0
+    for c, w in shard:
+        rows = range(gy) if w is None else range(w[1], w[3])
+        load += sum(row_cost[c][y] for y in rows) + piece
+    return load
+
+
+def time_shard(shard, rig, params, label, args, dev, steps=20, warmup=8):
+    """Forward + backward ms per step of one rank's camera batch (the split
+    step's rendering work; the Adam step is the same on every rank)."""
+    W_, H_, F = args.width, args.height, args.features
+    sets = make_settings([rig[c] for c, _ in shard], dev, args.compat, None,
+                         [w for _, w in shard] if any(w is not None for _, w in shard) else None)
+    ras = GaussianRasterizerBatch(sets, raw_params=True)
+    n = len(shard)
+    g = torch.Generator(device=dev).manual_seed(5)
+    ups = [torch.randn(n, 3, H_, W_, device=dev, generator=g), torch.randn(n, 1, H_, W_, device=dev, generator=g),
+           torch.randn(n, F, H_, W_, device=dev, generator=g) if F else None]
+    leaves = {k: v.detach().clone().requires_grad_(True) for k, v in params.items()}
+    m2 = torch.zeros_like(params["means3D"])
+
+    def one():
+        for v in leaves.values():
+            v.grad = None
+        rv = raw_rendervar(leaves, label, m2)
+        if F:
+            im, _, feat, depth, _ = ras(**rv)
+            torch.autograd.backward([im, depth, feat], ups)
+        else:
+            im, _, depth, _ = ras(**{k: v for k, v in rv.items() if k != "semantic_feature"})
+            torch.autograd.backward([im, depth], ups[:2])
+    for _ in range(warmup):
+        one()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        one()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps * 1e3
+
+
+def measured_balance(n_cams, world, rank, rig, params, label, args, dev, costs):
+    """Measured-feedback balancing of the window split (--balance measured):
+    every rank's shard of the modelled cut is timed (all of them in this
+    process for a --proxy-world rank; each rank its own, gathered, in a
+    distributed run), and each rank's whole-camera load is rescaled by its
+    measured step per modelled unit (distributed.rank_load_scale) before the
+    windows are cut again.  Returns (whole_scale, the first cut's per-rank ms)."""
+    gy = (args.height + 15) // 16
+    shards = [split_shard(n_cams, r, world, "windows", args.width, args.height, costs) for r in range(world)]
+    model = [shard_model_load(sh, costs, gy) for sh in shards]
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        t = torch.tensor([time_shard(shards[rank], rig, params, label, args, dev)], dtype=torch.float64,
+                         device=dev)
+        allt = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(allt, t)
+        ms = [float(x.item()) for x in allt]
+    else:
+        ms = [time_shard(sh, rig, params, label, args, dev) for sh in shards]
+    return rank_load_scale(ms, model), ms
 
 
 def rig_costs(rig, params, label, args, dev):
@@ -521,7 +594,15 @@ def main():
             raise SystemExit(f"--cams-total {args.cams_total} < {s_world} ranks")
         rig = camera_rig(args.cams_total, args.width, args.height, seed=args.seed)
         costs = rig_costs(rig, params, label, args, dev) if args.split == "windows" else None
-        shard = split_shard(args.cams_total, s_rank, s_world, args.split, args.width, args.height, costs)
+        wscale, first_ms = None, None
+        if args.whole_scale:
+            wscale = [float(x) for x in args.whole_scale.split(",")]
+            if len(wscale) != s_world:
+                raise SystemExit(f"--whole-scale needs {s_world} factors")
+        elif args.split == "windows" and args.balance == "measured" and s_world > 1:
+            wscale, first_ms = measured_balance(args.cams_total, s_world, s_rank, rig, params, label, args, dev,
+                                                costs)
+        shard = split_shard(args.cams_total, s_rank, s_world, args.split, args.width, args.height, costs, wscale)
         my_cams = [rig[c] for c, _ in shard]
         if any(w is not None for _, w in shard):
             my_windows = [w for _, w in shard]
@@ -884,12 +965,15 @@ def main():
         if world > 1:
             rig_s = camera_rig(n_split, args.width, args.height, seed=args.seed)
             costs_s = rig_costs(rig_s, params0, label, args, dev) if args.split == "windows" else None
-            mine = split_shard(n_split, rank, world, args.split, args.width, args.height, costs_s)
+            ws_s = None
+            if args.split == "windows" and args.balance == "measured":
+                ws_s, _ = measured_balance(n_split, world, rank, rig_s, params0, label, args, dev, costs_s)
+            mine = split_shard(n_split, rank, world, args.split, args.width, args.height, costs_s, ws_s)
             wins = [w for _, w in mine] if any(w is not None for _, w in mine) else None
             parts_s = batch_inputs(make_settings([rig_s[c] for c, _ in mine], dev, args.compat, None, wins),
                                    args.sub_batches)
             el_s = timed(lambda: step_batch(parts_s))
-            cams_rank = [len(split_shard(n_split, r, world, args.split, args.width, args.height, costs_s))
+            cams_rank = [len(split_shard(n_split, r, world, args.split, args.width, args.height, costs_s, ws_s))
                          for r in range(world)]
             del parts_s
         else:
@@ -999,15 +1083,17 @@ def main():
         model = []
         rc_, pc_ = costs if costs is not None else (None, 0.0)
         for r_ in range(s_world):
-            sh_ = split_shard(args.cams_total, r_, s_world, args.split, W_, H_, costs)
+            sh_ = split_shard(args.cams_total, r_, s_world, args.split, W_, H_, costs, wscale)
             load = 0.0
             for c_, w_ in sh_:
                 rows = range(gy_) if w_ is None else range(w_[1], w_[3])
                 load += (sum(rc_[c_][y] for y in rows) + pc_) if rc_ is not None else 0.0
-            model.append({"rank": r_, "pieces": len(sh_), "model_ms": round(load, 4),
+            model.append({"rank": r_, "pieces": len(sh_), "model_load": round(load, 1),
                           "shard": [[c_, w_] for c_, w_ in sh_]})
-        result["split_model"] = {"piece_fraction": PIECE_FRACTION, "piece_ms": round(pc_, 4),
-                                 "camera_ms": [round(sum(r) + pc_, 4) for r in rc_] if rc_ else None,
+        result["split_model"] = {"piece_fraction": PIECE_FRACTION, "piece_cost": round(pc_, 2),
+                                 "balance": args.balance,
+                                 "whole_scale": [round(x, 4) for x in wscale] if wscale else None,
+                                 "first_cut_fwd_bwd_ms": [round(x, 4) for x in first_ms] if first_ms else None,
                                  "ranks": model}
     if args.step_times:
         result["host_step_ms"] = [round((b - a) * 1e3, 3) for a, b in zip([t0] + host_marks, host_marks)]

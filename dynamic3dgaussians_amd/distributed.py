@@ -24,7 +24,8 @@ def shard_cameras(n_cams: int, rank: int, world: int) -> List[int]:
 
 
 def shard_camera_windows(n_cams: int, rank: int, world: int, grid_x: int, grid_y: int,
-                         row_cost: Optional[Sequence[Sequence[float]]] = None, piece_cost: float = 0.0
+                         row_cost: Optional[Sequence[Sequence[float]]] = None, piece_cost: float = 0.0,
+                         whole_scale: Optional[Sequence[float]] = None
                          ) -> List[Tuple[int, Optional[Tuple[int, int, int, int]]]]:
     """Balanced split of an n_cams rig over `world` ranks with image sharding
     (gs_camera tile_*): the first world * (n_cams // world) cameras whole,
@@ -42,6 +43,10 @@ def shard_camera_windows(n_cams: int, rank: int, world: int, grid_x: int, grid_y
     fixed work of rendering one more camera (its projection and binning
     launches, in row_cost units): a rank whose run spans two left-over
     cameras is charged it and given fewer rows (a few refinement passes).
+    `whole_scale[k]` (measured-feedback balancing, rank_load_scale): a factor
+    on rank k's whole-camera load, the rank's measured step per modelled unit
+    relative to the mean -- the model counts instances, and cameras differ in
+    blend work per instance.
     Returns
     [(camera, window or None)], window = (x0, y0, x1, y1) in tiles, rank-major
     deterministic (every rank computes the same cut).  The windows of a camera
@@ -53,6 +58,8 @@ def shard_camera_windows(n_cams: int, rank: int, world: int, grid_x: int, grid_y
         return out
     whole = [sum(cost(c, y) for c in range(q * world) if c % world == k for y in range(grid_y))
              for k in range(world)]
+    if whole_scale is not None:
+        whole = [w * float(f) for w, f in zip(whole, whole_scale)]
     seq = [(c, y) for c in range(q * world, n_cams) for y in range(grid_y)]
     pre = [0.0]
     for c, y in seq:
@@ -99,6 +106,17 @@ def shard_camera_windows(n_cams: int, rank: int, world: int, grid_x: int, grid_y
         if ys:
             out.append((c, (0, ys[0], grid_x, ys[-1] + 1)))
     return out
+
+
+def rank_load_scale(measured_ms: Sequence[float], model_load: Sequence[float]) -> List[float]:
+    """Measured-feedback factors for shard_camera_windows(whole_scale=...):
+    each rank's measured step per unit of modelled load (row_cost units),
+    relative to the mean over the ranks.  Every rank must call it with the
+    same numbers (gather the step times first), so every rank cuts the same
+    windows."""
+    rate = [m / max(l, 1e-30) for m, l in zip(measured_ms, model_load)]
+    mean = sum(rate) / len(rate)
+    return [r / mean for r in rate]
 
 
 class StaleBucketError(RuntimeError):

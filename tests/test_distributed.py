@@ -360,6 +360,25 @@ def test_shard_camera_windows_balances_row_costs(n_cams, world, gy, seed):
         for c, w in sh:
             cover[c, (0 if w is None else w[1]):(gy if w is None else w[3])] += 1
     assert (cover == 1).all()
+    # measured-feedback balance (bench.py --balance measured): a rank whose
+    # measured step per modelled unit is 20 % above the mean gets less of the
+    # left-over rows; the windows still partition every camera
+    from dynamic3dgaussians_amd.distributed import rank_load_scale
+    base = [sum(cost[c, (0 if w is None else w[1]):(gy if w is None else w[3])].sum() for c, w in
+                shard_camera_windows(n_cams, r, world, gx, gy, row_cost=cost)) for r in range(world)]
+    ms = [b * (1.2 if r == 1 else 1.0) for r, b in enumerate(base)]
+    scale = rank_load_scale(ms, base)
+    assert scale[1] > scale[0] and abs(np.mean(scale) - 1.0) < 1e-9
+    cover[:] = 0
+    got = []
+    for r in range(world):
+        sh = shard_camera_windows(n_cams, r, world, gx, gy, row_cost=cost, whole_scale=scale)
+        got.append(sum(cost[c, (0 if w is None else w[1]):(gy if w is None else w[3])].sum() for c, w in sh))
+        for c, w in sh:
+            cover[c, (0 if w is None else w[1]):(gy if w is None else w[3])] += 1
+    assert (cover == 1).all()
+    if n_cams // world > 0:  # a rank with whole cameras to rescale
+        assert got[1] <= base[1] + 1e-9
 
 
 def _async_worker(rank, world, port, q):
