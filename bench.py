@@ -272,8 +272,9 @@ def measured_balance(n_cams, world, rank, rig, params, label, args, dev, costs):
     shards = [split_shard(n_cams, r, world, "windows", args.width, args.height, costs) for r in range(world)]
     model = [shard_model_load(sh, costs, gy) for sh in shards]
     if dist.is_initialized() and dist.get_world_size() > 1:
+        cdev = dev if dist.get_backend() == "nccl" else torch.device("cpu")  # gloo rehearsals: host tensors
         t = torch.tensor([time_shard(shards[rank], rig, params, label, args, dev)], dtype=torch.float64,
-                         device=dev)
+                         device=cdev)
         allt = [torch.zeros_like(t) for _ in range(world)]
         dist.all_gather(allt, t)
         ms = [float(x.item()) for x in allt]
@@ -1094,6 +1095,7 @@ def main():
                                  "balance": args.balance,
                                  "whole_scale": [round(x, 4) for x in wscale] if wscale else None,
                                  "first_cut_fwd_bwd_ms": [round(x, 4) for x in first_ms] if first_ms else None,
+                                 "row_cost": [[int(v) for v in r] for r in rc_] if rc_ else None,
                                  "ranks": model}
     if args.step_times:
         result["host_step_ms"] = [round((b - a) * 1e3, 3) for a, b in zip([t0] + host_marks, host_marks)]

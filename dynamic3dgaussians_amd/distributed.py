@@ -94,12 +94,36 @@ def shard_camera_windows(n_cams: int, rank: int, world: int, grid_x: int, grid_y
     def pieces(bounds, k):
         return len({c for c, _ in seq[bounds[k]:bounds[k + 1]]})
 
+    def loads(bounds):
+        return [whole[k] + pre[bounds[k + 1]] - pre[bounds[k]] + piece_cost * pieces(bounds, k)
+                for k in range(world)]
+
     bounds = cut(whole)
-    for _ in range(4 if piece_cost > 0 else 0):
+    cands = [bounds]
+    for _ in range(6 if piece_cost > 0 else 0):
         nb = cut([w + piece_cost * pieces(bounds, k) for k, w in enumerate(whole)])
-        if nb == bounds:
+        if nb in cands:
             break
+        cands.append(nb)
         bounds = nb
+    # the piece refinement can oscillate (a run gains or loses its second
+    # camera between passes): keep the candidate whose largest modelled load
+    # is least, then move single boundaries row by row while that improves it
+    bounds = min(cands, key=lambda b: (max(loads(b)), cands.index(b)))
+    if piece_cost > 0:
+        best = max(loads(bounds))
+        improved = True
+        while improved:
+            improved = False
+            for k in range(1, world):
+                for d in (-1, 1):
+                    b = list(bounds)
+                    b[k] += d
+                    if not (b[k - 1] <= b[k] <= b[k + 1]):
+                        continue
+                    m = max(loads(b))
+                    if m < best - 1e-9:
+                        bounds, best, improved = b, m, True
     mine = seq[bounds[rank]:bounds[rank + 1]]
     for c in range(q * world, n_cams):
         ys = [y for cc, y in mine if cc == c]
