@@ -711,6 +711,9 @@ def main():
     # elementwise launches per step; tests/test_gpu_raw_params.py holds it to
     # the torch-activation step); GS_BENCH_RAW=0 keeps torch's activations.
     raw = os.environ.get("GS_BENCH_RAW", "1") != "0"
+    # the sync-free forward (gs_forward_batch; GS_BENCH_SYNC_FREE=0: the
+    # two-phase plan -> host read -> render order of the reference)
+    sync_free = os.environ.get("GS_BENCH_SYNC_FREE", "1") != "0"
     means2D_placeholder = torch.zeros_like(params["means3D"])
 
     # one upstream gradient per camera, materialized once (the batch's
@@ -723,7 +726,8 @@ def main():
             C_ = len(idx)
             ups = (up_color.expand(C_, -1, -1, -1).contiguous(), up_depth.expand(C_, -1, -1, -1).contiguous(),
                    up_feat.expand(C_, -1, -1, -1).contiguous() if up_feat is not None else None)
-            parts.append((GaussianRasterizerBatch([setts[i] for i in idx], raw_params=raw), ups, streams[gi]))
+            parts.append((GaussianRasterizerBatch([setts[i] for i in idx], raw_params=raw, sync_free=sync_free),
+                          ups, streams[gi]))
         return parts
 
     batch_parts = batch_inputs(settings, args.sub_batches)
@@ -1054,6 +1058,8 @@ def main():
                             "cameras)" if args.mode == "batch" else "per camera (GaussianRasterizer drop-in)"),
                    "optimizer": optim_kind,
                    "streams": n_streams if args.mode == "percam" else len(batch_parts),
+                   "forward": ("sync-free (gs_forward_batch: binning sized from the previous step)" if sync_free
+                               and args.mode == "batch" else "two-phase (plan, host read, render)"),
                    "activations": ("in-kernel (raw parameters, GS_FLAG_ACTIVATE)" if raw and args.mode == "batch"
                                    else "torch ops (params2rendervar)"),
                    "grad_sum": ("in-kernel (camera sum in preprocess_bwd)" if args.mode == "batch" else
