@@ -682,22 +682,31 @@ def main():
     up_feat = torch.randn(args.features, H_, W_, device=dev, generator=g) if args.features else None
 
     # per-camera instance counts for the algorithmic byte model
-    inst = []
-    with torch.no_grad():
-        rv = params2rendervar(params, label)
-        from dynamic3dgaussians_amd import _C
-        for s in settings:
-            # one camera (and its tile window) through the batch entry point
-            out = _C.rasterize_gaussians_batch(
-                s.bg, rv["means3D"], rv["colors_precomp"], rv.get("semantic_feature"),
-                rv["opacities"], rv["scales"], rv["rotations"], 1.0, torch.Tensor([]),
-                s.viewmatrix.reshape(1, 16), s.projmatrix.reshape(1, 16), [s.c_x], [s.c_y], [s.tanfovx],
-                [s.tanfovy], H_, W_, torch.Tensor([]), 0, s.campos.reshape(1, 3), False, False,
-                compat=args.compat, windows=[s.tile_window])
-            # list instances actually binned (the byte model's L), visible
-            # Gaussians and the reference's num_rendered
-            inst.append((int(out[9][0]), int((out[5][0] > 0).sum().item()), int(out[0][0])))
-    del out
+    def instance_counts():
+        """Per camera of the rank: list instances actually binned (the byte
+        model's L), visible Gaussians and the reference's num_rendered, of
+        the parameters as they are now."""
+        res = []
+        with torch.no_grad():
+            rv = params2rendervar(params, label)
+            from dynamic3dgaussians_amd import _C
+            for s in settings:
+                # one camera (and its tile window) through the batch entry point
+                out = _C.rasterize_gaussians_batch(
+                    s.bg, rv["means3D"], rv["colors_precomp"], rv.get("semantic_feature"),
+                    rv["opacities"], rv["scales"], rv["rotations"], 1.0, torch.Tensor([]),
+                    s.viewmatrix.reshape(1, 16), s.projmatrix.reshape(1, 16), [s.c_x], [s.c_y], [s.tanfovx],
+                    [s.tanfovy], H_, W_, torch.Tensor([]), 0, s.campos.reshape(1, 3), False, False,
+                    compat=args.compat, windows=[s.tile_window])
+                res.append((int(out[9][0]), int((out[5][0] > 0).sum().item()), int(out[0][0])))
+        return res
+
+    # The parameters train during the run (Adam on fixed synthetic upstream
+    # gradients), so the scene the kernels render drifts from step to step:
+    # the counts are taken before the timed steps and again after them, and
+    # the byte model uses their mean.
+    inst0 = instance_counts()
+    inst = inst0
 
     # 4 = the box's hardware queues per process (GPU_MAX_HW_QUEUES): measured
     # 822 / 846 / 871 / 912 / 888 Mpix/s at 1 / 2 / 3 / 4 / 6 streams
@@ -904,6 +913,9 @@ def main():
     elapsed = time.perf_counter() - t0
     stages = _lib.timing_read()
     _lib.timing_enable(False)
+    drain()
+    inst1 = instance_counts()
+    inst = [tuple((a + b) / 2 for a, b in zip(x, y)) for x, y in zip(inst0, inst1)]
     if args.dump_params and rank == 0:
         drain()
         torch.cuda.synchronize()
@@ -1080,6 +1092,7 @@ def main():
             "value": round(mpix_total / (other_elapsed / args.steps), 3),
             "streams": n_streams if other == "percam" else 1},
         "instances_per_cam": int(np.mean([L for L, _, _ in inst])),
+        "instances_per_cam_before_after": [int(np.mean([x[0] for x in inst0])), int(np.mean([x[0] for x in inst1]))],
         "num_rendered_per_cam": int(np.mean([R for _, _, R in inst])),
     }
     if strong:

@@ -1,6 +1,8 @@
 # configs[3] per-rank proxies of the 27-camera windows split over N ranks
 # (bench.py --proxy-world N --proxy-rank r), REPS interleaved runs of every
-# rank (100-step windows), after the single-GPU 27-camera bench line the
+# rank (the bench default window: 20 steps after 3 warm-up steps, as the
+# single-GPU line -- the parameters train, so the scene drifts over a run),
+# after the single-GPU 27-camera bench line the
 # speed-up is quoted against; then tools/split_predict.py over all of them.
 # With the measured-feedback balance (bench.py --balance measured, the
 # default) rank 0's first run measures every rank's shard and the others
@@ -18,7 +20,7 @@ for rep in $(seq 1 ${REPS:-3}); do
 for r in ${RANKS:-0 1 2 3 4 5 6 7}; do
   f=$O/proxy_r${r}_$rep.json
   timeout -k 10 200 python bench.py --cams-total 27 --proxy-world ${N:-8} --proxy-rank $r --no-cpu-baseline \
-    --steps 100 --warmup 10 ${WS:+--whole-scale $WS} ${BENCH_ARGS:-} > $f 2> ${f%.json}.err || { tail -5 ${f%.json}.err; exit 2; }
+    --steps ${STEPS:-20} --warmup ${WARMUP:-3} ${WS:+--whole-scale $WS} ${BENCH_ARGS:-} > $f 2> ${f%.json}.err || { tail -5 ${f%.json}.err; exit 2; }
   python -c "import json; d=json.load(open('$f')); m=d['split_model']['ranks'][$r]; print('proxy', $r, $rep, d['ms_per_step'], m['pieces'], m['model_load'])"
   if [ -z "$WS" ]; then
     WS=$(python -c "import json; d=json.load(open('$f')); w=d['split_model'].get('whole_scale'); print(','.join(str(x) for x in w) if w else '')")
