@@ -216,14 +216,15 @@ def split_shard(n_cams, rank, world, how, W, H, costs=None, whole_scale=None):
                                 piece_cost=piece, whole_scale=whole_scale)
 
 
-def shard_model_load(shard, costs, gy):
+def shard_model_load(shard, costs, gy, whole_scale=1.0):
     """The modelled load of a rank's shard in row_cost units (its rows plus
-    the fixed cost of every piece)."""
+    the fixed cost of every piece; whole cameras' rows times `whole_scale`,
+    as shard_camera_windows weighs them)."""
     row_cost, piece = costs
     load = 0.0
     for c, w in shard:
         rows = range(gy) if w is None else range(w[1], w[3])
-        load += sum(row_cost[c][y] for y in rows) + piece
+        load += sum(row_cost[c][y] for y in rows) * (whole_scale if w is None else 1.0) + piece
     return load
 
 
@@ -261,26 +262,32 @@ def time_shard(shard, rig, params, label, args, dev, steps=20, warmup=8):
     return (time.perf_counter() - t0) / steps * 1e3
 
 
-def measured_balance(n_cams, world, rank, rig, params, label, args, dev, costs):
+def measured_balance(n_cams, world, rank, rig, params, label, args, dev, costs, iters=2):
     """Measured-feedback balancing of the window split (--balance measured):
-    every rank's shard of the modelled cut is timed (all of them in this
+    every rank's shard of the current cut is timed (all of them in this
     process for a --proxy-world rank; each rank its own, gathered, in a
-    distributed run), and each rank's whole-camera load is rescaled by its
-    measured step per modelled unit (distributed.rank_load_scale) before the
-    windows are cut again.  Returns (whole_scale, the first cut's per-rank ms)."""
+    distributed run), each rank's whole-camera load is rescaled by its
+    measured step per modelled unit (distributed.rank_load_scale), and the
+    windows are cut again -- `iters` times, the factors compounding.
+    Returns (whole_scale, every round's per-rank ms)."""
     gy = (args.height + 15) // 16
-    shards = [split_shard(n_cams, r, world, "windows", args.width, args.height, costs) for r in range(world)]
-    model = [shard_model_load(sh, costs, gy) for sh in shards]
-    if dist.is_initialized() and dist.get_world_size() > 1:
-        cdev = dev if dist.get_backend() == "nccl" else torch.device("cpu")  # gloo rehearsals: host tensors
-        t = torch.tensor([time_shard(shards[rank], rig, params, label, args, dev)], dtype=torch.float64,
-                         device=cdev)
-        allt = [torch.zeros_like(t) for _ in range(world)]
-        dist.all_gather(allt, t)
-        ms = [float(x.item()) for x in allt]
-    else:
-        ms = [time_shard(sh, rig, params, label, args, dev) for sh in shards]
-    return rank_load_scale(ms, model), ms
+    ws = [1.0] * world
+    rounds = []
+    for _ in range(iters):
+        shards = [split_shard(n_cams, r, world, "windows", args.width, args.height, costs, ws) for r in range(world)]
+        model = [shard_model_load(sh, costs, gy, ws[r]) for r, sh in enumerate(shards)]
+        if dist.is_initialized() and dist.get_world_size() > 1:
+            cdev = dev if dist.get_backend() == "nccl" else torch.device("cpu")  # gloo rehearsals: host tensors
+            t = torch.tensor([time_shard(shards[rank], rig, params, label, args, dev)], dtype=torch.float64,
+                             device=cdev)
+            allt = [torch.zeros_like(t) for _ in range(world)]
+            dist.all_gather(allt, t)
+            ms = [float(x.item()) for x in allt]
+        else:
+            ms = [time_shard(sh, rig, params, label, args, dev) for sh in shards]
+        rounds.append(ms)
+        ws = [w * f for w, f in zip(ws, rank_load_scale(ms, model))]
+    return ws, rounds
 
 
 def rig_costs(rig, params, label, args, dev):
@@ -1113,7 +1120,7 @@ def main():
         result["split_model"] = {"piece_fraction": PIECE_FRACTION, "piece_cost": round(pc_, 2),
                                  "balance": args.balance,
                                  "whole_scale": [round(x, 4) for x in wscale] if wscale else None,
-                                 "first_cut_fwd_bwd_ms": [round(x, 4) for x in first_ms] if first_ms else None,
+                                 "cut_fwd_bwd_ms": [[round(x, 4) for x in r] for r in first_ms] if first_ms else None,
                                  "row_cost": [[int(v) for v in r] for r in rc_] if rc_ else None,
                                  "ranks": model}
     if args.step_times:

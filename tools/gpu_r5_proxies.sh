@@ -24,7 +24,7 @@ for r in ${RANKS:-0 1 2 3 4 5 6 7}; do
   python -c "import json; d=json.load(open('$f')); m=d['split_model']['ranks'][$r]; print('proxy', $r, $rep, d['ms_per_step'], m['pieces'], m['model_load'])"
   if [ -z "$WS" ]; then
     WS=$(python -c "import json; d=json.load(open('$f')); w=d['split_model'].get('whole_scale'); print(','.join(str(x) for x in w) if w else '')")
-    python -c "import json; d=json.load(open('$f')); print('first cut (fwd+bwd ms per rank):', d['split_model'].get('first_cut_fwd_bwd_ms'), 'whole_scale:', d['split_model'].get('whole_scale'))"
+    python -c "import json; d=json.load(open('$f')); print('cuts (fwd+bwd ms per rank):', d['split_model'].get('cut_fwd_bwd_ms'), 'whole_scale:', d['split_model'].get('whole_scale'))"
   fi
 done
 done
