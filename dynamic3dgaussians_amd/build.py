@@ -40,7 +40,6 @@ VARIANT_FLAGS = {"": [], "stats": ["-DGS_STATS"], "stamps": ["-DGS_STAMPS"],
                  "exp_nofeat": ["-DGS_EXP_NO_FEAT_ATOMIC"],
                  "exp_noatomic": ["-DGS_EXP_NO_FEAT_ATOMIC", "-DGS_EXP_NO_ACC_ATOMIC"],
                  "exp_fwd_nofeatst": ["-DGS_EXP_FWD_NO_FEAT_STORE"],  # traffic of the feature planes
-                 "exp_fwd_featnt": ["-DGS_EXP_FWD_FEAT_NT"],
                  "ctl": []}  # the product's flags under a variant's (ctypes) binding: the A/B control
 ARCH = os.environ.get("GSPLAT_OFFLOAD_ARCH", "gfx950")
 

@@ -758,11 +758,6 @@ blend_done:
 #ifdef GS_EXP_FWD_NO_FEAT_STORE  // timing / traffic only: the feature planes are not written
           continue;
 #endif
-#ifdef GS_EXP_FWD_FEAT_NT  // traffic experiment: non-temporal (streaming) feature stores
-          constexpr int kPol = 2;
-#else
-          constexpr int kPol = 0;
-#endif
 #pragma unroll
           for (int fb = 0; fb < FB; ++fb)
 #pragma unroll
@@ -771,7 +766,7 @@ blend_done:
               const int ch = chs + 4 * (lane >> 5);
               const float b = (COMPAT == COMPAT_REFERENCE && ch < 3) ? bg[ch < 3 ? ch : 0] : 0.0f;
               __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[2 * fb + blk][r] + Tp * b), rsrc, (int)voff,
-                                                    (int)((uint32_t)chs * (uint32_t)HW * 4u), kPol);
+                                                    (int)((uint32_t)chs * (uint32_t)HW * 4u), 0);
             }
           continue;
         }
