@@ -68,7 +68,7 @@ sys.path.insert(0, REPO)
 
 from dynamic3dgaussians_amd import _lib  # noqa: E402
 from dynamic3dgaussians_amd.camera import camera_rig  # noqa: E402
-from dynamic3dgaussians_amd.distributed import (GradBucket, rank_load_scale, shard_camera_windows,  # noqa: E402
+from dynamic3dgaussians_amd.distributed import (GradBucket, ShardedAdam, rank_load_scale, shard_camera_windows,  # noqa: E402
                                                 shard_cameras)
 from dynamic3dgaussians_amd.optim import FusedAdam  # noqa: E402
 from dynamic3dgaussians_amd.rasterizer import (GaussianRasterizationSettings,  # noqa: E402
@@ -663,7 +663,33 @@ def main():
     local_overlap = (not dist_on and args.features > 0 and args.mode == "batch"
                      and os.environ.get("GS_BENCH_OVERLAP", "0") == "1")
     split_opt = overlap or local_overlap
-    if split_opt:
+    # The camera batch takes the raw parameters and applies params2rendervar's
+    # activations in its preprocess kernels (GS_FLAG_ACTIVATE: ~20 fewer
+    # elementwise launches per step; tests/test_gpu_raw_params.py holds it to
+    # the torch-activation step); GS_BENCH_RAW=0 keeps torch's activations.
+    raw = os.environ.get("GS_BENCH_RAW", "1") != "0"
+    # The camera batch as one rank of N (N > 1, or a --proxy-world stand-in):
+    # Adam sharded over the ranks (distributed.ShardedAdam, ZeRO stage 1) --
+    # reduce-scatter, Adam on the rank's 1/N of the parameters, all-gather --
+    # with the backward writing its gradients straight into the exchange
+    # buffer (grad_into).  GS_BENCH_ZERO=0: the all-reduce + full Adam on
+    # every rank; =force: also at a world of one with a process group (the
+    # RCCL reduce-scatter / all-gather rehearsal on one GPU).
+    zero_env = os.environ.get("GS_BENCH_ZERO", "1")
+    zero = (args.mode == "batch" and raw and zero_env != "0"
+            and (world > 1 or args.proxy_world > 1 or (zero_env == "force" and dist_on)))
+    z_rank, z_world = (args.proxy_rank, args.proxy_world) if args.proxy_world else (rank, world)
+    if zero:
+        lrs = {g_["name"]: g_["lr"] for g_ in groups}
+        z_coll = dist_on and (world > 1 or zero_env == "force")
+        if overlap:  # geometry in line, features behind the next step (two gradient buffers)
+            zgeo = ShardedAdam({k: v for k, v in params.items() if k != "semantic_feature"}, lrs, rank=z_rank,
+                               world=z_world, eps=1e-15, collectives=z_coll)
+            zfeat = ShardedAdam({"semantic_feature": params["semantic_feature"]}, lrs, rank=z_rank, world=z_world,
+                                eps=1e-15, n_grad_buffers=2, collectives=z_coll)
+        else:
+            zopt = ShardedAdam(params, lrs, rank=z_rank, world=z_world, eps=1e-15, collectives=z_coll)
+    elif split_opt:
         opt = make_opt([g_ for g_ in groups if g_["name"] != "semantic_feature"])
         opt_feat = make_opt([g_ for g_ in groups if g_["name"] == "semantic_feature"])
     else:
@@ -673,7 +699,9 @@ def main():
     # one fill clears it.  N = 1 has no exchange: gradients stay unbound, so
     # autograd hands the backward's tensors to the leaves without the six
     # accumulate kernels and the fill (-0.06 ms per step).
-    if overlap:
+    if zero:
+        pass
+    elif overlap:
         bucket = GradBucket({k: v for k, v in params.items() if k != "semantic_feature"}, bind_grads=True)
         feat_buckets = [GradBucket({"semantic_feature": params["semantic_feature"]}, bind_grads=True)
                         for _ in range(2)]
@@ -722,11 +750,6 @@ def main():
         # the leaves' accumulation crosses the camera streams by design
         torch.autograd.graph.set_warn_on_accumulate_grad_stream_mismatch(False)
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(device=dev) for _ in range(n_streams - 1)]
-    # The camera batch takes the raw parameters and applies params2rendervar's
-    # activations in its preprocess kernels (GS_FLAG_ACTIVATE: ~20 fewer
-    # elementwise launches per step; tests/test_gpu_raw_params.py holds it to
-    # the torch-activation step); GS_BENCH_RAW=0 keeps torch's activations.
-    raw = os.environ.get("GS_BENCH_RAW", "1") != "0"
     # the sync-free forward (gs_forward_batch; GS_BENCH_SYNC_FREE=0: the
     # two-phase plan -> host read -> render order of the reference)
     sync_free = os.environ.get("GS_BENCH_SYNC_FREE", "1") != "0"
@@ -748,14 +771,70 @@ def main():
 
     batch_parts = batch_inputs(settings, args.sub_batches)
 
-    def run_part(ras, ups, rv, ready=None):
+    def run_part(ras, ups, rv, ready=None, grad_into=None):
         up_c, up_d, up_f = ups
         if up_f is not None:  # G3 call (label + semantic_feature)
-            im, radius, feat, depth, _ = ras(**rv, feature_ready=ready)
+            im, radius, feat, depth, _ = ras(**rv, feature_ready=ready, grad_into=grad_into)
             torch.autograd.backward([im, depth, feat], [up_c, up_d, up_f])
         else:                 # G2 call (label only)
-            im, radius, depth, _ = ras(**rv)
+            im, radius, depth, _ = ras(**rv, grad_into=grad_into)
             torch.autograd.backward([im, depth], [up_c, up_d])
+
+    # the raw parameters' GaussianRasterizer argument names (raw_rendervar)
+    arg_of = {"means3D": "means3D", "rgb_colors": "colors_precomp", "unnorm_rotations": "rotations",
+              "logit_opacities": "opacities", "log_scales": "scales", "semantic_feature": "semantic_feature"}
+
+    def zero_buffers(k):
+        """(sharded optimizer, gradient buffer) pairs of step parity k."""
+        return [(zgeo, 0), (zfeat, k)] if overlap else [(zopt, 0)]
+
+    def step_zero(parts):
+        """One rank's step with the sharded Adam: the backward writes the
+        gradients into the exchange buffers; geometry reduce-scatter + Adam
+        on the rank's slice + all-gather in line; with `overlap` the feature
+        exchange and update behind the next step's projection and binning
+        (their blend waits on the event), double-buffered."""
+        main = torch.cuda.current_stream(dev)
+        k = pipe["k"] if overlap else 0
+        kb = k % 2
+        pending = pipe["done"][kb] if overlap else None
+        if pending is not None:  # step k-2's exchange still reads gradient buffer kb
+            main.wait_event(pending)
+        rv = raw_rendervar(params, label, means2D_placeholder)
+        if len(parts) == 1:
+            dest = {}
+            for o_, b_ in zero_buffers(kb):
+                dest.update({arg_of[n_]: t_ for n_, t_ in o_.grad_views(b_).items()})
+            run_part(parts[0][0], parts[0][1], rv, ready=pipe["done"][(k - 1) % 2] if overlap else None,
+                     grad_into=dest)
+        else:
+            # sub-batches on their own streams accumulate through autograd
+            drain()
+            for o_, b_ in zero_buffers(kb):
+                o_.bind(b_)
+                o_.zero_grad(b_)
+            for _, _, st in parts:
+                st.wait_stream(main)
+            for ras, ups, st in parts:
+                with torch.cuda.stream(st):
+                    run_part(ras, ups, rv)
+            for _, _, st in parts:
+                main.wait_stream(st)
+        if not overlap:
+            zopt.step(0)
+            return
+        zgeo.step(0)                                   # geometry: on the critical path
+        work = zfeat.reduce_scatter(kb, async_op=True)  # features: behind the next step
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            if work is not None:
+                work.wait()
+            zfeat.update(kb)
+            zfeat.all_gather()
+            ev = torch.cuda.Event()
+            ev.record(side)
+        pipe["done"][kb] = ev
+        pipe["k"] = k + 1
 
     def drain():
         """Overlap mode: the main stream waits for every pending feature update."""
@@ -810,6 +889,8 @@ def main():
         pipe["k"] += 1
 
     def step_batch(parts=batch_parts):
+        if zero:
+            return step_zero(parts)
         if overlap and len(parts) == 1:
             return step_overlap(parts)
         if local_overlap and len(parts) == 1:
@@ -845,10 +926,15 @@ def main():
         if mode == "batch":
             return step_batch()
         drain()
-        if overlap:
-            feat_buckets[0].bind()
-            feat_buckets[0].zero_grad()
-        bucket.zero_grad()
+        if zero:
+            for o_, b_ in zero_buffers(0):
+                o_.bind(b_)
+                o_.zero_grad(b_)
+        else:
+            if overlap:
+                feat_buckets[0].bind()
+                feat_buckets[0].zero_grad()
+            bucket.zero_grad()
         if sink is not None:
             sink.reset()
         rv = params2rendervar(params, label)
@@ -884,6 +970,10 @@ def main():
         summed = sink.gradients() if sink is not None else {k: v.grad for k, v in leaves.items()}
         keys = [k for k in leaves if k != "means2D" and summed.get(k) is not None]
         torch.autograd.backward([rv[k] for k in keys], [summed[k] for k in keys])
+        if zero:
+            for o_, b_ in zero_buffers(0):
+                o_.step(b_)
+            return
         bucket.all_reduce()
         opt.step()
         if overlap:
@@ -1075,7 +1165,9 @@ def main():
                                "fwd+bwd of every camera + grad all-reduce + Adam",
                    "mode": ("camera batch (GaussianRasterizerBatch: one launch per stage for the rank's "
                             "cameras)" if args.mode == "batch" else "per camera (GaussianRasterizer drop-in)"),
-                   "optimizer": optim_kind,
+                   "optimizer": (f"sharded Adam (ZeRO-1, distributed.ShardedAdam): rank {z_rank}'s 1/{z_world} "
+                                 "of the parameters, gradients written into the exchange buffer" if zero
+                                 else optim_kind),
                    "streams": n_streams if args.mode == "percam" else len(batch_parts),
                    "forward": ("sync-free (gs_forward_batch: binning sized from the previous step)" if sync_free
                                and args.mode == "batch" else "two-phase (plan, host read, render)"),
@@ -1086,7 +1178,13 @@ def main():
                    "gaussians": args.gaussians, "cams_per_rank": len(my_cams), "width": W_,
                    "height": H_, "feature_channels": args.features, "compat": args.compat,
                    "parallelism": f"camera-sharded dp{world}",
-                   "grad_exchange": ("geometry all-reduce before Adam; feature all-reduce + Adam overlapped with the "
+                   "grad_exchange": ("geometry reduce-scatter + sharded Adam + all-gather in line; the features' "
+                                     "behind the next step's projection and binning" if (zero and overlap) else
+                                     "reduce-scatter + sharded Adam + all-gather" if (zero and world > 1) else
+                                     f"none (a one-GPU stand-in for rank {z_rank} of {z_world}: its Adam slice, "
+                                     "no collective)" if (zero and args.proxy_world) else
+                                     "reduce-scatter + sharded Adam + all-gather (forced at one rank)" if zero else
+                                     "geometry all-reduce before Adam; feature all-reduce + Adam overlapped with the "
                                      "next step's projection and binning" if overlap else
                                      "one all-reduce before Adam" if world > 1 else
                                      "none (one rank); the feature Adam step overlapped with the next step's "

@@ -242,6 +242,9 @@ def rasterize_gaussians(background, means3D, colors, semantic_feature, opacity, 
 _BUFFER_ORDER = ("dmeans2D", "dcolors", "dsem", "dopacity", "dmeans3D", "dcov3D", "dsh", "dscales", "drot")
 
 
+_NO_DEST = torch.empty(0)  # backward_batch's `out` entry: allocate this gradient
+
+
 def _buffer_shapes(P, F, M):
     return dict(dmeans2D=(P, 3), dcolors=(P, 3), dsem=(P, F), dopacity=(P, 1), dmeans3D=(P, 3),
                 dcov3D=(P, 6), dsh=(P, M, 3), dscales=(P, 3), drot=(P, 4))
@@ -611,7 +614,7 @@ def rasterize_gaussians_batch_backward(background, means3D, radii, colors, seman
                                        dL_dout_depth, dL_dout_alpha, sh, degree, campos, geomBuffer,
                                        num_instances, binningBuffer, imageBuffer, alphas, debug, *,
                                        compat=None, grad_mask=None, densify=None, opacity=None,
-                                       activate=False, windows=None):
+                                       activate=False, windows=None, out=None):
     """The backward of a camera batch (gs_backward_batch): the arguments of
     rasterize_gaussians_backward with stacked per-camera matrices, scalars
     and upstream gradients ([C, ...]), in the binding's positional camera
@@ -619,11 +622,20 @@ def rasterize_gaussians_batch_backward(background, means3D, radii, colors, seman
     per-Gaussian gradient SUMMED over the cameras.  `densify` as in
     rasterize_gaussians_backward (per-camera statistics, summed).
     `activate` (with the raw `opacity`): the gradients of the raw opacity /
-    scale / rotation parameters (GS_FLAG_ACTIVATE)."""
+    scale / rotation parameters (GS_FLAG_ACTIVATE).  `out`: optional
+    {name: tensor} destinations of backward_buffers' names (e.g. the views of
+    a gradient bucket, distributed.ShardedAdam.grad_views): those gradients
+    are WRITTEN there (every element, not accumulated) instead of into fresh
+    tensors; each must be a contiguous fp32 device tensor of the gradient's
+    element count (dsem at the compiled feature width)."""
     L_ = _lib.load()
     cm = _compat_code(compat)
     if activate and not _present(opacity):
         raise RuntimeError("activate=True needs the raw opacities")
+    if out:
+        unknown = set(out) - set(_buffer_shapes(0, 0, 0))
+        if unknown:
+            raise RuntimeError(f"out: unknown gradient names {sorted(unknown)}")
     nat = _native_mod()
     if nat is not None and means3D.is_cuda and means3D.dim() == 2 and means3D.size(0) > 0:
         try:
@@ -637,6 +649,7 @@ def rasterize_gaussians_batch_backward(background, means3D, radii, colors, seman
                                       imageBuffer, alphas, bool(debug), cm, _opt(grad_mask),
                                       None if densify is None else list(densify), _opt(opacity), bool(activate),
                                       _windows_arg(windows, len(c_x)),
+                                      [out.get(k, _NO_DEST) for k in _buffer_shapes(0, 0, 0)] if out else [],
                                       torch.cuda.current_stream(means3D.device).cuda_stream)
         except RuntimeError as ex:
             raise _lib.GsplatError(str(ex)) from None
@@ -675,7 +688,13 @@ def rasterize_gaussians_batch_backward(background, means3D, radii, colors, seman
     radii_c = radii.to(device=dev, dtype=torch.int32).contiguous()
     if tuple(radii_c.shape) != (C, P):
         raise RuntimeError(f"radii must be [C={C}, P={P}]")
+    dest = out or {}
     out = backward_buffers(P, inp.F, inp.M, dev)
+    for k, t in dest.items():
+        want = out[k]
+        if t.dtype != torch.float32 or t.device != dev or not t.is_contiguous() or t.numel() != want.numel():
+            raise RuntimeError(f"out['{k}'] must be a contiguous fp32 tensor of {want.numel()} elements on {dev}")
+        out[k] = t.view(want.shape)
     if densify is not None:
         for t in densify:
             if tuple(t.shape) != (P,) or t.dtype != torch.float32 or t.device != dev or not t.is_contiguous():

@@ -50,6 +50,9 @@ class GsNeighborGraph(ctypes.Structure):
                 ("prev_inv_rot", c_void_p), ("rev_ptr", c_void_p), ("rev_pos", c_void_p)]
 
 
+GS_ADAM_MAX_TENSORS = 16  # include/gs_optim.h
+
+
 class GsAdamTensor(ctypes.Structure):
     """include/gs_optim.h gs_adam_tensor."""
     _fields_ = [("param", c_void_p), ("grad", c_void_p), ("exp_avg", c_void_p), ("exp_avg_sq", c_void_p),
@@ -59,7 +62,7 @@ class GsAdamTensor(ctypes.Structure):
 class GsAdamArgs(ctypes.Structure):
     """include/gs_optim.h gs_adam_args (GS_ADAM_MAX_TENSORS = 16)."""
     _fields_ = [("n_tensors", c_int32), ("_pad", c_int32), ("beta1", ctypes.c_double),
-                ("beta2", ctypes.c_double), ("eps", ctypes.c_double), ("t", GsAdamTensor * 16)]
+                ("beta2", ctypes.c_double), ("eps", ctypes.c_double), ("t", GsAdamTensor * GS_ADAM_MAX_TENSORS)]
 
 
 class GsDensifyStats(ctypes.Structure):

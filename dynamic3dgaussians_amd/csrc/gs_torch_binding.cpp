@@ -375,12 +375,14 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tenso
     const OptT& dL_alpha, const OptT& sh, int64_t degree, const Tensor& campos, const Tensor& geom,
     const std::vector<int64_t>& num_instances, const OptT& binning, const Tensor& img, const Tensor& alphas,
     bool debug, int64_t compat, const OptT& grad_mask, c10::optional<std::vector<Tensor>> densify,
-    const OptT& opacity, bool activate, const std::vector<std::vector<int64_t>>& windows, int64_t stream) {
+    const OptT& opacity, bool activate, const std::vector<std::vector<int64_t>>& windows,
+    const std::vector<Tensor>& out, int64_t stream) {
   if (activate && !present(opacity)) throw std::runtime_error("activate=True needs the raw opacities");
   Inputs in(means3D, colors, sem, activate ? opacity : c10::nullopt, scales, rotations, scale_modifier, cov3D, sh,
             degree);
   if (activate) in.g.flags |= GS_FLAG_ACTIVATE;
   const int64_t C = (int64_t)cx.size();
+  if (!out.empty() && out.size() != 9) throw std::runtime_error("out must hold the 9 gradient destinations");
   const Tensor& img_ref = present(dL_color) ? *dL_color : alphas;
   const int64_t H = img_ref.size(-2), W = img_ref.size(-1);
   Cameras k(in.dev, bg, views, projs, campos, cx, cy, tx, ty, W, H, windows);
@@ -403,8 +405,22 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tenso
   if ((int64_t)num_instances.size() != C) throw std::runtime_error("num_instances must have C entries");
   const std::vector<std::vector<int64_t>> shapes = {{P, 3}, {P, 3}, {P, in.F}, {P, 1}, {P, 3},
                                                     {P, 6}, {P, in.M, 3}, {P, 3}, {P, 4}};
+  // Caller-owned destinations (a gradient bucket's views): written, not
+  // accumulated; an empty tensor = allocate.
   std::vector<Tensor> o;
-  for (int i = 0; i < 9; ++i) o.push_back(at::empty(shapes[i], f32));
+  for (int i = 0; i < 9; ++i) {
+    if (out.empty() || out[i].numel() == 0) {
+      o.push_back(at::empty(shapes[i], f32));
+      continue;
+    }
+    const Tensor& d = out[i];
+    int64_t n = 1;
+    for (int64_t e : shapes[i]) n *= e;
+    if (d.scalar_type() != at::kFloat || d.device() != in.dev || !d.is_contiguous() || d.numel() != n)
+      throw std::runtime_error("out[" + std::to_string(i) + "] must be a contiguous fp32 device tensor of " +
+                               std::to_string(n) + " elements");
+    o.push_back(d.view(shapes[i]));
+  }
   if (densify.has_value()) {
     const auto& d = *densify;
     if (d.size() != 3) throw std::runtime_error("densify must hold (accum, denom, max_radius)");

@@ -11,11 +11,14 @@ all_reduce (train.py:288-290, external.py:136-140).
 """
 from __future__ import annotations
 
+import ctypes
 import weakref
 from typing import Dict, Iterable, List, Mapping, Optional, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
+
+from . import _lib
 
 
 def shard_cameras(n_cams: int, rank: int, world: int) -> List[int]:
@@ -392,3 +395,193 @@ def all_reduce_max_(t: torch.Tensor, group=None) -> torch.Tensor:
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     return t
+
+
+class ShardedAdam:
+    """Adam with the update sharded over the ranks (ZeRO stage 1), for the
+    camera-sharded step: instead of an all_reduce of every gradient followed
+    by the same full Adam update on every rank, one reduce_scatter(SUM) hands
+    each rank the summed gradients of its 1/N slice of the parameters, the
+    rank runs Adam on that slice only (the fused kernel of gs_optim.h, one
+    launch), and one all_gather returns the updated slices to every rank.
+    The ring moves the same bytes as the all_reduce (reduce-scatter + all-
+    gather IS the ring all-reduce), the Adam step's HBM traffic (7 fp32 per
+    element: param, grad, both moments read, three written) and its moments'
+    memory drop N-fold -- at 300k Gaussians x 46 floats, Adam is 61 us of a
+    1.4 ms rank step at N = 8, the largest per-rank fixed cost.
+
+    Layout.  The parameters' storage moves into one flat fp32 buffer
+    (`param_flat`, padded to N x chunk, chunk a multiple of `align`): each
+    Parameter keeps its identity (its .data becomes a view), so the caller's
+    dict, the rasterizer inputs and anything else holding the Parameters are
+    unchanged.  Gradients live in `n_grad_buffers` flat buffers of the same
+    layout (two for a gradient set exchanged behind the next step).  Two ways
+    to fill one:
+      * grad_views(k): {name: view} destinations for the camera batch's
+        backward (GaussianRasterizerBatch(...)(..., grad_into=...)): the
+        kernels write the summed gradients straight into the bucket -- no
+        gradient tensors, no accumulation, no fill, no pack copy;
+      * bind(k) + zero_grad(k): .grad of every parameter is its view and
+        autograd accumulates into it (gradients from any autograd path).
+    The padding is never written and stays zero.
+
+    step(k) = reduce_scatter(k) + update(k) + all_gather(); the three are
+    public so that an exchange can run behind other work (reduce_scatter with
+    async_op=True, the update and the gather on a side stream).  Without a
+    process group (or with `collectives=False`) nothing is exchanged: the
+    rank updates its own slice of its own gradients -- a one-GPU stand-in for
+    rank `rank` of an N-rank step (bench.py --proxy-world).  `emulate`
+    (default: gloo with CUDA tensors, which gloo only all-reduces) runs the
+    reduce-scatter / all-gather as all-reduces of the whole buffer.
+
+    Adam is torch.optim.Adam's (amsgrad off, no weight decay; gs_optim.h):
+    one step count for every parameter, bias corrections computed in double
+    on the host, per-parameter learning rates `lr[name]`.  At N = 1 it is
+    bit-identical to FusedAdam over the same parameters; at N > 1 the
+    gradient sums are the collective's.  Not the reference's optimizer
+    object (no param_groups / state surgery): densification rebuilds it.
+    """
+
+    def __init__(self, params: Mapping[str, torch.Tensor], lr: Mapping[str, float], rank: Optional[int] = None,
+                 world: Optional[int] = None, group=None, betas=(0.9, 0.999), eps: float = 1e-15,
+                 n_grad_buffers: int = 1, align: int = 64, collectives: Optional[bool] = None,
+                 emulate: Optional[bool] = None):
+        self.names = list(params)
+        self.params = [params[k] for k in self.names]
+        if not self.params:
+            raise ValueError("ShardedAdam: no parameters")
+        self.lr = [float(lr[k]) for k in self.names]
+        self.beta1, self.beta2 = float(betas[0]), float(betas[1])
+        self.eps = float(eps)
+        dist_on = dist.is_available() and dist.is_initialized()
+        self.group = group
+        world = (dist.get_world_size(group) if dist_on else 1) if world is None else int(world)
+        rank = (dist.get_rank(group) if dist_on else 0) if rank is None else int(rank)
+        if not 0 <= rank < world:
+            raise ValueError(f"ShardedAdam: rank {rank} outside a world of {world}")
+        self.collectives = (dist_on and world > 1) if collectives is None else bool(collectives)
+        if self.collectives and not (dist_on and dist.get_world_size(group) == world
+                                     and dist.get_rank(group) == rank):
+            raise ValueError("ShardedAdam: collectives need the process group's own rank and world")
+        self.world, self.rank = world, rank
+        dev = self.params[0].device
+        for k, p in zip(self.names, self.params):
+            if p.dtype != torch.float32 or p.device != dev:
+                raise ValueError(f"ShardedAdam: parameter '{k}' must be fp32 on {dev}")
+        sizes = [p.numel() for p in self.params]
+        self.total = sum(sizes)
+        self.chunk = -(-self.total // (world * align)) * align
+        self.lo, self.hi = rank * self.chunk, (rank + 1) * self.chunk
+        n = world * self.chunk
+        self.param_flat = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.offsets = []
+        o = 0
+        with torch.no_grad():
+            for p, m in zip(self.params, sizes):
+                self.param_flat[o:o + m].copy_(p.detach().reshape(-1))
+                p.data = self.param_flat[o:o + m].view_as(p)
+                self.offsets.append(o)
+                o += m
+        self.grad_flat = [torch.zeros(n, dtype=torch.float32, device=dev) for _ in range(max(1, n_grad_buffers))]
+        # gloo moves CUDA tensors through all_reduce only: its rehearsals
+        # (2 ranks on one GPU) emulate the reduce-scatter / all-gather with it
+        if emulate is None:
+            emulate = self.collectives and dev.type == "cuda" and dist.get_backend(group) == "gloo"
+        self._emulate = bool(emulate) and self.collectives
+        if self.collectives and not self._emulate:
+            self.grad_shard = [torch.zeros(self.chunk, dtype=torch.float32, device=dev) for _ in self.grad_flat]
+        else:
+            self.grad_shard = [g[self.lo:self.hi] for g in self.grad_flat]
+        self.exp_avg = torch.zeros(self.chunk, dtype=torch.float32, device=dev)
+        self.exp_avg_sq = torch.zeros(self.chunk, dtype=torch.float32, device=dev)
+        self.t = 0
+        # the rank's slice as pieces of the parameters: (param index, flat start, flat end)
+        self.pieces = []
+        for i, (o, m) in enumerate(zip(self.offsets, sizes)):
+            a, b = max(self.lo, o), min(self.hi, o + m)
+            if a < b:
+                self.pieces.append((i, a, b))
+        self._args = {}
+
+    # ------------------------------------------------------------ gradients
+    def grad_views(self, k: int = 0) -> Dict[str, torch.Tensor]:
+        """{name: view of gradient buffer k shaped like the parameter}."""
+        g = self.grad_flat[k]
+        return {name: g[o:o + p.numel()].view_as(p) for name, p, o in zip(self.names, self.params, self.offsets)}
+
+    def bind(self, k: int = 0) -> None:
+        """Make every parameter's .grad its view into gradient buffer k."""
+        for p, v in zip(self.params, self.grad_views(k).values()):
+            p.grad = v
+
+    def zero_grad(self, k: int = 0) -> None:
+        """Zero gradient buffer k (accumulating fills: bind(); grad_views()
+        destinations are written whole by the backward and need none)."""
+        self.grad_flat[k].zero_()
+
+    # ------------------------------------------------------------ exchange
+    def reduce_scatter(self, k: int = 0, async_op: bool = False):
+        """Sum gradient buffer k over the ranks into this rank's slice
+        (grad_shard[k]).  Returns the work handle with async_op (wait() on
+        it on the stream that runs update(k)), else None."""
+        if not self.collectives:
+            return None
+        if self._emulate:
+            return dist.all_reduce(self.grad_flat[k], op=dist.ReduceOp.SUM, group=self.group, async_op=async_op)
+        return dist.reduce_scatter_tensor(self.grad_shard[k], self.grad_flat[k], op=dist.ReduceOp.SUM,
+                                          group=self.group, async_op=async_op)
+
+    def all_gather(self, async_op: bool = False):
+        """Every rank's updated slice into every rank's param_flat (in place:
+        this rank's slice is the input)."""
+        if not self.collectives:
+            return None
+        if self._emulate:
+            buf = torch.zeros_like(self.param_flat)
+            buf[self.lo:self.hi].copy_(self.param_flat[self.lo:self.hi])
+            dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group)
+            self.param_flat.copy_(buf)
+            return None
+        return dist.all_gather_into_tensor(self.param_flat, self.param_flat[self.lo:self.hi], group=self.group,
+                                           async_op=async_op)
+
+    # ------------------------------------------------------------ update
+    def update(self, k: int = 0) -> None:
+        """Adam on this rank's slice, from grad_shard[k] (one launch)."""
+        self.t += 1
+        bc1 = 1.0 - self.beta1 ** self.t
+        bc2s = (1.0 - self.beta2 ** self.t) ** 0.5
+        entries = []
+        g = self.grad_shard[k]
+        for i, a, b in self.pieces:
+            s, e = a - self.lo, b - self.lo
+            entries.append((self.param_flat[a:b], g[s:e], self.exp_avg[s:e], self.exp_avg_sq[s:e],
+                            (self.lr[i] / bc1) * -1, bc2s))
+        self._apply(k, entries)
+
+    def _apply(self, k, entries) -> None:
+        if not entries:
+            return
+        if len(entries) > _lib.GS_ADAM_MAX_TENSORS:
+            raise _lib.GsplatError(f"ShardedAdam: {len(entries)} parameter pieces > {_lib.GS_ADAM_MAX_TENSORS}")
+        if not self.param_flat.is_cuda:
+            raise _lib.GsplatError("ShardedAdam: the update is the HIP kernel (device parameters only)")
+        args = self._args.get(k)
+        if args is None:  # the pointers are fixed for the optimizer's life; only the step fields change
+            args = self._args[k] = _lib.GsAdamArgs(n_tensors=len(entries), beta1=self.beta1, beta2=self.beta2,
+                                                   eps=self.eps)
+            for j, (p, g, m, v, _, _) in enumerate(entries):
+                tj = args.t[j]
+                tj.param, tj.grad, tj.exp_avg, tj.exp_avg_sq = p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr()
+                tj.numel = p.numel()
+        for j, (_, _, _, _, step_size, bc2s) in enumerate(entries):
+            args.t[j].step_size, args.t[j].bc2_sqrt = step_size, bc2s
+        _lib.check(_lib.load().gs_adam_step(ctypes.byref(args), None,
+                                            torch.cuda.current_stream(self.param_flat.device).cuda_stream),
+                   "sharded adam step")
+
+    def step(self, k: int = 0) -> None:
+        """reduce_scatter(k) -> update(k) -> all_gather(), in line."""
+        self.reduce_scatter(k)
+        self.update(k)
+        self.all_gather()

@@ -432,7 +432,8 @@ class _RasterizeGaussiansBatch(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, means3D, means2D, sh, colors_precomp, semantic_feature, opacities, scales, rotations,
-                cov3Ds_precomp, cams, label, densify_out, raw_params=False, feature_ready=None, plan_state=None):
+                cov3Ds_precomp, cams, label, densify_out, raw_params=False, feature_ready=None, plan_state=None,
+                grad_into=None):
         if not isinstance(cams, _BatchCameras):
             cams = _BatchCameras(cams)
         rs0 = cams.rs0
@@ -459,6 +460,10 @@ class _RasterizeGaussiansBatch(torch.autograd.Function):
         ctx.C = C
         ctx.densify_out = densify_out
         ctx.raw_params = raw_params
+        ctx.grad_into = _grad_destinations(grad_into, semantic_feature)
+        if ctx.grad_into and isinstance(label, torch.Tensor) and not (
+                label.dim() == 1 and label.numel() == means3D.size(0) and label.dtype in _FUSABLE_LABEL_DTYPES):
+            raise ValueError("grad_into needs a per-Gaussian float label (applied in-kernel) or none")
         ctx.set_materialize_grads(False)
         ctx.sem_shape = None if semantic_feature is None else tuple(semantic_feature.shape)
         ctx.save_for_backward(colors_precomp, semantic_feature, means3D, scales, rotations, cov3Ds_precomp,
@@ -484,7 +489,7 @@ class _RasterizeGaussiansBatch(torch.autograd.Function):
             cov3Ds_precomp, views, projs, *cam4, grad_color, grad_out_feature, grad_depth, grad_alpha, sh,
             rs0.sh_degree, cpos, geom, ctx.num_instances, binning, img, alpha, rs0.debug, compat=ctx.compat,
             grad_mask=label if fuse else None, densify=ctx.densify_out, opacity=raw_opacities,
-            activate=ctx.raw_params, windows=windows)
+            activate=ctx.raw_params, windows=windows, out=ctx.grad_into)
         (grad_means2D, grad_colors_precomp, grad_semantic_feature, grad_opacities, grad_means3D,
          grad_cov3Ds_precomp, grad_sh, grad_scales, grad_rotations) = grads
         if ctx.sem_shape is not None:
@@ -505,13 +510,39 @@ class _RasterizeGaussiansBatch(torch.autograd.Function):
             grad_cov3Ds_precomp = grad_cov3Ds_precomp * lab
         grads = (grad_means3D, grad_means2D, grad_sh, grad_colors_precomp, grad_semantic_feature,
                  grad_opacities, grad_scales, grad_rotations, grad_cov3Ds_precomp, None, None, None, None, None,
-                 None)
-        return tuple(g if need else None for g, need in zip(grads, ctx.needs_input_grad))
+                 None, None)
+        # gradients written into caller-owned destinations: autograd gets None
+        taken = [False] * len(grads)
+        for k in (ctx.grad_into or {}):
+            taken[_GRAD_SLOT[k]] = True
+        return tuple(g if (need and not t) else None for g, need, t in zip(grads, ctx.needs_input_grad, taken))
+
+
+# backward_buffers' gradient name -> _RasterizeGaussiansBatch.forward argument slot
+_GRAD_SLOT = dict(dmeans3D=0, dmeans2D=1, dsh=2, dcolors=3, dsem=4, dopacity=5, dscales=6, drot=7, dcov3D=8)
+# GaussianRasterizer argument name -> backward_buffers' gradient name
+_GRAD_NAME = dict(means3D="dmeans3D", means2D="dmeans2D", shs="dsh", colors_precomp="dcolors",
+                  semantic_feature="dsem", opacities="dopacity", scales="dscales", rotations="drot",
+                  cov3D_precomp="dcov3D")
+
+
+def _grad_destinations(grad_into, semantic_feature):
+    """{argument name: tensor} -> backward_batch's {gradient name: tensor}."""
+    if not grad_into:
+        return None
+    out = {}
+    for k, t in grad_into.items():
+        if k not in _GRAD_NAME:
+            raise ValueError(f"grad_into: unknown argument '{k}' (one of {sorted(_GRAD_NAME)})")
+        if not isinstance(t, torch.Tensor):
+            raise TypeError(f"grad_into['{k}'] must be a tensor")
+        out[_GRAD_NAME[k]] = t
+    return out
 
 
 def rasterize_gaussians_batch(means3D, means2D, sh, colors_precomp, semantic_feature, opacities, scales,
                               rotations, cov3Ds_precomp, settings_list, label=None, densify_out=None,
-                              raw_params=False, feature_ready=None, plan_state=None):
+                              raw_params=False, feature_ready=None, plan_state=None, grad_into=None):
     """rasterize_gaussians over a list of camera settings; outputs [C, ...]
     (color, radii, feature_map, depth, alpha).  `densify_out`: optional
     (accum, denom, max_radius) fp32 [P] tensors the backward fills with the
@@ -522,11 +553,17 @@ def rasterize_gaussians_batch(means3D, means2D, sh, colors_precomp, semantic_fea
     `feature_ready`: a recorded torch.cuda.Event the blend waits for before it
     reads semantic_feature (an overlapped optimizer update of the features on
     another stream; gs_gaussians.feature_ready).  `plan_state`: a
-    _C.BinningPlan for the sync-free forward (gs_forward_batch)."""
+    _C.BinningPlan for the sync-free forward (gs_forward_batch).
+    `grad_into`: {argument name: tensor} -- the backward WRITES those
+    arguments' camera-summed gradients into the given tensors (e.g. a
+    gradient bucket's views, distributed.ShardedAdam.grad_views) and hands
+    autograd None for them, so no gradient tensor is allocated, accumulated
+    or copied into a bucket; gradients reaching those tensors through other
+    autograd paths are not added."""
     cams = settings_list if isinstance(settings_list, _BatchCameras) else _BatchCameras(list(settings_list))
     return _RasterizeGaussiansBatch.apply(means3D, means2D, sh, colors_precomp, semantic_feature, opacities,
                                           scales, rotations, cov3Ds_precomp, cams, label, densify_out,
-                                          bool(raw_params), feature_ready, plan_state)
+                                          bool(raw_params), feature_ready, plan_state, grad_into)
 
 
 class GaussianRasterizerBatch(nn.Module):
@@ -568,10 +605,13 @@ class GaussianRasterizerBatch(nn.Module):
         self.densify_stats = None
 
     def forward(self, means3D, means2D, opacities=None, shs=None, semantic_feature=None, colors_precomp=None,
-                scales=None, rotations=None, cov3D_precomp=None, label=_UNSET, feature_ready=None):
+                scales=None, rotations=None, cov3D_precomp=None, label=_UNSET, feature_ready=None,
+                grad_into=None):
         """The GaussianRasterizer call; `feature_ready` (keyword, optional): a
         recorded torch.cuda.Event the blend waits for before reading
-        semantic_feature (gs_gaussians.feature_ready)."""
+        semantic_feature (gs_gaussians.feature_ready).  `grad_into` (keyword,
+        optional): {argument name: tensor} destinations the backward writes
+        those gradients into (rasterize_gaussians_batch)."""
         if (shs is None and colors_precomp is None) or (shs is not None and colors_precomp is not None):
             raise Exception('Please provide excatly one of either SHs or precomputed colors!')
         if ((scales is None or rotations is None) and cov3D_precomp is None) or \
@@ -592,7 +632,7 @@ class GaussianRasterizerBatch(nn.Module):
             self.densify_stats = {"means2D_gradient_accum": dens[0], "denom": dens[1], "max_2D_radius": dens[2]}
         color, radii, feature_map, depth, alpha = rasterize_gaussians_batch(
             means3D, means2D, shs, colors_precomp, semantic_feature, opacities, scales, rotations,
-            cov3D_precomp, self._cams, lab, dens, self.raw_params, feature_ready, self.plan)
+            cov3D_precomp, self._cams, lab, dens, self.raw_params, feature_ready, self.plan, grad_into)
         has_sem = semantic_feature is not None
         if has_label and has_sem:      # G3
             return color, radii, feature_map, depth, alpha

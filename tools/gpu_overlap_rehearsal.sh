@@ -1,7 +1,15 @@
-# bench.py's overlapped feature all-reduce (N > 1) rehearsed with two ranks on
-# the box's one GPU over gloo: the parameters after the timed steps must match
-# the unoverlapped exchange (GS_BENCH_OVERLAP=0) to within the run-to-run
-# noise of the float-atomic gradient sums (tools/compare_params.py).
+# bench.py's gradient exchanges at N > 1 rehearsed on the box's one GPU; the
+# parameters after the timed steps of every variant must match the plain
+# exchange (GS_BENCH_ZERO=0 GS_BENCH_OVERLAP=0: one all-reduce, the full Adam
+# on every rank) to within the run-to-run noise of the float-atomic gradient
+# sums (tools/compare_params.py against two runs of the plain exchange):
+#   zov  the default: sharded Adam (reduce-scatter, 1/N update, all-gather)
+#        with the feature exchange behind the next step
+#   z    sharded Adam, in line
+#   ov   all-reduce with the overlapped feature exchange
+# First two ranks over gloo (sharing the GPU), then the same over RCCL at a
+# world of one (RCCL refuses two ranks on one GPU; the =force settings run
+# the collectives there anyway).
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd $R
@@ -13,19 +21,26 @@ run() {  # name, port, extra env
     --nproc-per-node 2 --master-addr 127.0.0.1 --master-port $2 bench.py $A --dump-params $O/$1.npz \
     > $O/$1.json 2> $O/$1.err || { tail -20 $O/$1.err; exit 1; }
 }
-run ov1 29561 GS_BENCH_OVERLAP=1 && run ov0a 29562 GS_BENCH_OVERLAP=0 && run ov0b 29563 GS_BENCH_OVERLAP=0 || exit 1
-python -c "import json; d=json.load(open('$O/ov1.json')); print(d['config']['grad_exchange'], d['ms_per_step'])"
-python tools/compare_params.py $O/ov1.npz $O/ov0a.npz $O/ov0b.npz || { rm -f $O/*.npz; exit 1; }
-# The same exchange over RCCL at a world of one (RCCL refuses two ranks on one
-# GPU): GS_BENCH_OVERLAP=force runs the async all-reduce on RCCL's stream and
-# the side stream's wait on it; its parameters against two unoverlapped runs.
-rrun() {  # name, port, overlap setting
-  env GS_BENCH_FORCE_DIST=1 GS_BENCH_OVERLAP=$3 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 \
+run ref_a 29561 "GS_BENCH_ZERO=0 GS_BENCH_OVERLAP=0" && run ref_b 29562 "GS_BENCH_ZERO=0 GS_BENCH_OVERLAP=0" \
+  && run zov 29563 "GS_BENCH_ZERO=1 GS_BENCH_OVERLAP=1" && run z 29564 "GS_BENCH_ZERO=1 GS_BENCH_OVERLAP=0" \
+  && run ov 29565 "GS_BENCH_ZERO=0 GS_BENCH_OVERLAP=1" || exit 1
+rc=0
+for t in zov z ov; do
+  python -c "import json; d=json.load(open('$O/$t.json')); print('$t:', d['config']['grad_exchange'], d['ms_per_step'])"
+  python tools/compare_params.py $O/$t.npz $O/ref_a.npz $O/ref_b.npz || rc=1
+done
+rrun() {  # name, port, extra env
+  env GS_BENCH_FORCE_DIST=1 $3 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 \
     --nproc-per-node 1 --master-addr 127.0.0.1 --master-port $2 bench.py ${A/--gpus 2/--gpus 1} \
     --dump-params $O/$1.npz > $O/$1.json 2> $O/$1.err || { tail -20 $O/$1.err; exit 1; }
 }
-rrun rccl_ov1 29571 force && rrun rccl_ov0a 29572 0 && rrun rccl_ov0b 29573 0 || exit 1
-python -c "import json; d=json.load(open('$O/rccl_ov1.json')); print(d['config']['grad_exchange'], d['ms_per_step'])"
-python tools/compare_params.py $O/rccl_ov1.npz $O/rccl_ov0a.npz $O/rccl_ov0b.npz; rc=$?
+rrun rccl_ref_a 29571 "GS_BENCH_ZERO=0 GS_BENCH_OVERLAP=0" && rrun rccl_ref_b 29572 "GS_BENCH_ZERO=0 GS_BENCH_OVERLAP=0" \
+  && rrun rccl_zov 29573 "GS_BENCH_ZERO=force GS_BENCH_OVERLAP=force" \
+  && rrun rccl_z 29574 "GS_BENCH_ZERO=force GS_BENCH_OVERLAP=0" \
+  && rrun rccl_ov 29575 "GS_BENCH_ZERO=0 GS_BENCH_OVERLAP=force" || exit 1
+for t in rccl_zov rccl_z rccl_ov; do
+  python -c "import json; d=json.load(open('$O/$t.json')); print('$t:', d['config']['grad_exchange'], d['ms_per_step'])"
+  python tools/compare_params.py $O/$t.npz $O/rccl_ref_a.npz $O/rccl_ref_b.npz || rc=1
+done
 rm -f $O/*.npz  # the dumps are large; the comparisons above are the record
 exit $rc
