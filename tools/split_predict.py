@@ -11,10 +11,14 @@ its runs) plus the exposed gradient exchange:
     2 densification statistics -- as a ring all-reduce, 2 (N - 1) / N x bytes
     over a bus rate;
   * overlapped (bench.py's exchange at N > 1, F > 0): the geometry bucket
-    (14 fp32 per Gaussian) all-reduced before Adam, the feature bucket
-    all-reduced and stepped on a side stream behind the next step's
+    (14 fp32 per Gaussian) exchanged before the next step, the feature bucket
+    exchanged and stepped on a side stream behind the next step's
     projection and binning (gs_gaussians.feature_ready), so only the part of
-    it longer than the rank's pre-blend stages stays exposed.
+    it longer than the rank's pre-blend stages stays exposed.  With the
+    sharded Adam (distributed.ShardedAdam, the default for a rank of N) an
+    exchange is a reduce-scatter and an all-gather: (N - 1) / N x bytes
+    each, the ring all-reduce's 2 (N - 1) / N in total, so the same bus
+    time; the proxies run the rank's 1/N Adam slice.
 Rates: one xGMI link (153 GB/s, a single ring on the point-to-point fabric)
 and 300 GB/s (RCCL's rings over several of the 7 links).  The proxies also
 run the feature Adam step in line, which the overlapped exchange moves to
