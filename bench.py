@@ -621,7 +621,9 @@ def main():
     # kernels (GradientSink: GS_FLAG_ACCUMULATE into per-stream buffers)
     # instead of autograd adding 7 gradient tensors per camera into the
     # leaves; GS_BENCH_SINK=0 restores autograd's accumulation.
-    use_sink = os.environ.get("GS_BENCH_SINK", "1") != "0"
+    # (one camera: nothing to sum -- the per-camera step is then exactly the
+    # reference's train.py iteration: activations, render, backward, Adam)
+    use_sink = os.environ.get("GS_BENCH_SINK", "1") != "0" and len(my_cams) > 1
     sink = GradientSink() if use_sink else None
     settings = make_settings(my_cams, dev, args.compat, sink, my_windows)
     # the CPU-baseline / PSNR leg renders the initial scene (independent of the
@@ -922,9 +924,44 @@ def main():
         if split_opt:
             opt_feat.step()
 
+    def step_single_camera():
+        """The per-camera drop-in with one camera: the reference's training
+        iteration as train.py writes it (params2rendervar's activations in
+        torch, GaussianRasterizer, one backward, the optimizer step)."""
+        drain()
+        if zero:
+            for o_, b_ in zero_buffers(0):
+                o_.bind(b_)
+                o_.zero_grad(b_)
+        else:
+            if overlap:
+                feat_buckets[0].bind()
+                feat_buckets[0].zero_grad()
+            bucket.zero_grad()
+        rv = params2rendervar(params, label)
+        ras = GaussianRasterizer(settings[0])
+        if up_feat is not None:
+            im, _, feat, depth, _ = ras(**rv)
+            torch.autograd.backward([im, depth, feat], [up_color, up_depth, up_feat])
+        else:
+            im, _, depth, _ = ras(**rv)
+            torch.autograd.backward([im, depth], [up_color, up_depth])
+        if zero:
+            for o_, b_ in zero_buffers(0):
+                o_.step(b_)
+            return
+        bucket.all_reduce()
+        opt.step()
+        if overlap:
+            feat_buckets[0].all_reduce()
+        if split_opt:
+            opt_feat.step()
+
     def step(mode=args.mode):
         if mode == "batch":
             return step_batch()
+        if len(settings) == 1:
+            return step_single_camera()
         drain()
         if zero:
             for o_, b_ in zero_buffers(0):
@@ -1025,8 +1062,8 @@ def main():
     # the other call pattern on the same scene, timed the same way (reported
     # beside the headline: the per-camera drop-in or the camera batch)
     other = "percam" if args.mode == "batch" else "batch"
-    if my_windows is not None:
-        other = None  # the per-camera drop-in renders whole cameras only
+    if my_windows is not None or os.environ.get("GS_BENCH_OTHER") == "0":
+        other = None  # the per-camera drop-in renders whole cameras only (GS_BENCH_OTHER=0: not timed)
     for _ in range(args.warmup if other else 0):
         step(other)
     torch.cuda.synchronize()
@@ -1174,7 +1211,9 @@ def main():
                    "activations": ("in-kernel (raw parameters, GS_FLAG_ACTIVATE)" if raw and args.mode == "batch"
                                    else "torch ops (params2rendervar)"),
                    "grad_sum": ("in-kernel (camera sum in preprocess_bwd)" if args.mode == "batch" else
-                                "in-kernel (GradientSink)" if use_sink else "autograd"),
+                                "in-kernel (GradientSink)" if use_sink else
+                                "none (one camera: the reference's train.py iteration)" if len(my_cams) == 1 else
+                                "autograd"),
                    "gaussians": args.gaussians, "cams_per_rank": len(my_cams), "width": W_,
                    "height": H_, "feature_channels": args.features, "compat": args.compat,
                    "parallelism": f"camera-sharded dp{world}",
