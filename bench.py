@@ -578,6 +578,10 @@ def cpu_baseline(args, params, label, cam, settings, dev):
 
 def main():
     args = parse()
+    if os.environ.get("GS_BENCH_TRACEBACKS"):
+        # debugging a stuck run: every thread's Python stack to stderr every N s
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["GS_BENCH_TRACEBACKS"]), repeat=True, file=sys.stderr)
     # The bench line is the only output on stdout: native libraries may print
     # there (RCCL writes a version banner on rank 0 when the communicator
     # comes up), so fd 1 goes to stderr for the run and the line is written
@@ -1062,8 +1066,12 @@ def main():
     # the other call pattern on the same scene, timed the same way (reported
     # beside the headline: the per-camera drop-in or the camera batch)
     other = "percam" if args.mode == "batch" else "batch"
-    if my_windows is not None or os.environ.get("GS_BENCH_OTHER") == "0":
-        other = None  # the per-camera drop-in renders whole cameras only (GS_BENCH_OTHER=0: not timed)
+    # The per-camera drop-in renders whole cameras only.  The decision must be
+    # the same on every rank (the other mode's steps hold collectives): a
+    # split's ranks differ in whether they hold a window, so a split over
+    # N > 1 ranks skips it on all of them.  GS_BENCH_OTHER=0: not timed.
+    if my_windows is not None or (strong and world > 1) or os.environ.get("GS_BENCH_OTHER") == "0":
+        other = None
     for _ in range(args.warmup if other else 0):
         step(other)
     torch.cuda.synchronize()

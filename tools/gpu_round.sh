@@ -28,12 +28,14 @@ tail -2 $O/tests.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { cat $O/smoke.log; exit 3; }
 tail -1 $O/smoke.log
 fi
+if [ "${SKIP_BENCH:-0}" != "1" ]; then
 timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err || { tail $O/bench.err; exit 4; }
 cat $O/bench.json
 cd /tmp && export TMPDIR=/tmp
 rm -rf $O/bprof
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/bprof -o bench --output-format csv -- python3 $R/bench.py --no-cpu-baseline > $O/bench_under_rocprof.json 2> $O/bprof.err || exit 5
 cat $O/bench_under_rocprof.json
+fi
 cd $R
 if [ "${SKIP_DIST:-0}" != "1" ]; then
 GS_BENCH_BACKEND=gloo GS_BENCH_SHARE_GPU=1 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 > $O/dist2_weak.json 2> $O/dist2_weak.err || { tail $O/dist2_weak.err; exit 6; }
