@@ -1,27 +1,50 @@
 #!/usr/bin/env python3
 """Compare parameter dumps of bench.py runs (--dump-params): the run under
-test against a reference run and a repeat of the reference (the noise floor
-of float-atomic summation order).  Prints per tensor the mean / max absolute
-difference and exits non-zero if the tested run's mean difference exceeds
-max(3 x the floor, 1e-7).
+test against a reference run and one or more repeats of the reference (the
+noise floor of float-atomic summation order).
 
-    python tools/compare_params.py test.npz ref.npz ref_repeat.npz
+The statistic is the mean absolute difference over each tensor's elements
+after dropping the largest 0.1 % (`trimmed`): a few training steps amplify
+the order noise through discrete events -- one Gaussian's alpha crossing
+1/255 at one pixel in one run and not the other -- that move single
+elements by 1e-4..1e-2 in any pair of runs, so the plain mean of one pair
+is heavy-tailed; a systematic error (a wrong exchange, a lost slice) moves
+most elements and shows in the trimmed mean.  The floor is the largest
+trimmed mean over the reference pairs.  OK iff, for every tensor, the
+tested run's trimmed mean <= max(3 x floor, 1e-9).  The plain mean and max
+are printed beside it.
+
+    python tools/compare_params.py test.npz ref.npz ref_repeat.npz [ref_repeat2.npz ...]
 """
 import json
 import sys
 
 import numpy as np
 
+TRIM = 0.001
+
+
+def trimmed_mean(d):
+    d = np.sort(d.reshape(-1))
+    keep = d.size - int(d.size * TRIM)
+    return float(d[:keep].mean()) if keep > 0 else 0.0
+
 
 def main():
-    t, a, b = (np.load(p) for p in sys.argv[1:4])
+    t, a = np.load(sys.argv[1]), np.load(sys.argv[2])
+    reps = [np.load(p) for p in sys.argv[3:]]
+    if not reps:
+        raise SystemExit("need at least one repeat of the reference")
     out, ok = {}, True
     for k in a.files:
-        d = np.abs(t[k].astype(np.float64) - a[k])
-        f = np.abs(b[k].astype(np.float64) - a[k])
-        out[k] = {"mean": float(d.mean()), "max": float(d.max()), "floor_mean": float(f.mean()),
-                  "floor_max": float(f.max())}
-        ok &= out[k]["mean"] <= max(3 * out[k]["floor_mean"], 1e-7)
+        ref = a[k].astype(np.float64)
+        d = np.abs(t[k].astype(np.float64) - ref)
+        floors = [np.abs(r[k].astype(np.float64) - ref) for r in reps]
+        fl = max(trimmed_mean(f) for f in floors)
+        out[k] = {"trimmed_mean": trimmed_mean(d), "floor_trimmed_mean": fl, "mean": float(d.mean()),
+                  "max": float(d.max()), "floor_mean": max(float(f.mean()) for f in floors),
+                  "floor_max": max(float(f.max()) for f in floors)}
+        ok &= out[k]["trimmed_mean"] <= max(3 * fl, 1e-9)
     print(json.dumps(out, indent=1))
     print("OK" if ok else "MISMATCH")
     sys.exit(0 if ok else 1)

@@ -2,7 +2,7 @@
 # parameters after the timed steps of every variant must match the plain
 # exchange (GS_BENCH_ZERO=0 GS_BENCH_OVERLAP=0: one all-reduce, the full Adam
 # on every rank) to within the run-to-run noise of the float-atomic gradient
-# sums (tools/compare_params.py against two runs of the plain exchange):
+# sums (tools/compare_params.py against three runs of the plain exchange):
 #   zov  the default: sharded Adam (reduce-scatter, 1/N update, all-gather)
 #        with the feature exchange behind the next step
 #   z    sharded Adam, in line
@@ -22,12 +22,13 @@ run() {  # name, port, extra env
     > $O/$1.json 2> $O/$1.err || { tail -20 $O/$1.err; exit 1; }
 }
 run ref_a 29561 "GS_BENCH_ZERO=0 GS_BENCH_OVERLAP=0" && run ref_b 29562 "GS_BENCH_ZERO=0 GS_BENCH_OVERLAP=0" \
+  && run ref_c 29566 "GS_BENCH_ZERO=0 GS_BENCH_OVERLAP=0" \
   && run zov 29563 "GS_BENCH_ZERO=1 GS_BENCH_OVERLAP=1" && run z 29564 "GS_BENCH_ZERO=1 GS_BENCH_OVERLAP=0" \
   && run ov 29565 "GS_BENCH_ZERO=0 GS_BENCH_OVERLAP=1" || exit 1
 rc=0
 for t in zov z ov; do
   python -c "import json; d=json.load(open('$O/$t.json')); print('$t:', d['config']['grad_exchange'], d['ms_per_step'])"
-  python tools/compare_params.py $O/$t.npz $O/ref_a.npz $O/ref_b.npz || rc=1
+  python tools/compare_params.py $O/$t.npz $O/ref_a.npz $O/ref_b.npz $O/ref_c.npz || rc=1
 done
 rrun() {  # name, port, extra env
   env GS_BENCH_FORCE_DIST=1 $3 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 \
@@ -35,12 +36,13 @@ rrun() {  # name, port, extra env
     --dump-params $O/$1.npz > $O/$1.json 2> $O/$1.err || { tail -20 $O/$1.err; exit 1; }
 }
 rrun rccl_ref_a 29571 "GS_BENCH_ZERO=0 GS_BENCH_OVERLAP=0" && rrun rccl_ref_b 29572 "GS_BENCH_ZERO=0 GS_BENCH_OVERLAP=0" \
+  && rrun rccl_ref_c 29576 "GS_BENCH_ZERO=0 GS_BENCH_OVERLAP=0" \
   && rrun rccl_zov 29573 "GS_BENCH_ZERO=force GS_BENCH_OVERLAP=force" \
   && rrun rccl_z 29574 "GS_BENCH_ZERO=force GS_BENCH_OVERLAP=0" \
   && rrun rccl_ov 29575 "GS_BENCH_ZERO=0 GS_BENCH_OVERLAP=force" || exit 1
 for t in rccl_zov rccl_z rccl_ov; do
   python -c "import json; d=json.load(open('$O/$t.json')); print('$t:', d['config']['grad_exchange'], d['ms_per_step'])"
-  python tools/compare_params.py $O/$t.npz $O/rccl_ref_a.npz $O/rccl_ref_b.npz || rc=1
+  python tools/compare_params.py $O/$t.npz $O/rccl_ref_a.npz $O/rccl_ref_b.npz $O/rccl_ref_c.npz || rc=1
 done
 rm -f $O/*.npz  # the dumps are large; the comparisons above are the record
 exit $rc
