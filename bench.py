@@ -790,6 +790,8 @@ def main():
     arg_of = {"means3D": "means3D", "rgb_colors": "colors_precomp", "unnorm_rotations": "rotations",
               "logit_opacities": "opacities", "log_scales": "scales", "semantic_feature": "semantic_feature"}
 
+    zero_dest = {}  # step parity -> the backward's gradient destinations
+
     def zero_buffers(k):
         """(sharded optimizer, gradient buffer) pairs of step parity k."""
         return [(zgeo, 0), (zfeat, k)] if overlap else [(zopt, 0)]
@@ -808,9 +810,10 @@ def main():
             main.wait_event(pending)
         rv = raw_rendervar(params, label, means2D_placeholder)
         if len(parts) == 1:
-            dest = {}
-            for o_, b_ in zero_buffers(kb):
-                dest.update({arg_of[n_]: t_ for n_, t_ in o_.grad_views(b_).items()})
+            dest = zero_dest.get(kb)
+            if dest is None:
+                dest = zero_dest[kb] = {arg_of[n_]: t_ for o_, b_ in zero_buffers(kb)
+                                        for n_, t_ in o_.grad_views(b_).items()}
             run_part(parts[0][0], parts[0][1], rv, ready=pipe["done"][(k - 1) % 2] if overlap else None,
                      grad_into=dest)
         else:

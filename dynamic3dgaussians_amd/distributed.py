@@ -505,9 +505,12 @@ class ShardedAdam:
 
     # ------------------------------------------------------------ gradients
     def grad_views(self, k: int = 0) -> Dict[str, torch.Tensor]:
-        """{name: view of gradient buffer k shaped like the parameter}."""
-        g = self.grad_flat[k]
-        return {name: g[o:o + p.numel()].view_as(p) for name, p, o in zip(self.names, self.params, self.offsets)}
+        """{name: view of gradient buffer k shaped like the parameter} (the
+        same view objects on every call: the buffers never move)."""
+        if not hasattr(self, "_gviews"):
+            self._gviews = [{name: g[o:o + p.numel()].view_as(p)
+                             for name, p, o in zip(self.names, self.params, self.offsets)} for g in self.grad_flat]
+        return dict(self._gviews[k])
 
     def bind(self, k: int = 0) -> None:
         """Make every parameter's .grad its view into gradient buffer k."""
