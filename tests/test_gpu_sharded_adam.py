@@ -95,15 +95,16 @@ def test_ranks_slices_assemble_to_the_full_update(world):
     assert torch.equal(got, ref_flat)
 
 
-def _cams(n, W, H):
+def _cams(n, W, H, windows=None):
     out = []
-    for c in camera_rig(n, W, H, seed=3):
+    for i, c in enumerate(camera_rig(n, W, H, seed=3)):
+        kw = {} if windows is None or windows[i] is None else {"tile_window": windows[i]}
         out.append(GaussianRasterizationSettings(
             image_height=H, image_width=W, tanfovx=c.tanfovx, tanfovy=c.tanfovy, c_x=c.c_x, c_y=c.c_y,
             bg=torch.tensor([0.1, 0.2, 0.3], device=DEV),
             viewmatrix=torch.from_numpy(c.viewmatrix.copy()).to(DEV),
             projmatrix=torch.from_numpy(c.projmatrix.copy()).to(DEV), sh_degree=0,
-            campos=torch.from_numpy(c.campos.copy()).to(DEV)))
+            campos=torch.from_numpy(c.campos.copy()).to(DEV), **kw))
     return out
 
 
@@ -122,10 +123,22 @@ def _step(ras, params, label, ups, grad_into=None):
         torch.autograd.backward([im, depth], ups[:2])
 
 
-@pytest.mark.parametrize("F", [0, 32])
-def test_grad_into_writes_autograds_gradients(F):
+@pytest.mark.parametrize("F,binding,windows", [(0, "native", False), (32, "native", False),
+                                               (32, "ctypes", False), (32, "native", True)])
+def test_grad_into_writes_autograds_gradients(F, binding, windows):
+    from dynamic3dgaussians_amd import _C
     P, W, H, C = 6000, 160, 128, 3
-    sets = _cams(C, W, H)
+    sets = _cams(C, W, H, [None, (0, 2, 10, 6), (3, 0, 10, 8)] if windows else None)
+    assert _C.native_loaded(), "the native binding did not load"
+    keep = _C._native
+    try:
+        _C._native = keep if binding == "native" else None
+        _grad_into_case(sets, P, W, H, C, F)
+    finally:
+        _C._native = keep
+
+
+def _grad_into_case(sets, P, W, H, C, F):
     gen = torch.Generator(device=DEV).manual_seed(11)
     ups = [torch.randn(C, 3, H, W, device=DEV, generator=gen), torch.randn(C, 1, H, W, device=DEV, generator=gen),
            torch.randn(C, F, H, W, device=DEV, generator=gen) if F else None]
