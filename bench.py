@@ -576,6 +576,17 @@ def cpu_baseline(args, params, label, cam, settings, dev):
     return cb, psnr, psnr_gt
 
 
+def other_mode(mode, has_windows, strong, world, enabled=True):
+    """The call pattern timed beside the headline (the per-camera drop-in
+    or the camera batch), or None.  The per-camera drop-in renders whole
+    cameras only, and the decision must be the same on every rank (the other
+    mode's steps hold collectives): a split's ranks differ in whether they
+    hold a window, so a split over N > 1 ranks skips it on all of them."""
+    if not enabled or has_windows or (strong and world > 1):
+        return None
+    return "percam" if mode == "batch" else "batch"
+
+
 def main():
     args = parse()
     if os.environ.get("GS_BENCH_TRACEBACKS"):
@@ -1068,13 +1079,7 @@ def main():
 
     # the other call pattern on the same scene, timed the same way (reported
     # beside the headline: the per-camera drop-in or the camera batch)
-    other = "percam" if args.mode == "batch" else "batch"
-    # The per-camera drop-in renders whole cameras only.  The decision must be
-    # the same on every rank (the other mode's steps hold collectives): a
-    # split's ranks differ in whether they hold a window, so a split over
-    # N > 1 ranks skips it on all of them.  GS_BENCH_OTHER=0: not timed.
-    if my_windows is not None or (strong and world > 1) or os.environ.get("GS_BENCH_OTHER") == "0":
-        other = None
+    other = other_mode(args.mode, my_windows is not None, strong, world, os.environ.get("GS_BENCH_OTHER") != "0")
     for _ in range(args.warmup if other else 0):
         step(other)
     torch.cuda.synchronize()

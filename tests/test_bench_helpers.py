@@ -70,3 +70,18 @@ def test_committed_bench_line_has_no_fraction_above_one():
             line = json.load(f)
         for k, v in fracs(line["roofline"]):
             assert 0 <= v <= 1.0, (path, k, v)
+
+
+@pytest.mark.parametrize("world", [1, 2, 8])
+def test_other_mode_is_the_same_on_every_rank_of_a_split(world):
+    # the ranks of a split differ in whether they hold a tile window; the
+    # comparison's steps hold collectives, so the decision may not depend on it
+    # (a weak-scaling rank holds whole cameras only; at one rank a split
+    # is whole cameras too)
+    if world > 1:
+        got = {bench.other_mode("batch", w, True, world) for w in (False, True)}
+        assert got == {None}, got
+    assert bench.other_mode("batch", False, False, world) == "percam"
+    assert bench.other_mode("percam", False, False, world) == "batch"
+    assert bench.other_mode("batch", False, False, world, enabled=False) is None
+    assert bench.other_mode("batch", False, True, 1) == "percam"  # one rank: whole cameras
