@@ -101,7 +101,7 @@ def parse():
                     help="one GPU standing in for rank --proxy-rank of an N-rank --cams-total split: the "
                          "rank's own cameras and windows, no collective (the per-rank shape)")
     ap.add_argument("--proxy-rank", type=int, default=0)
-    ap.add_argument("--cpu-tiles", type=int, default=10,
+    ap.add_argument("--cpu-tiles", type=int, default=20,
                     help="CPU baseline sample: a TxT block of 16x16 tiles at the centre of camera 0")
     ap.add_argument("--width", type=int, default=800)
     ap.add_argument("--height", type=int, default=800)
