@@ -1,0 +1,63 @@
+"""The analysis tools the round's GPU evidence rests on, on synthetic inputs:
+tools/compare_params.py (the exchange rehearsals' verdict) and
+tools/split_predict.py (the configs[3] prediction)."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args):
+    return subprocess.run([sys.executable] + args, cwd=ROOT, capture_output=True, text=True)
+
+
+def test_compare_params_tolerates_order_noise_and_flips_but_not_a_systematic_error(tmp_path):
+    rng = np.random.default_rng(0)
+    base = rng.standard_normal(200_000).astype(np.float32)
+
+    def run_like():
+        x = base + rng.standard_normal(base.size).astype(np.float32) * 1e-8
+        x[rng.integers(0, base.size, 40)] += 1e-3  # discrete alpha-threshold flips
+        return x
+    paths = {}
+    for name in ("ref_a", "ref_b", "ref_c", "ok"):
+        paths[name] = str(tmp_path / f"{name}.npz")
+        np.savez(paths[name], p=run_like())
+    bad = run_like()
+    bad[::2] += 1e-6  # half the elements off: a lost contribution
+    paths["bad"] = str(tmp_path / "bad.npz")
+    np.savez(paths["bad"], p=bad)
+    refs = [paths["ref_a"], paths["ref_b"], paths["ref_c"]]
+    ok = _run(["tools/compare_params.py", paths["ok"]] + refs)
+    assert ok.returncode == 0 and ok.stdout.strip().endswith("OK"), ok.stdout + ok.stderr
+    bad_r = _run(["tools/compare_params.py", paths["bad"]] + refs)
+    assert bad_r.returncode == 1 and bad_r.stdout.strip().endswith("MISMATCH"), bad_r.stdout + bad_r.stderr
+
+
+def test_split_predict_takes_the_slowest_rank_and_the_exposed_exchange(tmp_path):
+    full = {"ms_per_step": 9.0, "config": {"workload": "300k Gaussians x 27 cams"}}
+    fp = tmp_path / "full.json"
+    fp.write_text(json.dumps(full))
+    proxies = []
+    for r in range(8):
+        for rep, ms in enumerate((1.30 + 0.01 * r, 1.31 + 0.01 * r)):
+            d = {"ms_per_step": ms, "config": {"workload": f"rank {r} of 8 of 300k Gaussians x 27 cams split"},
+                 "stages_ms_per_step": {"preprocess": 0.06, "scan": 0.05, "duplicate": 0.05, "sort": 0.08,
+                                        "ranges": 0.01}}
+            p = tmp_path / f"p{r}_{rep}.json"
+            p.write_text(json.dumps(d))
+            proxies.append(str(p))
+    out = _run(["tools/split_predict.py", str(fp)] + proxies)
+    assert out.returncode == 0, out.stderr
+    d = json.loads(out.stdout)
+    assert d["slowest_rank"] == 7 and abs(d["slowest_rank_ms"] - 1.375) < 1e-9
+    pr = d["predictions"]["300GB/s overlapped"]
+    # geometry ring all-reduce of 300k x 14 fp32 at 300 GB/s, 8 ranks
+    geo = 2 * 7 / 8 * 300_000 * 14 * 4 / 300e9 * 1e3
+    assert abs(pr["geometry_allreduce_ms"] - round(geo, 3)) < 1e-9
+    assert abs(pr["step_ms"] - round(1.375 + pr["exposed_ms"], 4)) < 1e-4
+    assert abs(pr["speedup_vs_1gpu"] - round(9.0 / pr["step_ms"], 3)) < 1e-3
