@@ -770,6 +770,9 @@ def main():
     # the sync-free forward (gs_forward_batch; GS_BENCH_SYNC_FREE=0: the
     # two-phase plan -> host read -> render order of the reference)
     sync_free = os.environ.get("GS_BENCH_SYNC_FREE", "1") != "0"
+    # the binning passes' walk in 3-D Morton order of the means
+    # (GaussianRasterizerBatch(spatial_order=True), gs_gaussians.walk_order)
+    walk = os.environ.get("GS_BENCH_WALK", "0") == "1"
     means2D_placeholder = torch.zeros_like(params["means3D"])
 
     # one upstream gradient per camera, materialized once (the batch's
@@ -782,7 +785,8 @@ def main():
             C_ = len(idx)
             ups = (up_color.expand(C_, -1, -1, -1).contiguous(), up_depth.expand(C_, -1, -1, -1).contiguous(),
                    up_feat.expand(C_, -1, -1, -1).contiguous() if up_feat is not None else None)
-            parts.append((GaussianRasterizerBatch([setts[i] for i in idx], raw_params=raw, sync_free=sync_free),
+            parts.append((GaussianRasterizerBatch([setts[i] for i in idx], raw_params=raw, sync_free=sync_free,
+                                                  spatial_order=walk),
                           ups, streams[gi]))
         return parts
 

@@ -242,6 +242,23 @@ def rasterize_gaussians(background, means3D, colors, semantic_feature, opacity, 
 _BUFFER_ORDER = ("dmeans2D", "dcolors", "dsem", "dopacity", "dmeans3D", "dcov3D", "dsh", "dscales", "drot")
 
 
+def spatial_order(means3D: torch.Tensor) -> torch.Tensor:
+    """gs_spatial_order: the ids 0..P-1 in 3-D Morton order of the means
+    (int32 [P] on the means' device) -- a walk order for the binning passes
+    (gs_gaussians.walk_order) that keeps each binning workgroup's slice of
+    the Gaussians compact on the screen."""
+    if not (means3D.is_cuda and means3D.dtype == torch.float32 and means3D.dim() == 2 and means3D.size(1) == 3):
+        raise RuntimeError("spatial_order: means3D must be an fp32 [P, 3] device tensor")
+    L_ = _lib.load()
+    m = means3D.detach().contiguous()
+    P = m.size(0)
+    order = torch.empty(P, dtype=torch.int32, device=m.device)
+    scratch = torch.empty(max(1, L_.gs_spatial_order_scratch_bytes(P)), dtype=torch.uint8, device=m.device)
+    check(L_.gs_spatial_order(P, m.data_ptr(), order.data_ptr(), scratch.data_ptr(), _stream(m.device)),
+          "spatial order")
+    return order
+
+
 _NO_DEST = torch.empty(0)  # backward_batch's `out` entry: allocate this gradient
 
 
@@ -497,7 +514,8 @@ class BinningPlan:
 def rasterize_gaussians_batch(background, means3D, colors, semantic_feature, opacity, scales, rotations,
                               scale_modifier, cov3D_precomp, viewmatrices, projmatrices, c_x, c_y, tan_fovx,
                               tan_fovy, image_height, image_width, sh, degree, campos, prefiltered, debug,
-                              *, compat=None, activate=False, windows=None, feature_ready=None, plan_state=None):
+                              *, compat=None, activate=False, windows=None, feature_ready=None, plan_state=None,
+                              walk_order=None):
     """The forward of C cameras at once (gs_forward_plan_batch +
     gs_forward_render_batch): the arguments of rasterize_gaussians with
     per-camera matrices stacked ([C,4,4] or [C,16], campos [C,3]) and the
@@ -516,7 +534,9 @@ def rasterize_gaussians_batch(background, means3D, colors, semantic_feature, opa
     does not fit (bit-identical outputs either way).  The returned
     num_instances is then the per-camera length the binning buffer is laid
     out with (what the backward takes); the exact counts are in
-    plan_state.num_instances."""
+    plan_state.num_instances.  `walk_order`: an int32 device tensor of the P
+    ids in the order the binning passes walk them (spatial_order), or None
+    (gs_gaussians.walk_order; outputs do not depend on it)."""
     L_ = _lib.load()
     sync_free = plan_state is not None and not debug
     cm = _compat_code(compat)
@@ -540,7 +560,7 @@ def rasterize_gaussians_batch(background, means3D, colors, semantic_feature, opa
                                     int(image_width), _opt(sh), int(degree), campos, bool(prefiltered),
                                     bool(debug), cm, bool(activate), _windows_arg(windows, C_),
                                     _event_handle(feature_ready), cap,
-                                    plan_state.hint if sync_free else [],
+                                    plan_state.hint if sync_free else [], _opt(walk_order),
                                     torch.cuda.current_stream(means3D.device).cuda_stream)
         except RuntimeError as ex:
             raise _lib.GsplatError(str(ex)) from None
@@ -564,6 +584,11 @@ def rasterize_gaussians_batch(background, means3D, colors, semantic_feature, opa
                 torch.empty(0, **u8), [0] * C)
     g = inp.struct(_lib.GS_FLAG_ACTIVATE if activate else 0)
     g.feature_ready = _event_handle(feature_ready) or None
+    if walk_order is not None:
+        if not (walk_order.is_cuda and walk_order.dtype == torch.int32 and walk_order.is_contiguous()
+                and walk_order.numel() == inp.P and walk_order.device == dev):
+            raise RuntimeError("walk_order must be a contiguous int32 device tensor of P ids")
+        g.walk_order = walk_order.data_ptr()
     out_color = torch.empty(C, 3, H, W, **f32)
     out_feature = torch.empty(C, inp.F, H, W, **f32)
     out_depth = torch.empty(C, 1, H, W, **f32)

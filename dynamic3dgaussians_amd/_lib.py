@@ -16,7 +16,7 @@ _lock = threading.Lock()
 _lib = None
 
 c_void_p = ctypes.c_void_p
-ABI_VERSION = 11  # include/gsplat_hip.h GS_ABI_VERSION
+ABI_VERSION = 12  # include/gsplat_hip.h GS_ABI_VERSION
 GS_FLAG_ACCUMULATE = 1  # include/gsplat_hip.h
 GS_FLAG_ACTIVATE = 2  # include/gsplat_hip.h: raw opacity / scale / rotation parameters
 c_int32, c_int64, c_float, c_size_t = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_size_t
@@ -32,7 +32,7 @@ class GsGaussians(ctypes.Structure):
                 ("rotations", c_void_p), ("cov3D_precomp", c_void_p),
                 ("scale_modifier", c_float), ("flags", ctypes.c_uint32),
                 ("grad_mask", c_void_p), ("densify_accum", c_void_p), ("densify_denom", c_void_p),
-                ("max_radius", c_void_p), ("feature_ready", c_void_p)]
+                ("max_radius", c_void_p), ("feature_ready", c_void_p), ("walk_order", c_void_p)]
 
 
 class GsCamera(ctypes.Structure):
@@ -127,6 +127,9 @@ PROTOTYPES = {
     "gs_check_plan_header": (ctypes.c_int, [c_void_p, c_int64]),
     "gs_check_ranges": (ctypes.c_int, [c_void_p, c_int64, c_int64, c_int64]),
     "gs_check_point_list": (ctypes.c_int, [c_void_p, c_int64, c_int64]),
+    "gs_check_walk_order": (ctypes.c_int, [c_void_p, c_int64]),
+    "gs_spatial_order_scratch_bytes": (c_size_t, [c_int64]),
+    "gs_spatial_order": (ctypes.c_int, [c_int64, c_void_p, c_void_p, c_void_p, c_void_p]),
     "gs_test_wave_reduce": (ctypes.c_int, [ctypes.c_int, c_void_p, c_void_p, c_void_p]),
     "gs_timing_enable": (ctypes.c_int, [ctypes.c_int]),
     # include/gs_knn.h

@@ -238,8 +238,9 @@ SortCover sort_cover(const SortPlan& sp, int64_t tiles) {
   return cv;
 }
 
-TileArgs tile_args(int P, int W, int H, void* geom, void* image) {
+TileArgs tile_args(int P, int W, int H, void* geom, void* image, const int32_t* walk = nullptr) {
   TileArgs t{};
+  t.walk = walk;
   const GeomLayout gl(P);
   const ImgLayout il(W, H);
   t.P = P; t.W = W; t.H = H;
@@ -394,7 +395,16 @@ static int plan_enqueue(const gs_gaussians* g, const gs_camera* cams, int C, int
   const int W = cams[0].image_width, H = cams[0].image_height;
   if (int e = make_batch(cams, C, P, W, H, cb)) return e;
   const GeomLayout gl(P);
-  const TileArgs ta = tile_args(P, W, H, geom, image);
+  if (debug && g->walk_order && P > 0) {
+    // debug mode: the walk order must be a permutation of the ids (a
+    // repeated or missing id would bin a Gaussian twice or not at all)
+    std::vector<int32_t> w(P);
+    const hipError_t e = hipMemcpyAsync(w.data(), g->walk_order, 4 * (size_t)P, hipMemcpyDeviceToHost, s);
+    if (e != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+      return fail((int)e, "walk_order: cannot read it back");
+    if (int r = gs_check_walk_order(w.data(), P)) return r;
+  }
+  const TileArgs ta = tile_args(P, W, H, geom, image, g->walk_order);
   PreprocessArgs a{};
   a.P = P; a.D = g->D; a.M = g->M; a.W = W; a.H = H;
   a.grid_x = ta.grid_x; a.grid_y = ta.grid_y;
@@ -544,7 +554,7 @@ static int render_impl(const gs_gaussians* g, const gs_camera* cams, int C, int 
   const GeomLayout gl(P);
   const ImgLayout il(W, H);
   const float* rec = at<float>(geom, gl.rec);
-  TileArgs ta = tile_args(P, W, H, geom, image);
+  TileArgs ta = tile_args(P, W, H, geom, image, g->walk_order);
   ta.binning = total > 0 ? binning : nullptr;
   {
     // the dispatch order (longest list first) from the ranges: the stage the
@@ -924,6 +934,18 @@ int gs_sort_pairs(int64_t n, uint64_t* keys, uint32_t* vals, int end_bit, void* 
     (void)hipMemcpyAsync(vals, v1, 4 * n, hipMemcpyDeviceToDevice, s);
   }
   return check("sort", 0, s);
+}
+
+// ---- the binning passes' spatial walk order (gs_gaussians.walk_order) ----
+
+size_t gs_spatial_order_scratch_bytes(int64_t P) { return SpatialLayout(P < 0 ? 0 : P).total; }
+
+int gs_spatial_order(int64_t P, const float* means3D, int32_t* order, void* scratch, gs_stream_t stream) {
+  if (P < 0 || P > 0x7FFFFFFF) return fail(-1, "spatial order: P = %lld out of range", (long long)P);
+  if (P > 0 && (!means3D || !order || !scratch)) return fail(-1, "spatial order: null pointer");
+  launch_spatial_order(P, means3D, order, scratch, (hipStream_t)stream);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : fail((int)e, "spatial order: %s", hipGetErrorString(e));
 }
 
 // ---- exact k-nearest neighbours (include/gs_knn.h) ----

@@ -10,6 +10,7 @@
 #include <stdio.h>
 
 #include <string>
+#include <vector>
 
 #include "../../include/gsplat_hip.h"
 #include "gs_meta.h"
@@ -79,6 +80,21 @@ int gs_check_point_list(const uint32_t* ids, int64_t L, int64_t P) {
     if ((int64_t)ids[i] >= P)
       return gs_set_error(-3, "point list: entry %lld holds Gaussian id %u >= P = %lld", (long long)i, ids[i],
                           (long long)P);
+  return 0;
+}
+
+int gs_check_walk_order(const int32_t* order, int64_t P) {
+  if (!order && P > 0) return gs_set_error(-1, "walk order: null");
+  std::vector<unsigned char> seen((size_t)(P > 0 ? P : 0), 0);
+  for (int64_t i = 0; i < P; ++i) {
+    const int64_t v = order[i];
+    if (v < 0 || v >= P)
+      return gs_set_error(-3, "walk order: entry %lld holds id %lld outside [0, %lld)", (long long)i, (long long)v,
+                          (long long)P);
+    if (seen[(size_t)v]++)
+      return gs_set_error(-3, "walk order: id %lld appears twice (entry %lld): not a permutation", (long long)v,
+                          (long long)i);
+  }
   return 0;
 }
 

@@ -161,6 +161,7 @@ struct TileArgs {
   uint64_t* keys2;       // L (sort twin for long tiles)
   uint32_t* plist;       // L
   void* binning;         // binning buffer base (batch: camera c at CamBatch::bin_off[c]), or null
+  const int32_t* walk;   // P: the binning passes' walk order (a permutation of the ids), or null (id order)
 };
 // TileArgs of camera c of a batch (pointers of camera 0 -> camera c).
 __host__ __device__ inline TileArgs cam_tile_args(const TileArgs& a0, const CamBatch& cb, int c) {
@@ -268,6 +269,13 @@ struct KnnLayout {
   explicit KnnLayout(int64_t N);
 };
 bool launch_knn(int64_t N, int K, const float* pts, double* out_d, int64_t* out_i, void* ws, hipStream_t s);
+// Spatial walk order of the binning passes (gs_spatial_order): the ids in 3-D
+// Morton order of the points (the kNN's bounding box, codes and radix sort).
+struct SpatialLayout {
+  size_t bbox, keys, vals, sort, total;
+  explicit SpatialLayout(int64_t N);
+};
+void launch_spatial_order(int64_t N, const float* pts, int32_t* order, void* ws, hipStream_t s);
 
 // Neighbour losses (gs_neighbor.hip, include/gs_neighbor.h).
 struct NeighborArgs {

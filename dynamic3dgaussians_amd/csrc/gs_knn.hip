@@ -270,4 +270,43 @@ bool launch_knn(int64_t N, int K, const float* pts, double* out_d, int64_t* out_
   return true;
 }
 
+SpatialLayout::SpatialLayout(int64_t N) {
+  size_t o = 0;
+  bbox = o; o = align_up(o + 32, 256);
+  keys = o; o = align_up(o + 8 * (size_t)N, 256);
+  vals = o; o = align_up(o + 4 * (size_t)N, 256);
+  sort = o; o = align_up(o + SortLayout(N).total, 256);
+  total = o;
+}
+
+// The binning passes' walk order: the point ids sorted by the 30-bit Morton
+// code of their position in the bounding box (the kNN's first three steps).
+// Any permutation gives the same binning (every tile list is sorted by its
+// unique (depth bits, id) keys); a spatially coherent one gives each binning
+// workgroup's slice of the walk a compact footprint on every camera's screen,
+// so its per-tile runs are long and its key stores coalesce.
+void launch_spatial_order(int64_t N, const float* pts, int32_t* order, void* ws, hipStream_t s) {
+  if (N <= 0) return;
+  const SpatialLayout L(N);
+  char* w = static_cast<char*>(ws);
+  uint32_t* bb = reinterpret_cast<uint32_t*>(w + L.bbox);
+  uint64_t* keys = reinterpret_cast<uint64_t*>(w + L.keys);
+  uint32_t* vals = reinterpret_cast<uint32_t*>(w + L.vals);
+  (void)hipMemsetAsync(bb, 0xFF, 12, s);
+  (void)hipMemsetAsync(bb + 3, 0, 12, s);
+  const unsigned nb = blocks_for(N, 256) < 256 ? blocks_for(N, 256) : 256;
+  hipLaunchKernelGGL(knn_bbox_kernel, dim3(nb), dim3(256), 0, s, N, pts, bb);
+  hipLaunchKernelGGL(knn_morton_kernel, dim3(blocks_for(N, 256)), dim3(256), 0, s, N, pts, bb, keys, vals);
+  if (N > 1) {
+    const SortLayout sl(N);
+    char* sc = w + L.sort;
+    uint64_t* k1 = reinterpret_cast<uint64_t*>(sc + sl.keys1);
+    uint32_t* v1 = reinterpret_cast<uint32_t*>(sc + sl.vals1);
+    if (launch_radix_sort(N, keys, vals, k1, v1, reinterpret_cast<uint32_t*>(sc + sl.hist),
+                          reinterpret_cast<uint32_t*>(sc + sl.rowtot), 30, s))
+      vals = v1;
+  }
+  (void)hipMemcpyAsync(order, vals, 4 * (size_t)N, hipMemcpyDeviceToDevice, s);
+}
+
 }  // namespace gs

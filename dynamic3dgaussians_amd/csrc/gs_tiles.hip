@@ -45,6 +45,13 @@
 
 namespace gs {
 
+// The Gaussian at walk position w of the binning passes: the caller's walk
+// order (gs_gaussians.walk_order, a permutation) or the ids themselves.  The
+// plan and bucket passes walk the same order, so their per-block counts
+// match; the tile lists do not depend on it (the sort orders every list by
+// its unique (depth bits, id) keys).
+__device__ inline int walk_id(const TileArgs& a, int w) { return a.walk ? a.walk[w] : w; }
+
 // Instances of one rect handled by one lane; larger rects are spread over the
 // wave (a full-screen Gaussian must not serialize its wave for 2,500 tiles).
 constexpr int LANE_TILES = 16;
@@ -67,8 +74,9 @@ __global__ __launch_bounds__(TB_THREADS) void tile_hist_kernel(TileArgs a0, CamB
   const int g0 = b * per, g1 = min(a.P, g0 + per);
   // the first slice's rects are requested before the cursor set-up, so their
   // latency overlaps it (the set-up ends in a barrier the compiler does not
-  // hoist loads across)
-  uint4 rnext = g0 + tid < g1 ? a.rect[g0 + tid] : make_uint4(0u, 0u, 0u, 0u);
+  // hoist loads across); walk position -> Gaussian id through the walk order
+  int inext = g0 + tid < g1 ? walk_id(a, g0 + tid) : 0;
+  uint4 rnext = g0 + tid < g1 ? a.rect[inext] : make_uint4(0u, 0u, 0u, 0u);
   for (int i = tid; i < nt; i += TB_THREADS)
     s_bin[i] = WRITE ? a.ranges[t0 + i].x + a.thist[(size_t)b * a.num_tiles + t0 + i] : 0u;
   __syncthreads();
@@ -79,13 +87,17 @@ __global__ __launch_bounds__(TB_THREADS) void tile_hist_kernel(TileArgs a0, CamB
     int x0 = 0, y0 = 0, w = 0, n = 0;
     uint64_t key = 0;
     const uint4 r = rnext;  // {x0 | y0 << 16, x1 | y1 << 16, depth bits, tiles_touched}
-    if (base + TB_THREADS < g1 && g + TB_THREADS < g1) rnext = a.rect[g + TB_THREADS];
+    const int gi = inext;   // the Gaussian at walk position g
+    if (base + TB_THREADS < g1 && g + TB_THREADS < g1) {
+      inext = walk_id(a, g + TB_THREADS);
+      rnext = a.rect[inext];
+    }
     if (g < g1) {
       x0 = (int)(r.x & 0xFFFFu);
       y0 = (int)(r.x >> 16);
       w = (int)(r.y & 0xFFFFu) - x0;
       n = w * ((int)(r.y >> 16) - y0);
-      if (WRITE && n > 0) key = ((uint64_t)r.z << 32) | (uint32_t)g;
+      if (WRITE && n > 0) key = ((uint64_t)r.z << 32) | (uint32_t)gi;
       if (!WRITE) rect_n += r.w;
     }
     auto emit = [&](int x, int y, uint64_t k) {
@@ -151,7 +163,8 @@ __global__ __launch_bounds__(TB_THREADS) void tile_bucket_kernel(TileArgs a0, Ca
   const int per = (a.P + TB_BLOCKS - 1) / TB_BLOCKS;
   const int g0 = b * per, g1 = min(a.P, g0 + per);
   const int T = a.num_tiles;
-  uint4 rnext = g0 + tid < g1 ? a.rect[g0 + tid] : make_uint4(0u, 0u, 0u, 0u);
+  int inext = g0 + tid < g1 ? walk_id(a, g0 + tid) : 0;
+  uint4 rnext = g0 + tid < g1 ? a.rect[inext] : make_uint4(0u, 0u, 0u, 0u);
   // this block's run length in every tile: the column scan left each block's
   // offset inside the tile in thist (the next block's offset, or the tile
   // total, ends the run)
@@ -214,13 +227,17 @@ __global__ __launch_bounds__(TB_THREADS) void tile_bucket_kernel(TileArgs a0, Ca
     int x0 = 0, y0 = 0, w = 0, n = 0;
     uint64_t key = 0;
     const uint4 r = rnext;  // {x0 | y0 << 16, x1 | y1 << 16, depth bits, tiles_touched}
-    if (base + TB_THREADS < g1 && g + TB_THREADS < g1) rnext = a.rect[g + TB_THREADS];
+    const int gi = inext;
+    if (base + TB_THREADS < g1 && g + TB_THREADS < g1) {
+      inext = walk_id(a, g + TB_THREADS);
+      rnext = a.rect[inext];
+    }
     if (g < g1) {
       x0 = (int)(r.x & 0xFFFFu);
       y0 = (int)(r.x >> 16);
       w = (int)(r.y & 0xFFFFu) - x0;
       n = w * ((int)(r.y >> 16) - y0);
-      if (n > 0) key = ((uint64_t)r.z << 32) | (uint32_t)g;
+      if (n > 0) key = ((uint64_t)r.z << 32) | (uint32_t)gi;
     }
     auto emit = [&](int x, int y, uint64_t k) {
       const uint32_t u = (uint32_t)(y * gx + x - t0);

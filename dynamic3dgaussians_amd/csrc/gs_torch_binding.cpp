@@ -96,6 +96,7 @@ struct Inputs {
     g.grad_mask = nullptr;
     g.densify_accum = g.densify_denom = g.max_radius = nullptr;
     g.feature_ready = nullptr;
+    g.walk_order = nullptr;
   }
 };
 
@@ -293,10 +294,17 @@ forward_batch(const Tensor& bg, const Tensor& means3D, const OptT& colors, const
               const std::vector<double>& tx, const std::vector<double>& ty, int64_t H, int64_t W, const OptT& sh,
               int64_t degree, const Tensor& campos, bool prefiltered, bool debug, int64_t compat, bool activate,
               const std::vector<std::vector<int64_t>>& windows, int64_t feature_ready,
-              const std::vector<int64_t>& capacity, const std::vector<int64_t>& hint, int64_t stream) {
+              const std::vector<int64_t>& capacity, const std::vector<int64_t>& hint, const OptT& walk_order,
+              int64_t stream) {
   Inputs in(means3D, colors, sem, opacity, scales, rotations, scale_modifier, cov3D, sh, degree);
   if (activate) in.g.flags |= GS_FLAG_ACTIVATE;
   in.g.feature_ready = reinterpret_cast<gs_event_t>(feature_ready);
+  if (present(walk_order)) {
+    const Tensor& w = *walk_order;
+    if (w.scalar_type() != at::kInt || w.device() != in.dev || !w.is_contiguous() || w.numel() != in.P)
+      throw std::runtime_error("walk_order must be a contiguous int32 device tensor of P ids");
+    in.g.walk_order = w.data_ptr<int32_t>();
+  }
   Cameras k(in.dev, bg, views, projs, campos, cx, cy, tx, ty, W, H, windows);
   const int32_t C = (int32_t)k.cams.size();
   const auto f32 = at::TensorOptions().dtype(at::kFloat).device(in.dev);

@@ -433,7 +433,7 @@ class _RasterizeGaussiansBatch(torch.autograd.Function):
     @staticmethod
     def forward(ctx, means3D, means2D, sh, colors_precomp, semantic_feature, opacities, scales, rotations,
                 cov3Ds_precomp, cams, label, densify_out, raw_params=False, feature_ready=None, plan_state=None,
-                grad_into=None):
+                grad_into=None, walk_order=None):
         if not isinstance(cams, _BatchCameras):
             cams = _BatchCameras(cams)
         rs0 = cams.rs0
@@ -450,7 +450,8 @@ class _RasterizeGaussiansBatch(torch.autograd.Function):
             rs0.bg, means3D, colors_precomp, semantic_feature, opacities, scales, rotations, rs0.scale_modifier,
             cov3Ds_precomp, views, projs, [p[0] for p in pp], [p[1] for p in pp], tx, ty, rs0.image_height,
             rs0.image_width, sh, rs0.sh_degree, cpos, rs0.prefiltered, rs0.debug, compat=compat,
-            activate=raw_params, windows=cams.windows, feature_ready=feature_ready, plan_state=plan_state)
+            activate=raw_params, windows=cams.windows, feature_ready=feature_ready, plan_state=plan_state,
+            walk_order=walk_order)
         num_rendered, color, feature_map, depth, alpha, radii, geom, binning, img, num_instances = out
         ctx.rs0 = rs0
         ctx.cams = (views, projs, cpos, pp, tx, ty, cams.windows)
@@ -510,7 +511,7 @@ class _RasterizeGaussiansBatch(torch.autograd.Function):
             grad_cov3Ds_precomp = grad_cov3Ds_precomp * lab
         grads = (grad_means3D, grad_means2D, grad_sh, grad_colors_precomp, grad_semantic_feature,
                  grad_opacities, grad_scales, grad_rotations, grad_cov3Ds_precomp, None, None, None, None, None,
-                 None, None)
+                 None, None, None)
         # gradients written into caller-owned destinations: autograd gets None
         taken = [False] * len(grads)
         for k in (ctx.grad_into or {}):
@@ -542,7 +543,7 @@ def _grad_destinations(grad_into, semantic_feature):
 
 def rasterize_gaussians_batch(means3D, means2D, sh, colors_precomp, semantic_feature, opacities, scales,
                               rotations, cov3Ds_precomp, settings_list, label=None, densify_out=None,
-                              raw_params=False, feature_ready=None, plan_state=None, grad_into=None):
+                              raw_params=False, feature_ready=None, plan_state=None, grad_into=None, walk_order=None):
     """rasterize_gaussians over a list of camera settings; outputs [C, ...]
     (color, radii, feature_map, depth, alpha).  `densify_out`: optional
     (accum, denom, max_radius) fp32 [P] tensors the backward fills with the
@@ -559,11 +560,12 @@ def rasterize_gaussians_batch(means3D, means2D, sh, colors_precomp, semantic_fea
     gradient bucket's views, distributed.ShardedAdam.grad_views) and hands
     autograd None for them, so no gradient tensor is allocated, accumulated
     or copied into a bucket; gradients reaching those tensors through other
-    autograd paths are not added."""
+    autograd paths are not added.  `walk_order`: the binning passes' walk
+    order (_C.spatial_order; outputs do not depend on it)."""
     cams = settings_list if isinstance(settings_list, _BatchCameras) else _BatchCameras(list(settings_list))
     return _RasterizeGaussiansBatch.apply(means3D, means2D, sh, colors_precomp, semantic_feature, opacities,
                                           scales, rotations, cov3Ds_precomp, cams, label, densify_out,
-                                          bool(raw_params), feature_ready, plan_state, grad_into)
+                                          bool(raw_params), feature_ready, plan_state, grad_into, walk_order)
 
 
 class GaussianRasterizerBatch(nn.Module):
@@ -590,12 +592,22 @@ class GaussianRasterizerBatch(nn.Module):
     _C.BinningPlan kept in `self.plan`) and the headers are read after every
     stage is enqueued; a call whose lists outgrow it is rendered again with
     the exact lengths.  Outputs and gradients are bit-identical to
-    sync_free=False (the reference's two-phase order)."""
+    sync_free=False (the reference's two-phase order).
 
-    def __init__(self, settings_list, track_densify=False, raw_params=False, sync_free=True):
+    `spatial_order=True`: the binning passes walk the Gaussians in 3-D
+    Morton order of their means (gs_gaussians.walk_order, ABI 12), so each
+    binning workgroup's slice is compact on every camera's screen and its
+    per-tile key runs are long; outputs are bit-identical either way (every
+    tile list is sorted by its unique (depth bits, id) keys)."""
+
+    def __init__(self, settings_list, track_densify=False, raw_params=False, sync_free=True, spatial_order=False,
+                 order_refresh=256):
         super().__init__()
         self.settings_list = list(settings_list)
         self.plan = _C.BinningPlan() if sync_free else None
+        self.spatial_order = bool(spatial_order)
+        self.order_refresh = max(1, int(order_refresh))
+        self._walk, self._walk_calls = None, 0
         self._cams = _BatchCameras(self.settings_list)
         if track_densify and self._cams.windows is not None:
             raise ValueError("densification statistics need whole-image cameras: a tile window counts a "
@@ -603,6 +615,19 @@ class GaussianRasterizerBatch(nn.Module):
         self.track_densify = track_densify
         self.raw_params = bool(raw_params)
         self.densify_stats = None
+
+    def _walk_order(self, means3D):
+        """spatial_order=True: the binning passes walk the Gaussians in 3-D
+        Morton order of their means (_C.spatial_order), recomputed when P
+        changes and every `order_refresh` calls (the means move while they
+        train; a stale order is only less coherent, never wrong)."""
+        if not self.spatial_order or not means3D.is_cuda or means3D.size(0) == 0:
+            return None
+        if (self._walk is None or self._walk.numel() != means3D.size(0)
+                or self._walk_calls % self.order_refresh == 0):
+            self._walk = _C.spatial_order(means3D)
+        self._walk_calls += 1
+        return self._walk
 
     def forward(self, means3D, means2D, opacities=None, shs=None, semantic_feature=None, colors_precomp=None,
                 scales=None, rotations=None, cov3D_precomp=None, label=_UNSET, feature_ready=None,
@@ -632,7 +657,8 @@ class GaussianRasterizerBatch(nn.Module):
             self.densify_stats = {"means2D_gradient_accum": dens[0], "denom": dens[1], "max_2D_radius": dens[2]}
         color, radii, feature_map, depth, alpha = rasterize_gaussians_batch(
             means3D, means2D, shs, colors_precomp, semantic_feature, opacities, scales, rotations,
-            cov3D_precomp, self._cams, lab, dens, self.raw_params, feature_ready, self.plan, grad_into)
+            cov3D_precomp, self._cams, lab, dens, self.raw_params, feature_ready, self.plan, grad_into,
+            self._walk_order(means3D))
         has_sem = semantic_feature is not None
         if has_label and has_sem:      # G3
             return color, radii, feature_map, depth, alpha

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 11
+#define GS_ABI_VERSION 12
 
 /* compat modes: numerics of the as-shipped reference vs corrected ones */
 #define GS_COMPAT_REFERENCE 0
@@ -110,6 +110,15 @@ typedef struct gs_gaussians {
    * all-reduce) orders that update before the blend without ordering the
    * projection and binning behind it. */
   gs_event_t feature_ready;
+  /* Optional (ABI 12; no reference analogue): the order in which the
+   * binning passes (tile histogram and bucket) walk the Gaussians -- P ids,
+   * a permutation of [0, P) -- or NULL (id order).  Outputs do not depend
+   * on it: every tile list is sorted by its unique (depth bits, id) keys.  A
+   * spatially coherent order (gs_spatial_order) gives each binning
+   * workgroup's slice a compact footprint on every camera's screen, so its
+   * per-tile runs are long and its key stores coalesce.  Debug mode checks
+   * that it is a permutation (gs_check_walk_order). */
+  const int32_t *walk_order;
 } gs_gaussians;
 
 /* Camera / raster settings (GaussianRasterizationSettings,
@@ -344,10 +353,20 @@ int gs_debug_export(int64_t P, int32_t W, int32_t H, const void *geom_buffer,
  *   every range in [0, L], begin <= end, the non-empty ranges contiguous in
  *   tile order and covering exactly [0, L); longest range <= max_len (< 0: no
  *   bound).
- * gs_check_point_list: every id of a camera's L list entries < P. */
+ * gs_check_point_list: every id of a camera's L list entries < P.
+ * gs_check_walk_order: the P entries are a permutation of [0, P). */
 int gs_check_plan_header(const uint32_t *hdr, int64_t tiles);
 int gs_check_ranges(const uint32_t *ranges, int64_t tiles, int64_t L, int64_t max_len);
 int gs_check_point_list(const uint32_t *ids, int64_t L, int64_t P);
+int gs_check_walk_order(const int32_t *order, int64_t P);
+
+/* A spatially coherent walk order for gs_gaussians.walk_order (ABI 12): the
+ * ids 0..P-1 sorted by the 30-bit Morton code of means3D (P x 3) in its
+ * bounding box (the stable radix sort below; ties keep id order).  scratch
+ * is gs_spatial_order_scratch_bytes(P) bytes.  Any later change of the means
+ * only makes the order less coherent, never wrong. */
+size_t gs_spatial_order_scratch_bytes(int64_t P);
+int gs_spatial_order(int64_t P, const float *means3D, int32_t *order, void *scratch, gs_stream_t stream);
 
 /* Stable LSD radix sort of (u64 key, u32 value) pairs on bits [0, end_bit)
  * -- the standalone form of the binning sort (cub::DeviceRadixSort::SortPairs

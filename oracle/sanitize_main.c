@@ -9,7 +9,7 @@
  *     SH degrees 0 / 3 or precomputed colours, F = 0 / 32, both compat modes,
  *     an off-centre principal point, Gaussians on and beyond the image edges;
  *   - the library's host validators (dynamic3dgaussians_amd/csrc/gs_host.cpp:
- *     gs_check_plan_header / gs_check_ranges / gs_check_point_list,
+ *     gs_check_plan_header / gs_check_ranges / gs_check_point_list / gs_check_walk_order,
  *     gs_last_error) on the oracle's own plan, lists and ranges and on
  *     corrupted copies of them (each must be refused with a message).
  * Prints "sanitize ok" and exits 0 when clean; tests/test_sanitize.py runs it.
@@ -173,6 +173,19 @@ static void run_case(int P, int W, int H, int D, int F, int compat, int precomp,
   bad[4] = (uint32_t)T + 1u;
   EXPECT(gs_check_plan_header(bad, T) < 0, "sort prefix > tiles accepted");
   EXPECT(gs_check_plan_header(NULL, T) < 0, "null header accepted");
+  {
+    /* a walk order: a permutation passes, a repeated id and an id out of range do not */
+    int32_t *wo = xcalloc((size_t)P, 4);
+    for (int i = 0; i < P; ++i) wo[i] = P - 1 - i;
+    EXPECT(gs_check_walk_order(wo, P) == 0, "valid walk order refused: %s", gs_last_error());
+    if (P > 1) {
+      wo[0] = wo[1];
+      EXPECT(gs_check_walk_order(wo, P) < 0, "repeated id in the walk order accepted");
+      wo[0] = P;
+      EXPECT(gs_check_walk_order(wo, P) < 0, "out-of-range id in the walk order accepted");
+    }
+    free(wo);
+  }
   if (L > 2) {
     uint32_t *r2 = xcalloc((size_t)2 * T, 4);
     memcpy(r2, ranges, sizeof(uint32_t) * 2 * T);
