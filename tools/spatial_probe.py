@@ -71,7 +71,10 @@ def main():
     if a.features:
         up.append(torch.randn(C, a.features, H, W, device=dev, generator=gen))
     label = torch.ones(a.gaussians, device=dev)
-    ras = {name: GaussianRasterizerBatch(sets) for name in scenes}
+    # the library's own form: the index-order scene, the binning passes
+    # walking it in Morton order (GaussianRasterizerBatch(spatial_order=True))
+    scenes["walk_order"] = scenes["index_order"]
+    ras = {name: GaussianRasterizerBatch(sets, spatial_order=(name == "walk_order")) for name in scenes}
 
     def step(name):
         s = scenes[name]
@@ -93,7 +96,8 @@ def main():
         for _ in range(2):
             imgs[name] = step(name).detach()
     torch.cuda.synchronize()
-    same = bool(torch.equal(imgs["index_order"], imgs["morton_order"]))
+    same = {"morton_order": bool(torch.equal(imgs["index_order"], imgs["morton_order"])),
+            "walk_order": bool(torch.equal(imgs["index_order"], imgs["walk_order"]))}
     for _ in range(a.reps):
         for name in scenes:
             torch.cuda.synchronize()
