@@ -72,37 +72,24 @@ __global__ __launch_bounds__(TB_THREADS) void tile_hist_kernel(TileArgs a0, CamB
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   const int per = (a.P + TB_BLOCKS - 1) / TB_BLOCKS;
   const int g0 = b * per, g1 = min(a.P, g0 + per);
-  const int iters = g1 > g0 ? (g1 - g0 + TB_THREADS - 1) / TB_THREADS : 0;
-  // Walk position of thread tid at iteration it: consecutive threads take
-  // consecutive positions, except in the count pass over a coherent walk
-  // order (a.walk), where each thread takes its own contiguous run of the
-  // slice: the block's counts do not depend on the visiting order, and
-  // spatially adjacent Gaussians on adjacent lanes would emit the same tiles
-  // at once -- same-address LDS atomics, serialised.  (The direct bucket pass
-  // keeps the adjacent lanes: their equal tiles are consecutive slots, i.e.
-  // coalesced stores.)
-  const bool spread = !WRITE && a.walk != nullptr;
-  auto pos = [&](int it) { return spread ? g0 + tid * iters + it : g0 + it * TB_THREADS + tid; };
   // the first slice's rects are requested before the cursor set-up, so their
   // latency overlaps it (the set-up ends in a barrier the compiler does not
   // hoist loads across); walk position -> Gaussian id through the walk order
-  const int p0 = pos(0);
-  int inext = iters > 0 && p0 < g1 ? walk_id(a, p0) : 0;
-  uint4 rnext = iters > 0 && p0 < g1 ? a.rect[inext] : make_uint4(0u, 0u, 0u, 0u);
+  int inext = g0 + tid < g1 ? walk_id(a, g0 + tid) : 0;
+  uint4 rnext = g0 + tid < g1 ? a.rect[inext] : make_uint4(0u, 0u, 0u, 0u);
   for (int i = tid; i < nt; i += TB_THREADS)
     s_bin[i] = WRITE ? a.ranges[t0 + i].x + a.thist[(size_t)b * a.num_tiles + t0 + i] : 0u;
   __syncthreads();
   const int gx = a.grid_x;
   uint32_t rect_n = 0;
-  for (int it = 0; it < iters; ++it) {
-    const int g = pos(it);
+  for (int base = g0; base < g1; base += TB_THREADS) {
+    const int g = base + tid;
     int x0 = 0, y0 = 0, w = 0, n = 0;
     uint64_t key = 0;
     const uint4 r = rnext;  // {x0 | y0 << 16, x1 | y1 << 16, depth bits, tiles_touched}
     const int gi = inext;   // the Gaussian at walk position g
-    const int gn = pos(it + 1);
-    if (it + 1 < iters && gn < g1) {
-      inext = walk_id(a, gn);
+    if (base + TB_THREADS < g1 && g + TB_THREADS < g1) {
+      inext = walk_id(a, g + TB_THREADS);
       rnext = a.rect[inext];
     }
     if (g < g1) {
@@ -176,6 +163,8 @@ __global__ __launch_bounds__(TB_THREADS) void tile_bucket_kernel(TileArgs a0, Ca
   const int per = (a.P + TB_BLOCKS - 1) / TB_BLOCKS;
   const int g0 = b * per, g1 = min(a.P, g0 + per);
   const int T = a.num_tiles;
+  int inext = g0 + tid < g1 ? walk_id(a, g0 + tid) : 0;
+  uint4 rnext = g0 + tid < g1 ? a.rect[inext] : make_uint4(0u, 0u, 0u, 0u);
   // this block's run length in every tile: the column scan left each block's
   // offset inside the tile in thist (the next block's offset, or the tile
   // total, ends the run)
@@ -217,15 +206,6 @@ __global__ __launch_bounds__(TB_THREADS) void tile_bucket_kernel(TileArgs a0, Ca
   __syncthreads();
   const uint32_t total = s_total;
   const bool staged = total <= (uint32_t)cap;
-  // walk positions as in tile_hist_kernel: with a coherent walk order and the
-  // keys staged (their order inside a run is free), each thread takes its own
-  // contiguous run of the slice, so adjacent lanes do not hit one cursor
-  const int iters = g1 > g0 ? (g1 - g0 + TB_THREADS - 1) / TB_THREADS : 0;
-  const bool spread = staged && a.walk != nullptr;
-  auto pos = [&](int it) { return spread ? g0 + tid * iters + it : g0 + it * TB_THREADS + tid; };
-  const int p0 = pos(0);
-  int inext = iters > 0 && p0 < g1 ? walk_id(a, p0) : 0;
-  uint4 rnext = iters > 0 && p0 < g1 ? a.rect[inext] : make_uint4(0u, 0u, 0u, 0u);
   {
     uint32_t lo = s_wsum[wv] + incl - run;  // local start of this thread's first tile
 #pragma unroll
@@ -242,15 +222,14 @@ __global__ __launch_bounds__(TB_THREADS) void tile_bucket_kernel(TileArgs a0, Ca
   }
   __syncthreads();
   const int gx = a.grid_x;
-  for (int it = 0; it < iters; ++it) {
-    const int g = pos(it);
+  for (int base = g0; base < g1; base += TB_THREADS) {
+    const int g = base + tid;
     int x0 = 0, y0 = 0, w = 0, n = 0;
     uint64_t key = 0;
     const uint4 r = rnext;  // {x0 | y0 << 16, x1 | y1 << 16, depth bits, tiles_touched}
     const int gi = inext;
-    const int gn = pos(it + 1);
-    if (it + 1 < iters && gn < g1) {
-      inext = walk_id(a, gn);
+    if (base + TB_THREADS < g1 && g + TB_THREADS < g1) {
+      inext = walk_id(a, g + TB_THREADS);
       rnext = a.rect[inext];
     }
     if (g < g1) {
