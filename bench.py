@@ -771,8 +771,9 @@ def main():
     # two-phase plan -> host read -> render order of the reference)
     sync_free = os.environ.get("GS_BENCH_SYNC_FREE", "1") != "0"
     # the binning passes' walk in 3-D Morton order of the means
-    # (GaussianRasterizerBatch(spatial_order=True), gs_gaussians.walk_order)
-    walk = os.environ.get("GS_BENCH_WALK", "0") == "1"
+    # (GaussianRasterizerBatch(spatial_order=...), gs_gaussians.walk_order):
+    # "auto" (default) once the lists outgrow the bucket pass's LDS staging
+    walk = {"1": True, "0": False}.get(os.environ.get("GS_BENCH_WALK", "auto"), "auto")
     means2D_placeholder = torch.zeros_like(params["means3D"])
 
     # one upstream gradient per camera, materialized once (the batch's
@@ -1228,6 +1229,9 @@ def main():
                    "streams": n_streams if args.mode == "percam" else len(batch_parts),
                    "forward": ("sync-free (gs_forward_batch: binning sized from the previous step)" if sync_free
                                and args.mode == "batch" else "two-phase (plan, host read, render)"),
+                   "binning_walk": ("3-D Morton order of the means (gs_gaussians.walk_order)"
+                                    if args.mode == "batch" and any(p_[0]._walk is not None for p_ in batch_parts)
+                                    else "id order"),
                    "activations": ("in-kernel (raw parameters, GS_FLAG_ACTIVATE)" if raw and args.mode == "batch"
                                    else "torch ops (params2rendervar)"),
                    "grad_sum": ("in-kernel (camera sum in preprocess_bwd)" if args.mode == "batch" else

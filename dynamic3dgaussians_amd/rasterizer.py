@@ -594,18 +594,23 @@ class GaussianRasterizerBatch(nn.Module):
     the exact lengths.  Outputs and gradients are bit-identical to
     sync_free=False (the reference's two-phase order).
 
-    `spatial_order=True`: the binning passes walk the Gaussians in 3-D
+    `spatial_order`: True -- the binning passes walk the Gaussians in 3-D
     Morton order of their means (gs_gaussians.walk_order, ABI 12), so each
     binning workgroup's slice is compact on every camera's screen and its
-    per-tile key runs are long; outputs are bit-identical either way (every
-    tile list is sorted by its unique (depth bits, id) keys)."""
+    per-tile key runs are long; "auto" (the default) -- only when the
+    previous call's lists outgrow the bucket pass's LDS staging (large
+    scenes, e.g. BASELINE configs[4]); False -- id order.  Outputs are
+    bit-identical either way (every tile list is sorted by its unique
+    (depth bits, id) keys)."""
 
-    def __init__(self, settings_list, track_densify=False, raw_params=False, sync_free=True, spatial_order=False,
+    def __init__(self, settings_list, track_densify=False, raw_params=False, sync_free=True, spatial_order="auto",
                  order_refresh=256):
         super().__init__()
         self.settings_list = list(settings_list)
         self.plan = _C.BinningPlan() if sync_free else None
-        self.spatial_order = bool(spatial_order)
+        if spatial_order not in (True, False, "auto"):
+            raise ValueError("spatial_order: True, False or 'auto'")
+        self.spatial_order = spatial_order
         self.order_refresh = max(1, int(order_refresh))
         self._walk, self._walk_calls = None, 0
         self._cams = _BatchCameras(self.settings_list)
@@ -616,12 +621,33 @@ class GaussianRasterizerBatch(nn.Module):
         self.raw_params = bool(raw_params)
         self.densify_stats = None
 
+    # The bucket pass's blocks (gs_common.h TB_BLOCKS per camera) stage their
+    # keys in LDS when they fit: cap = (159 KiB - 8 B x tiles) / 10 B per key
+    # (launch_tile_bucket, gs_tiles.hip); past it every key is stored where its
+    # slot lands, and only then does a spatially coherent walk pay (adjacent
+    # lanes' keys in consecutive slots: configs[4] bucket 0.75 -> 0.48 ms; at
+    # the bench scene, staged, the walk's rect gathers cost more than it saves).
+    _TB_BLOCKS, _TB_BINS = 128, 16384
+
+    def _walk_wanted(self):
+        if self.spatial_order != "auto":
+            return bool(self.spatial_order)
+        ni = self.plan.num_instances if self.plan is not None else None
+        if not ni:
+            return False
+        rs = self._cams.rs0
+        tiles = ((rs.image_width + 15) // 16) * ((rs.image_height + 15) // 16)
+        cap = (159 * 1024 - 8 * min(self._TB_BINS, tiles)) // 10
+        return max(ni) / self._TB_BLOCKS > cap
+
     def _walk_order(self, means3D):
-        """spatial_order=True: the binning passes walk the Gaussians in 3-D
-        Morton order of their means (_C.spatial_order), recomputed when P
-        changes and every `order_refresh` calls (the means move while they
-        train; a stale order is only less coherent, never wrong)."""
-        if not self.spatial_order or not means3D.is_cuda or means3D.size(0) == 0:
+        """The binning passes' walk: with spatial_order=True (or "auto" once
+        the previous call's lists outgrow the bucket pass's LDS staging) the
+        Gaussians in 3-D Morton order of their means (_C.spatial_order),
+        recomputed when P changes and every `order_refresh` calls (the means
+        move while they train; a stale order is only less coherent, never
+        wrong); else None (id order)."""
+        if not self._walk_wanted() or not means3D.is_cuda or means3D.size(0) == 0:
             return None
         if (self._walk is None or self._walk.numel() != means3D.size(0)
                 or self._walk_calls % self.order_refresh == 0):

@@ -75,6 +75,7 @@ def main():
     # walking it in Morton order (GaussianRasterizerBatch(spatial_order=True))
     scenes["walk_order"] = scenes["index_order"]
     ras = {name: GaussianRasterizerBatch(sets, spatial_order=(name == "walk_order")) for name in scenes}
+    assert ras["index_order"].spatial_order is False
 
     def step(name):
         s = scenes[name]
