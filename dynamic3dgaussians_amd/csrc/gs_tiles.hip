@@ -40,6 +40,8 @@
 //     the header).
 // Integer work, HBM- and latency-bound; 5 launches instead of the
 // reference's scan + 6-pass 64-bit radix sort + ranges.
+#include <cstdlib>
+
 #include "gs_common.h"
 #include "gs_kernels.h"
 
@@ -135,6 +137,75 @@ __global__ __launch_bounds__(TB_THREADS) void tile_hist_kernel(TileArgs a0, CamB
       for (int w2 = 0; w2 < TB_THREADS / 64; ++w2) sum += s_rect[w2];
       a.bsum[b] = sum;
     }
+  }
+}
+
+// The count pass as a 2-D difference array: each Gaussian adds +1 / -1 at
+// the four corners of its tile rect (4 LDS atomics instead of one per
+// instance -- 5.5 per Gaussian at the bench scene, 14.6 at configs[4] --
+// and, in a coherent walk order, far fewer same-address collisions), then a
+// row scan and a column scan over the (gy + 1) x (gx + 1) grid turn the
+// corners into every tile's count (integer sums: exactly tile_hist_kernel's
+// counts).  One launch over the whole tile grid (grids up to TB_BINS tiles;
+// launch_tile_plan falls back to the per-instance count beyond).
+__global__ __launch_bounds__(TB_THREADS) void tile_count_kernel(TileArgs a0, CamBatch cb) {
+  const TileArgs a = cam_tile_args(a0, cb, blockIdx.y);
+  extern __shared__ uint32_t s_d[];  // (gy + 1) x (gx + 1) difference counters
+  __shared__ uint32_t s_rect[TB_THREADS / 64];
+  constexpr int NW = TB_THREADS / 64;
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int gx = a.grid_x, gy = a.grid_y, DX = gx + 1, ND = DX * (gy + 1);
+  const int per = (a.P + TB_BLOCKS - 1) / TB_BLOCKS;
+  const int g0 = b * per, g1 = min(a.P, g0 + per);
+  for (int i = tid; i < ND; i += TB_THREADS) s_d[i] = 0u;
+  __syncthreads();
+  uint32_t rect_n = 0;
+  for (int g = g0 + tid; g < g1; g += TB_THREADS) {
+    const uint4 r = a.rect[walk_id(a, g)];  // {x0 | y0 << 16, x1 | y1 << 16, depth bits, tiles_touched}
+    rect_n += r.w;
+    const int x0 = min((int)(r.x & 0xFFFFu), gx), y0 = min((int)(r.x >> 16), gy);
+    const int x1 = min((int)(r.y & 0xFFFFu), gx), y1 = min((int)(r.y >> 16), gy);
+    if (x1 > x0 && y1 > y0) {
+      atomicAdd(&s_d[y0 * DX + x0], 1u);
+      atomicAdd(&s_d[y0 * DX + x1], 0xFFFFFFFFu);
+      atomicAdd(&s_d[y1 * DX + x0], 0xFFFFFFFFu);
+      atomicAdd(&s_d[y1 * DX + x1], 1u);
+    }
+  }
+  __syncthreads();
+  // inclusive scan of `n` entries at stride `step` from `base`, one wave
+  auto wave_scan = [&](int base, int n, int step) {
+    uint32_t carry = 0;
+    for (int c0 = 0; c0 < n; c0 += 64) {
+      const int i = c0 + lane;
+      uint32_t v = i < n ? s_d[base + i * step] : 0u;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+      }
+      if (i < n) s_d[base + i * step] = v + carry;
+      carry += __shfl(v, 63, 64);
+    }
+  };
+  for (int y = wv; y <= gy; y += NW) wave_scan(y * DX, DX, 1);  // along x
+  __syncthreads();
+  for (int x = wv; x <= gx; x += NW) wave_scan(x, gy + 1, DX);  // along y
+  __syncthreads();
+  const int T = a.num_tiles;
+  for (int t = tid; t < T; t += TB_THREADS) {
+    const int y = t / gx, x = t - y * gx;
+    a.thist[(size_t)b * T + t] = s_d[y * DX + x];
+  }
+  // the reference's num_rendered: bounding-rect instances of this block
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) rect_n += __shfl_xor(rect_n, o, 64);
+  if (lane == 0) s_rect[wv] = rect_n;
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t sum = 0;
+    for (int w2 = 0; w2 < NW; ++w2) sum += s_rect[w2];
+    a.bsum[b] = sum;
   }
 }
 
@@ -802,13 +873,38 @@ __global__ __launch_bounds__(NT) void tile_sort_kernel(TileArgs a0, CamBatch cb,
 
 // ------------------------------------------------------------------ launchers
 
+// Which count pass: the difference array (tile_count_kernel) with a
+// spatially coherent walk order (its adjacent lanes' instances are
+// same-tile LDS atomics: configs[4] plan 0.29 -> 0.13 ms), the per-instance
+// one (tile_hist_kernel<false>) in id order, where its ~5 atomics per
+// Gaussian spread over the grid cost less than the array's scans (bench plan
+// 0.120 vs 0.126-0.132 ms).  Env GS_COUNT_MODE=diff / instance forces one
+// (A/B).
+static int count_mode() {  // 0 auto, 1 diff, 2 per instance
+  static const int v = [] {
+    const char* e = getenv("GS_COUNT_MODE");
+    if (!e) return 0;
+    if (e[0] == 'd') return 1;
+    if (e[0] == 'i') return 2;
+    return 0;
+  }();
+  return v;
+}
+
 void launch_tile_plan(const TileArgs& a, const CamBatch& cb, int prefiltered, uint32_t* hdr_host, hipEvent_t done,
                       hipStream_t s) {
   const int T = a.num_tiles;
-  for (int t0 = 0; t0 < T; t0 += TB_BINS) {
-    const int nt = min(TB_BINS, T - t0);
-    hipLaunchKernelGGL(tile_hist_kernel<false>, dim3(TB_BLOCKS, cb.C), dim3(TB_THREADS), sizeof(uint32_t) * nt, s,
-                       a, cb, t0, nt);
+  const size_t nd = (size_t)(a.grid_x + 1) * (a.grid_y + 1);
+  const int mode = count_mode();
+  const bool diff = mode == 1 || (mode == 0 && a.walk != nullptr);
+  if (T <= TB_BINS && nd <= (size_t)TB_BINS + 1024 && diff) {
+    hipLaunchKernelGGL(tile_count_kernel, dim3(TB_BLOCKS, cb.C), dim3(TB_THREADS), sizeof(uint32_t) * nd, s, a, cb);
+  } else {
+    for (int t0 = 0; t0 < T; t0 += TB_BINS) {
+      const int nt = min(TB_BINS, T - t0);
+      hipLaunchKernelGGL(tile_hist_kernel<false>, dim3(TB_BLOCKS, cb.C), dim3(TB_THREADS), sizeof(uint32_t) * nt, s,
+                         a, cb, t0, nt);
+    }
   }
   hipLaunchKernelGGL(tile_rowscan_kernel, dim3((T + RS_T - 1) / RS_T, cb.C), dim3(RS_THREADS), 0, s, a.thist, a.ttotal, T,
                      cb);
