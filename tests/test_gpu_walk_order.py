@@ -104,3 +104,18 @@ def test_debug_mode_refuses_a_walk_that_is_not_a_permutation(P=4000, W=96, H=80,
         rasterize_gaussians_batch(src["means3D"], torch.zeros(P, 3, device=DEV), None, src["colors_precomp"],
                                   None, src["opacities"], src["scales"], src["rotations"], None, sets,
                                   walk_order=walk)
+
+
+@pytest.mark.parametrize("P", [1, 2, 63, 64, 65, 257])
+def test_spatial_order_small_and_degenerate(P):
+    means = make_means(P)
+    if P > 2:
+        means[: P // 2] = means[0]  # repeated points: equal codes keep id order (stable sort)
+    order = _C.spatial_order(means)
+    torch.cuda.synchronize()
+    assert torch.equal(torch.sort(order.long()).values, torch.arange(P, device=DEV))
+    codes = _morton(means)[order.long()]
+    assert bool((codes[1:] >= codes[:-1]).all())
+    eq = codes[1:] == codes[:-1]
+    assert bool((order[1:][eq] > order[:-1][eq]).all())  # ties in id order
+    assert _C.spatial_order(torch.zeros(0, 3, device=DEV)).numel() == 0
