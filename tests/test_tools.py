@@ -61,3 +61,20 @@ def test_split_predict_takes_the_slowest_rank_and_the_exposed_exchange(tmp_path)
     assert abs(pr["geometry_allreduce_ms"] - round(geo, 3)) < 1e-9
     assert abs(pr["step_ms"] - round(1.375 + pr["exposed_ms"], 4)) < 1e-4
     assert abs(pr["speedup_vs_1gpu"] - round(9.0 / pr["step_ms"], 3)) < 1e-3
+
+
+def test_compare_params_bounds_by_the_learning_rate(tmp_path):
+    # a chaotic run far above the floor but far below one update, and an
+    # exchange error of one update per element
+    rng = np.random.default_rng(1)
+    base = rng.standard_normal(100_000).astype(np.float32)
+
+    def run_like(shift=0.0):
+        return {"means3D": base + rng.standard_normal(base.size).astype(np.float32) * 1e-11 + shift}
+    paths = {}
+    for name, shift in (("a", 0.0), ("b", 0.0), ("c", 0.0), ("chaos", 5e-8), ("error", 1.6e-4)):
+        paths[name] = str(tmp_path / f"{name}.npz")
+        np.savez(paths[name], **run_like(shift))
+    refs = [paths["a"], paths["b"], paths["c"]]
+    assert _run(["tools/compare_params.py", paths["chaos"]] + refs).returncode == 0
+    assert _run(["tools/compare_params.py", paths["error"]] + refs).returncode == 1

@@ -10,9 +10,17 @@ the order noise through discrete events -- one Gaussian's alpha crossing
 elements by 1e-4..1e-2 in any pair of runs, so the plain mean of one pair
 is heavy-tailed; a systematic error (a wrong exchange, a lost slice) moves
 most elements and shows in the trimmed mean.  The floor is the largest
-trimmed mean over the reference pairs.  OK iff, for every tensor, the
-tested run's trimmed mean <= max(3 x floor, 1e-9).  The plain mean and max
-are printed beside it.
+trimmed mean over the reference pairs.
+
+A run now and then (one gloo rehearsal run in six, the plain reference path
+included) lands far above the floor on every tensor at once: the atomic
+order's noise amplified through one early discrete event across the whole
+scene over the run's training steps.  An exchange error is different in
+kind -- a lost, doubled or stale contribution moves every element by the
+order of its learning rate per step -- so the bound is also scaled by it:
+OK iff, for every tensor, the tested run's trimmed mean <=
+max(3 x floor, 1e-3 x lr, 1e-9) (bench.py's learning rates, train.py:119-135).
+The plain mean and max are printed beside it.
 
     python tools/compare_params.py test.npz ref.npz ref_repeat.npz [ref_repeat2.npz ...]
 """
@@ -22,6 +30,9 @@ import sys
 import numpy as np
 
 TRIM = 0.001
+# bench.py's Adam learning rates per tensor (train.py:119-135)
+LR = {"means3D": 1.6e-4, "rgb_colors": 2.5e-3, "unnorm_rotations": 1e-3, "logit_opacities": 0.05,
+      "log_scales": 1e-3, "semantic_feature": 1e-3}
 
 
 def trimmed_mean(d):
@@ -44,7 +55,9 @@ def main():
         out[k] = {"trimmed_mean": trimmed_mean(d), "floor_trimmed_mean": fl, "mean": float(d.mean()),
                   "max": float(d.max()), "floor_mean": max(float(f.mean()) for f in floors),
                   "floor_max": max(float(f.max()) for f in floors)}
-        ok &= out[k]["trimmed_mean"] <= max(3 * fl, 1e-9)
+        bound = max(3 * fl, 1e-3 * LR.get(k, 0.0), 1e-9)
+        out[k]["bound"] = bound
+        ok &= out[k]["trimmed_mean"] <= bound
     print(json.dumps(out, indent=1))
     print("OK" if ok else "MISMATCH")
     sys.exit(0 if ok else 1)
