@@ -197,7 +197,6 @@ def test_per_camera_drop_in_sync_free_matches_two_phase(compat, P=20000, W=208, 
         return [t.detach().clone() for t in (im, radii, feat, depth, alpha)], {k: v.grad for k, v in leaves.items()}
     assert _C.native_loaded(), "the native binding did not load"
     keep = _C._PERCAM_SYNC_FREE
-    _C._percam_plans = None  # no plan inherited from an earlier test's (freed) view-matrix address
     try:
         _C._PERCAM_SYNC_FREE = False
         refs = [run(s) for s in sets]
