@@ -185,11 +185,6 @@ def rasterize_gaussians(background, means3D, colors, semantic_feature, opacity, 
     cm = _compat_code(compat)
     nat = _native_mod()
     if nat is not None and means3D.is_cuda and means3D.dim() == 2 and means3D.size(0) > 0:
-        if not debug and _PERCAM_SYNC_FREE and isinstance(viewmatrix, torch.Tensor):
-            return _forward_one_sync_free(nat, background, means3D, colors, semantic_feature, opacity, scales,
-                                          rotations, scale_modifier, cov3D_precomp, viewmatrix, projmatrix, c_x,
-                                          c_y, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
-                                          prefiltered, cm)
         try:
             return nat.forward(background, means3D, _opt(colors), _opt(semantic_feature), _opt(opacity),
                                _opt(scales), _opt(rotations), float(scale_modifier), _opt(cov3D_precomp),
@@ -242,49 +237,6 @@ def rasterize_gaussians(background, means3D, colors, semantic_feature, opacity, 
     del keep
     feature_map = out_feature[:inp.F_user] if inp.F_user != inp.F else out_feature
     return (num_rendered, out_color, feature_map, out_depth, out_alpha, radii, geom, binning, img)
-
-
-# The per-camera drop-in forward without the host round trip (the camera
-# batch's gs_forward_batch with one camera): its binning capacity and sort
-# hint come from the previous call of the same camera -- the same view-matrix
-# tensor, Gaussian count and image size, as a training loop that reuses its
-# cameras' settings has it (train.py's dataset entries) -- kept in a bounded
-# table.  The first call of a camera, and one whose lists outgrow the
-# capacity, renders again with the exact lengths; outputs are bit-identical
-# to the two-phase call either way, and the binning buffer's layout is the
-# two-phase one (one camera's tile lists start it: the backward reads them
-# without the length).  GS_PERCAM_SYNC_FREE=0: the two-phase order.
-_PERCAM_SYNC_FREE = os.environ.get("GS_PERCAM_SYNC_FREE", "1") != "0"
-_PERCAM_PLANS_MAX = 4096
-_percam_plans: "OrderedDict" = None
-
-
-def _forward_one_sync_free(nat, background, means3D, colors, semantic_feature, opacity, scales, rotations,
-                           scale_modifier, cov3D_precomp, viewmatrix, projmatrix, c_x, c_y, tan_fovx, tan_fovy,
-                           image_height, image_width, sh, degree, campos, prefiltered, cm):
-    global _percam_plans
-    from collections import OrderedDict
-    if _percam_plans is None:
-        _percam_plans = OrderedDict()
-    H, W = int(image_height), int(image_width)
-    key = (viewmatrix.data_ptr(), means3D.device.index, int(means3D.size(0)), H, W)
-    plan = _percam_plans.pop(key, None) or BinningPlan()
-    _percam_plans[key] = plan
-    while len(_percam_plans) > _PERCAM_PLANS_MAX:
-        _percam_plans.popitem(last=False)
-    cap = plan.next_capacity(1)
-    try:
-        out = nat.forward_batch(background, means3D, _opt(colors), _opt(semantic_feature), _opt(opacity),
-                                _opt(scales), _opt(rotations), float(scale_modifier), _opt(cov3D_precomp),
-                                viewmatrix.reshape(1, 16), projmatrix.reshape(1, 16), [float(c_x)], [float(c_y)],
-                                [float(tan_fovx)], [float(tan_fovy)], H, W, _opt(sh), int(degree),
-                                campos.reshape(1, 3), bool(prefiltered), False, cm, False, [], 0, cap,
-                                plan.hint, None, torch.cuda.current_stream(means3D.device).cuda_stream)
-    except RuntimeError as ex:
-        raise _lib.GsplatError(str(ex)) from None
-    NR, color, fmap, depth, alpha, radii, geom, binning, img, NI, layout, hint, fitted = out
-    plan.update(list(NI), list(hint), fitted, first=not any(cap))
-    return (int(NR[0]), color[0], fmap[0], depth[0], alpha[0], radii[0], geom, binning, img)
 
 
 _BUFFER_ORDER = ("dmeans2D", "dcolors", "dsem", "dopacity", "dmeans3D", "dcov3D", "dsh", "dscales", "drot")

@@ -173,40 +173,3 @@ def test_sync_free_empty_and_debug_paths(W=96, H=80, C=3):
     for x, y in zip(a, b):
         assert torch.equal(x, y)
     assert r_dbg.plan.calls == 0  # debug runs the two-phase path
-
-
-@pytest.mark.parametrize("compat", ["reference", "fixed"])
-def test_per_camera_drop_in_sync_free_matches_two_phase(compat, P=20000, W=208, H=160, F=32):
-    # the drop-in GaussianRasterizer: the per-camera forward through
-    # gs_forward_batch with one camera (capacity and hint from the previous
-    # call of the same camera) against the two-phase order
-    from dynamic3dgaussians_amd.rasterizer import GaussianRasterizer
-    src = _scene(P, F, seed=12)
-    sets = _settings(camera_rig(2, W, H), W, H, compat)
-    gen = torch.Generator(device=DEV).manual_seed(4)
-    ups = [torch.randn(3, H, W, device=DEV, generator=gen), torch.randn(1, H, W, device=DEV, generator=gen),
-           torch.randn(F, H, W, device=DEV, generator=gen)]
-    lab = torch.ones(P, device=DEV)
-
-    def run(s):
-        leaves = {k: v.clone().requires_grad_(True) for k, v in src.items()}
-        im, radii, feat, depth, alpha = GaussianRasterizer(s)(means2D=torch.zeros(P, 3, device=DEV), label=lab,
-                                                              **leaves)
-        torch.autograd.backward([im, depth, feat], ups)
-        torch.cuda.synchronize()
-        return [t.detach().clone() for t in (im, radii, feat, depth, alpha)], {k: v.grad for k, v in leaves.items()}
-    assert _C.native_loaded(), "the native binding did not load"
-    keep = _C._PERCAM_SYNC_FREE
-    try:
-        _C._PERCAM_SYNC_FREE = False
-        refs = [run(s) for s in sets]
-        _C._PERCAM_SYNC_FREE = True
-        for _ in range(3):  # first call of each camera retries, then its own hint fits
-            for s, (ref_o, ref_g) in zip(sets, refs):
-                o, g = run(s)
-                _same(o, ref_o, g, ref_g)
-    finally:
-        _C._PERCAM_SYNC_FREE = keep
-    for s in sets:
-        plan = _C._percam_plans[(s.viewmatrix.data_ptr(), 0, P, H, W)]
-        assert plan.calls == 3 and plan.retries == 0, (plan.calls, plan.retries)
