@@ -166,3 +166,18 @@ def _grad_into_case(sets, P, W, H, C, F):
     bad["means3D"] = torch.empty(P - 1, 3, device=DEV)
     with pytest.raises((_lib.GsplatError, RuntimeError)):
         _step(GaussianRasterizerBatch(sets, raw_params=True), pb, label, ups, grad_into=bad)
+
+
+def test_grad_into_refuses_a_feature_width_the_kernels_pad():
+    # F = 35 runs the F = 36 kernels (padded rows): a P x 35 destination is
+    # not the backward's P x 36 output and must be refused, not mis-strided
+    P, W, H, C, F = 3000, 96, 80, 2, 35
+    sets = _cams(C, W, H)
+    gen = torch.Generator(device=DEV).manual_seed(3)
+    ups = [torch.randn(C, 3, H, W, device=DEV, generator=gen), torch.randn(C, 1, H, W, device=DEV, generator=gen),
+           torch.randn(C, F, H, W, device=DEV, generator=gen)]
+    params = _raw_params(P, F, seed=5)
+    opt = ShardedAdam(params, LRS, rank=0, world=1)
+    dest = {_ARG[k]: v for k, v in opt.grad_views(0).items()}
+    with pytest.raises((_lib.GsplatError, RuntimeError)):
+        _step(GaussianRasterizerBatch(sets, raw_params=True), params, torch.ones(P, device=DEV), ups, grad_into=dest)
