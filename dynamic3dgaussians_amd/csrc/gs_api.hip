@@ -156,17 +156,6 @@ thread_local PlanInfo g_plan;
 // the number of concurrent callers (not by the threads that ever called:
 // thread pools and autograd workers would otherwise each pin one for good).
 // Never freed: a pool destructor could run after the HIP runtime is gone.
-// Env GS_HEADER_COPY=1 (A/B of the header path): a hipMemcpy2DAsync of the
-// device headers in the stream instead of tile_offsets_kernel's stores to
-// mapped host memory.
-bool header_copy() {
-  static const bool v = [] {
-    const char* e = getenv("GS_HEADER_COPY");
-    return e && e[0] == '1';
-  }();
-  return v;
-}
-
 struct HeaderSlot {
   uint32_t* host = nullptr;  // host pointer
   uint32_t* dev = nullptr;   // the same memory as the kernels address it
@@ -194,7 +183,7 @@ struct HeaderLease {
     // device-scope release: tile_offsets_kernel's stores to this host memory
     // are system-scope atomics behind a system fence of their own
     if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess ||
-        hipEventCreateWithFlags(&s.ev, header_copy() ? hipEventDisableTiming : hipEventReleaseToDevice) !=
+        hipEventCreateWithFlags(&s.ev, hipEventReleaseToDevice) !=
             hipSuccess) {
       (void)hipHostFree(h);
       s = HeaderSlot{};
@@ -463,19 +452,13 @@ static int plan_read(const uint32_t (*host)[M_WORDS], int C, int prefiltered, in
   return 0;
 }
 
-// The headers' way to the host after plan_enqueue: in the default path
-// tile_offsets_kernel stored them and its dispatch records hl's event; with
-// GS_HEADER_COPY=1 a copy command and an event marker follow it here.
-// record_only: do not wait yet.
-static int publish_wait(HeaderLease& hl, const TileArgs& ta, const CamBatch& cb, int C, hipStream_t s,
-                        bool record_only) {
+// The headers' way to the host after plan_enqueue: tile_offsets_kernel
+// stored them to the mapped buffer and its dispatch records hl's event (an
+// in-stream copy of the device headers instead measured slower, DESIGN.md
+// section 4).  record_only: do not wait yet.
+static int publish_wait(HeaderLease& hl, int C, hipStream_t s, bool record_only) {
   hipError_t he = hipSuccess;
-  if (header_copy()) {
-    he = hipMemcpy2DAsync(hl.s.host, sizeof(uint32_t) * M_WORDS, ta.meta, (size_t)cb.img_stride,
-                          sizeof(uint32_t) * M_WORDS, C, hipMemcpyDeviceToHost, s);
-    if (he == hipSuccess) he = hipEventRecord(hl.s.ev, s);
-  }
-  if (he == hipSuccess && !record_only) he = hipEventSynchronize(hl.s.ev);
+  if (!record_only) he = hipEventSynchronize(hl.s.ev);
   if (he == hipSuccess && !record_only) {
     // every header's last word is 0 once written (header_sentinel): an event
     // that did not cover the header's kernel must not hand back stale words
@@ -514,15 +497,13 @@ static int plan_impl(const gs_gaussians* g, const gs_camera* cams, int C, int pr
   if (!hl.ok()) return fail((int)hipErrorOutOfMemory, "cannot allocate the page-locked plan header buffer");
   header_sentinel(hl, C);
   CamBatch cb;
-  if (int e = plan_enqueue(g, cams, C, prefiltered, debug, geom, image, radii, header_copy() ? nullptr : hl.s.dev,
-                           header_copy() ? nullptr : hl.s.ev,
-                           cb, s))
+  if (int e = plan_enqueue(g, cams, C, prefiltered, debug, geom, image, radii, hl.s.dev, hl.s.ev, cb, s))
     return e;
   // The one host read of the forward (CR/rasterizer_impl.cu:287), one for
   // the whole batch: the list instance counts size the binning buffer; the
   // reference's counts and the rest of the headers ride along.
   const TileArgs ta = tile_args(P, cams[0].image_width, cams[0].image_height, geom, image);
-  if (int e = publish_wait(hl, ta, cb, C, s, false)) return e;
+  if (int e = publish_wait(hl, C, s, false)) return e;
   PlanInfo info;
   if (int e = plan_read(reinterpret_cast<const uint32_t(*)[M_WORDS]>(hl.s.host), C, prefiltered, debug,
                         (int64_t)ta.grid_x * ta.grid_y, num_rendered, num_instances, info))
@@ -818,14 +799,12 @@ int gs_forward_batch(const gs_gaussians* g, const gs_camera* cams, int32_t C, in
   header_sentinel(hl, C);
   hipStream_t s = (hipStream_t)stream;
   CamBatch cb;
-  if (int e = plan_enqueue(g, cams, C, prefiltered, 0, geom, image, radii, header_copy() ? nullptr : hl.s.dev,
-                           header_copy() ? nullptr : hl.s.ev, cb,
-                           s))
+  if (int e = plan_enqueue(g, cams, C, prefiltered, 0, geom, image, radii, hl.s.dev, hl.s.ev, cb, s))
     return e;
   const int W = cams[0].image_width, H = cams[0].image_height;
   const TileArgs ta = tile_args(P, W, H, geom, image);
   const int64_t tiles = (int64_t)ta.grid_x * ta.grid_y;
-  if (int e = publish_wait(hl, ta, cb, C, s, true)) return e;
+  if (int e = publish_wait(hl, C, s, true)) return e;
   // Every stage behind the plan is enqueued before the host looks at the
   // headers: the GPU goes on from the plan to the bucket, sort and blend
   // launches while the host waits for the event.
