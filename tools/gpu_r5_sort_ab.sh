@@ -1,7 +1,9 @@
 # The tile sort's short length class in 128-thread workgroups against 256
 # (GS_SORT_SHORT_NT): the binning parity tests under the new default, then
 # interleaved bench lines at the bench scene and at rank 5's configs[3]
-# proxy (3 whole cameras + 2 window pieces).
+# proxy (3 whole cameras + 2 window pieces).  The switch and the 128-thread
+# variant were removed after this run: kept as the
+# record of the measurement.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/${TAG:-r05sort}; mkdir -p $O
