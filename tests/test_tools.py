@@ -1,6 +1,7 @@
 """The analysis tools the round's GPU evidence rests on, on synthetic inputs:
-tools/compare_params.py (the exchange rehearsals' verdict) and
-tools/split_predict.py (the configs[3] prediction)."""
+tools/compare_params.py (the exchange rehearsals' verdict),
+tools/split_predict.py (the configs[3] prediction) and tools/pmc_split.py (the
+binning kernels' PMC summary)."""
 import json
 import os
 import subprocess
@@ -78,3 +79,23 @@ def test_compare_params_bounds_by_the_learning_rate(tmp_path):
     refs = [paths["a"], paths["b"], paths["c"]]
     assert _run(["tools/compare_params.py", paths["chaos"]] + refs).returncode == 0
     assert _run(["tools/compare_params.py", paths["error"]] + refs).returncode == 1
+
+
+def test_pmc_split_averages_per_launch_and_splits_wave_cycles(tmp_path):
+    # two passes over the same two launches of one kernel, as rocprofv3 writes them
+    hdr = "Dispatch_Id,Kernel_Name,Counter_Name,Counter_Value\n"
+    k = "void gs::tile_sort_kernel<256, 10, 8>(gs::TileArgs, gs::CamBatch, int, int, int, int)"
+    p1 = tmp_path / "p1.csv"
+    p1.write_text(hdr + "".join(f'{d},"{k}",{c},{v}\n' for d in (1, 2) for c, v in
+                                (("SQ_WAVE_CYCLES", 1000), ("SQ_ACTIVE_INST_ANY", 200), ("SQ_WAIT_ANY", 700),
+                                 ("SQ_WAIT_INST_ANY", 100), ("SQ_WAVES", 10), ("SQ_INSTS_VALU", 2770),
+                                 ("SQ_INSTS_LDS", 660))))
+    p2 = tmp_path / "p2.csv"
+    p2.write_text(hdr + "".join(f'{d},"{k}",{c},{v}\n' for d in (1, 2) for c, v in
+                                (("SQ_LDS_BANK_CONFLICT", 35), ("SQ_LDS_IDX_ACTIVE", 100))))
+    r = _run(["tools/pmc_split.py", str(p1), str(p2)])
+    assert r.returncode == 0, r.stderr
+    row = json.loads(r.stdout)["gs::tile_sort_kernel<256, 10, 8>"]
+    assert row["SQ_WAVE_CYCLES"] == 1000 and row["launches"] == 2
+    assert (row["frac_issuing"], row["frac_parked"], row["frac_issue_stalled"]) == (0.2, 0.7, 0.1)
+    assert row["valu_per_wave"] == 277.0 and row["lds_per_wave"] == 66.0 and row["lds_conflict_frac"] == 0.35
