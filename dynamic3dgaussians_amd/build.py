@@ -31,15 +31,16 @@ if VARIANT:
     BUILD_DIR = os.path.join(OUT_DIR, f"obj_{VARIANT}")
 # Build variants: "stats" (work counters of the blend and sort kernels,
 # tools/render_stats.py), "stamps" / "stamps_fine" (per-wave lifetime stamps,
-# tools/batch_steps.py --stamps) and two timing-only removals whose results
-# are wrong by construction (the backward's atomic-free ceiling, DESIGN.md
-# section 4).  A variant name not listed here is a frozen snapshot (e.g. a
+# tools/batch_steps.py --stamps) and timing-only removals whose results are
+# wrong by construction (the backward's atomic-free ceiling, the tile sort's
+# floor).  A variant name not listed here is a frozen snapshot (e.g. a
 # copy of a previous product library for A/B timing) and is never rebuilt.
 VARIANT_FLAGS = {"": [], "stats": ["-DGS_STATS"], "stamps": ["-DGS_STAMPS"],
                  "stamps_fine": ["-DGS_STAMPS", "-DGS_STAMPS_FINE"],
                  "exp_nofeat": ["-DGS_EXP_NO_FEAT_ATOMIC"],
                  "exp_noatomic": ["-DGS_EXP_NO_FEAT_ATOMIC", "-DGS_EXP_NO_ACC_ATOMIC"],
                  "exp_fwd_nofeatst": ["-DGS_EXP_FWD_NO_FEAT_STORE"],  # traffic of the feature planes
+                 "exp_sort_copy": ["-DGS_EXP_SORT_COPY_ONLY"],  # the tile sort's floor: copy, no sort
                  "ctl": []}  # the product's flags under a variant's (ctypes) binding: the A/B control
 ARCH = os.environ.get("GSPLAT_OFFLOAD_ARCH", "gfx950")
 

@@ -27,9 +27,10 @@
 //  3. sort   (tile_sort_kernel): one workgroup per tile sorts its segment by
 //     the full key.  Common case, an MSD bucket sort: the top bits of the
 //     tile's depth-bit span pick one of 1,024 buckets (LDS atomics give each
-//     key its slot), one scan, one scatter, then every thread insertion-sorts
-//     its contiguous run of buckets by the full key -- the keys go from
-//     global memory to registers to one LDS buffer (the scatter target).  Tiles whose
+//     key its slot), one scan, one scatter, then every key takes its place
+//     in its bucket by counting the bucket's smaller keys -- the keys go from
+//     global memory to registers to one LDS buffer (the scatter target, then
+//     the sorted ids over its start).  Tiles whose
 //     keys crowd into few buckets fall back to an LSD radix sort in global
 //     memory (wave-owned quarters, ballot-matched stable scatter, skipped
 //     constant-digit passes, equal depths ordered by id).  Keys are unique,
@@ -584,7 +585,7 @@ __device__ inline uint64_t match_digit8(uint32_t d, uint64_t valid) {
 constexpr int BS_BITS = 10, BS_BITS_LONG = 11;
 constexpr int BS_KPT = 8;       // keys per thread held in registers (up to 8 NT keys per tile)
 constexpr int BS_KPT_LONG = 16;  // for launches whose tiles exceed 8 NT keys (20 / 24 measured slower)
-constexpr int BS_RUN_MAX = 48;  // longest per-thread run handed to the insertion sort (64: no change)
+constexpr int BS_BUCKET_MAX = 48;  // fullest bucket the bucket sort ranks (each key reads its bucket's keys)
 
 template <int NT, int BINS>
 struct RadixSmem {
@@ -707,17 +708,21 @@ __device__ __attribute__((always_inline)) KP tile_radix_sort(KP A, KP B, int n, 
 }
 
 // MSD bucket sort of a tile held in LDS -- the common case.  The top
-// BS_BITS bits of the tile's depth-bit span pick one of BS_BINS buckets
+// BITS bits of the tile's depth-bit span pick one of BS_BINS buckets
 // (counted with returning LDS atomics: the returned count is the key's slot
 // in its bucket), one scan turns the counts into bucket starts, one scatter
-// places the keys, and every thread insertion-sorts its contiguous run of
-// BS_BINS / NT buckets by the full (depth bits << 32 | id) key -- the
-// reference's (depth, index) order, with no stability requirement anywhere
-// since the final comparison is on the unique full key.  Three barriers
-// after the counts instead of the radix sort's five per 8-bit pass.  Returns
-// false, with A untouched, when the tile has more keys than the registers
-// hold or some thread's run is longer than BS_RUN_MAX (depths crowded into
-// few buckets): the caller then runs the radix sort.
+// places the keys in their buckets, and every key then finds its place in
+// its bucket by counting the bucket's keys below it (the full (depth bits
+// << 32 | id) key: unique, so the places are distinct and the order is the
+// reference's (depth, index) order).  The ids are left in LDS in sorted
+// order, as 32-bit words over the start of the key buffer.  Returns false,
+// with A untouched, when the tile has more keys than the registers hold or
+// some bucket more than BS_BUCKET_MAX keys (depths crowded into few
+// buckets): the caller then runs the radix sort.
+// (Round 5: the ranking replaced a per-thread insertion sort of each
+// thread's run of buckets -- chains of dependent LDS round trips, each wave
+// waiting for its longest run.  Tile sort per step 0.42 -> 0.31 ms at the
+// bench scene, 0.59 -> 0.39 ms at configs[4]; profiles/r05/rank_sort/.)
 
 template <int NT, int BITS, int BS_KPT>
 __device__ __attribute__((always_inline)) bool tile_bucket_sort(const uint64_t* A, uint64_t* B, int n,
@@ -769,12 +774,14 @@ __device__ __attribute__((always_inline)) bool tile_bucket_sort(const uint64_t* 
     rk[j] = i < n ? atomicAdd(&cnt[bk[j]], 1u) : 0u;
   }
   __syncthreads();
-  // thread t owns bins [t BPT, (t + 1) BPT): its run of keys in bucket order
+  // thread t owns bins [t BPT, (t + 1) BPT)
   uint32_t c[BPT], run = 0;
+  bool crowded = false;
 #pragma unroll
   for (int b = 0; b < BPT; ++b) {
     c[b] = owner ? cnt[tid * BPT + b] : 0u;
     run += c[b];
+    crowded = crowded || c[b] > (uint32_t)BS_BUCKET_MAX;
   }
   uint32_t inc = run;
 #pragma unroll
@@ -783,7 +790,7 @@ __device__ __attribute__((always_inline)) bool tile_bucket_sort(const uint64_t* 
     if (lane >= o) inc += y;
   }
   if (lane == 63) wsum[wave] = inc;
-  if (run > BS_RUN_MAX) sm.skip = 1;
+  if (crowded) sm.skip = 1;
   __syncthreads();
   if (sm.skip) return false;  // uniform: a crowded tile goes to the radix sort
   uint32_t base = inc - run;
@@ -802,16 +809,24 @@ __device__ __attribute__((always_inline)) bool tile_bucket_sort(const uint64_t* 
   for (int j = 0; j < BS_KPT; ++j)
     if (tid + j * NT < n) B[cnt[bk[j]] + rk[j]] = k[j];
   __syncthreads();
-  // insertion sort of the thread's run by the full key
-  for (uint32_t a = base + 1; a < base + run; ++a) {
-    const uint64_t v = B[a];
-    uint32_t b = a;
-    while (b > base && B[b - 1] > v) {
-      B[b] = B[b - 1];
-      --b;
+  // each key's place: its bucket's start plus the bucket's keys below it
+  uint32_t dst[BS_KPT];
+#pragma unroll
+  for (int j = 0; j < BS_KPT; ++j) {
+    dst[j] = 0u;
+    if (tid + j * NT < n) {
+      const uint32_t b0 = cnt[bk[j]];
+      const uint32_t b1 = bk[j] + 1 < (uint32_t)BS_BINS ? cnt[bk[j] + 1] : (uint32_t)n;
+      uint32_t r = 0;
+      for (uint32_t i = b0; i < b1; ++i) r += B[i] < k[j] ? 1u : 0u;
+      dst[j] = b0 + r;
     }
-    B[b] = v;
   }
+  __syncthreads();  // every key read: the ids overwrite the buffer's start
+  uint32_t* ids = reinterpret_cast<uint32_t*>(B);
+#pragma unroll
+  for (int j = 0; j < BS_KPT; ++j)
+    if (tid + j * NT < n) ids[dst[j]] = (uint32_t)k[j];
   __syncthreads();
   return true;
 }
@@ -847,24 +862,28 @@ __global__ __launch_bounds__(NT) void tile_sort_kernel(TileArgs a0, CamBatch cb,
     if (threadIdx.x == 0) plist[r.x] = (uint32_t)keys[r.x];
     return;
   }
+#ifdef GS_EXP_SORT_COPY_ONLY  // timing-only variant: the segment copied unsorted (the launch's floor)
+  for (int i = threadIdx.x; i < n; i += NT) plist[r.x + i] = (uint32_t)keys[r.x + i];
+  return;
+#endif
   if (n <= cap) {
     // keys straight from global memory into the bucket sort's registers
     // (no LDS staging copy: sort 0.457-0.462 vs 0.470-0.471 ms per bench step)
-    const uint64_t* out;
     if (tile_bucket_sort<NT, BITS, KPT>(keys + r.x, s_key, n, sm)) {
-      out = s_key;
+      const uint32_t* ids = reinterpret_cast<const uint32_t*>(s_key);  // sorted ids over the keys' start
+      for (int i = threadIdx.x; i < n; i += NT) plist[r.x + i] = ids[i];
     } else {
 #ifdef GS_STATS
       if (threadIdx.x == 0) atomicAdd(&g_sort_stats[1], 1ull);
 #endif
       // the keys in global memory are untouched (the bucket sort gives up
       // before its scatter); the radix passes run there with the twin buffer
-      out = tile_radix_sort<uint64_t*, NT, (1 << BITS)>(keys + r.x, keys2 + r.x, n, sm);
+      const uint64_t* out = tile_radix_sort<uint64_t*, NT, (1 << BITS)>(keys + r.x, keys2 + r.x, n, sm);
+      for (int i = threadIdx.x; i < n; i += NT) plist[r.x + i] = (uint32_t)out[i];
     }
 #ifdef GS_STATS
     if (threadIdx.x == 0) atomicAdd(&g_sort_stats[0], 1ull);
 #endif
-    for (int i = threadIdx.x; i < n; i += NT) plist[r.x + i] = (uint32_t)out[i];
   } else {  // longer than the LDS capacity of this launch: sort in global memory
     const uint64_t* out = tile_radix_sort<uint64_t*, NT, (1 << BITS)>(keys + r.x, keys2 + r.x, n, sm);
     for (int i = threadIdx.x; i < n; i += NT) plist[r.x + i] = (uint32_t)out[i];

@@ -1,0 +1,17 @@
+# The tile sort's bucket phase placing each key by counting its bucket's
+# smaller keys (instead of per-thread insertion sorts): the binning parity
+# tests on the new product library, then interleaved bench lines of the
+# previous library (frozen as variant r05_insert) against the new one under
+# the same ctypes binding (variant ctl), at the bench scene, at configs[4]
+# per rank and at rank 5's configs[3] proxy.
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+O=gpurun_out/${TAG:-r05rank}; mkdir -p $O
+timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_parity.py \
+  tests/test_gpu_walk_order.py tests/test_gpu_sync_free.py tests/test_gpu_batch.py tests/test_gpu_windows.py \
+  tests/test_gpu_sweep.py tests/test_gpu_fullsize.py > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+E="GSPLAT_VARIANT=r05_insert GSPLAT_VARIANT=ctl"
+TAG=${TAG:-r05rank}/bench REPS=3 ENVS="$E" BENCH_ARGS="--steps 20" bash tools/gpu_env_ab.sh || exit 2
+TAG=${TAG:-r05rank}/cfg4 REPS=2 ENVS="$E" BENCH_ARGS="--gaussians 1000000 --width 1920 --height 1080 --cams 4 --features 32 --steps 10 --warmup 3" bash tools/gpu_env_ab.sh || exit 3
+TAG=${TAG:-r05rank}/px5 REPS=2 ENVS="$E" BENCH_ARGS="--cams-total 27 --proxy-world 8 --proxy-rank 5 --steps 100 --warmup 10" bash tools/gpu_env_ab.sh || exit 4
