@@ -842,7 +842,7 @@ extern "C" int gs_sort_stats_read(unsigned long long* out) {
 // One tile per workgroup of NT threads (tiles of length lo < n <= hi; the
 // others exit).  Keys bucket-sorted up to `cap` (the launch's dynamic LDS):
 // loaded from global memory straight into registers and scattered into one
-// LDS buffer of cap keys, where the insertion sorts run (no staging copy and
+// LDS buffer of cap keys, where they are ranked (no staging copy and
 // no second buffer: twice the workgroups per CU of the two-buffer sort); a
 // tile the bucket sort hands back (crowded depths, or more than KPT keys per
 // thread) and one longer than cap are radix-sorted in global memory.
