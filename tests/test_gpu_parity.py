@@ -117,18 +117,31 @@ def test_preprocess_and_binning_bitexact(kw):
     assert 0.0 <= frac < 1.0
 
 
-@pytest.mark.parametrize("mode", ["ties", "crowded", "ties_crowded"])
+@pytest.mark.parametrize("mode", ["ties", "crowded", "ties_crowded", "groups"])
 def test_binning_depth_ties_and_crowded_depths(mode):
-    """The per-tile sort's two paths (gs_tiles.hip): the MSD bucket sort with
-    per-thread insertion sorts, and the radix sort it falls back to when the
-    depths crowd into few buckets.  'ties': groups of Gaussians share a mean
-    (bit-identical depths, so the list order inside a group is the Gaussian
-    index, as the reference's stable sort leaves it); 'crowded': most means
-    on a thin shell at one distance from the camera, a few elsewhere (most of
-    a tile's keys in one or two buckets of its span: the radix path)."""
+    """The per-tile sort's two paths (gs_tiles.hip): the MSD bucket sort
+    (each key placed by counting its bucket's smaller keys), and the radix
+    sort it falls back to when a bucket holds more than 48 keys.  'ties':
+    groups of Gaussians share a mean (bit-identical depths, so the list order
+    inside a group is the Gaussian index, as the reference's stable sort
+    leaves it); 'crowded': most means on a thin shell at one distance from
+    the camera, a few elsewhere (most of a tile's keys in a few buckets of
+    its span -- the radix path when the limit was a thread's run of buckets,
+    the bucket sort since it is one bucket's keys); 'groups': disjoint
+    groups of 2 .. 64 Gaussians on one mean each, around the 48-key bucket
+    limit (47, 48, 49: one bucket of that many keys where only the group
+    reaches), so both sides of the fallback boundary run (stats build:
+    3 radix fallbacks among its tiles, none in the other modes)."""
     inp = H.scene(P=4000, W=96, H=64)
     m = inp["means3D"].clone()
     g = torch.Generator().manual_seed(3)
+    if mode == "groups":
+        perm = torch.randperm(m.shape[0], generator=g)
+        o = 0
+        for k in (2, 3, 8, 16, 47, 48, 49, 64):
+            idx = perm[o:o + k]
+            m[idx] = m[idx[0]].clone()
+            o += k
     if "ties" in mode:
         src = torch.randint(0, m.shape[0], (m.shape[0] // 2,), generator=g)
         dst = torch.randperm(m.shape[0], generator=g)[: m.shape[0] // 2]
