@@ -33,15 +33,18 @@ if VARIANT:
 # tools/render_stats.py), "stamps" / "stamps_fine" (per-wave lifetime stamps,
 # tools/batch_steps.py --stamps) and timing-only removals whose results are
 # wrong by construction (the backward's atomic-free ceiling, the tile sort's
-# floor).  A variant name not listed here is a frozen snapshot (e.g. a
-# copy of a previous product library for A/B timing) and is never rebuilt.
+# floor).  The timing-only removals are not in the
+# product sources: they are text patches (tools/variants.py) applied to a
+# copy of csrc/ for that variant's build.  A variant name not listed here is
+# a frozen snapshot (e.g. a copy of a previous product library for A/B
+# timing) and is never rebuilt.
 VARIANT_FLAGS = {"": [], "stats": ["-DGS_STATS"], "stamps": ["-DGS_STAMPS"],
                  "stamps_fine": ["-DGS_STAMPS", "-DGS_STAMPS_FINE"],
-                 "exp_nofeat": ["-DGS_EXP_NO_FEAT_ATOMIC"],
-                 "exp_noatomic": ["-DGS_EXP_NO_FEAT_ATOMIC", "-DGS_EXP_NO_ACC_ATOMIC"],
-                 "exp_fwd_nofeatst": ["-DGS_EXP_FWD_NO_FEAT_STORE"],  # traffic of the feature planes
-                 "exp_sort_copy": ["-DGS_EXP_SORT_COPY_ONLY"],  # the tile sort's floor: copy, no sort
+                 "exp_nofeat": [], "exp_noatomic": [],  # the backward's atomics (tools/variants.py)
+                 "exp_fwd_nofeatst": [],  # traffic of the feature planes
+                 "exp_sort_copy": [],  # the tile sort's floor: copy, no sort
                  "ctl": []}  # the product's flags under a variant's (ctypes) binding: the A/B control
+PATCHED = ("exp_nofeat", "exp_noatomic", "exp_fwd_nofeatst", "exp_sort_copy")
 ARCH = os.environ.get("GSPLAT_OFFLOAD_ARCH", "gfx950")
 
 # Per-file flags.  The preprocess kernels are compiled without FMA
@@ -78,6 +81,8 @@ def _deps() -> list[str]:
     files = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f != "gs_torch_binding.cpp"]
     files += _headers()
     files.append(os.path.abspath(__file__))
+    if VARIANT in PATCHED:
+        files.append(os.path.join(REPO, "tools", "variants.py"))
     return files
 
 
@@ -90,11 +95,27 @@ def is_stale() -> bool:
     return any(os.path.getmtime(f) > t for f in _deps())
 
 
+def _patched_sources() -> str:
+    """A copy of csrc/ with the variant's text patches (tools/variants.py)."""
+    sys.path.insert(0, REPO)
+    from tools import variants
+    out = os.path.join(OUT_DIR, f"src_{VARIANT}")
+    os.makedirs(out, exist_ok=True)
+    for f in os.listdir(CSRC):
+        if f.endswith((".hip", ".h", ".cpp")):
+            with open(os.path.join(CSRC, f)) as fh:
+                text = variants.apply(VARIANT, f, fh.read())
+            with open(os.path.join(out, f), "w") as fh:
+                fh.write(text)
+    return out
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not is_stale():
         return LIB
     os.makedirs(BUILD_DIR, exist_ok=True)
     cc = hipcc()
+    src_dir = _patched_sources() if VARIANT in PATCHED else CSRC
 
     def compile_one(item):
         src, extra = item
@@ -103,7 +124,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
             cmd = [cc, "-x", "c++", "-O3", "-std=c++17", "-fPIC", "-Wall", "-I", CSRC, "-I", INCLUDE, *extra,
                    "-c", os.path.join(CSRC, src), "-o", obj]
         else:
-            cmd = [cc, *COMMON, *VARIANT_FLAGS[VARIANT], *extra, "-c", os.path.join(CSRC, src), "-o", obj]
+            cmd = [cc, *COMMON, *VARIANT_FLAGS[VARIANT], *extra, "-c", os.path.join(src_dir, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)

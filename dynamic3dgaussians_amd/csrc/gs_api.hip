@@ -156,25 +156,39 @@ thread_local PlanInfo g_plan;
 // the number of concurrent callers (not by the threads that ever called:
 // thread pools and autograd workers would otherwise each pin one for good).
 // Never freed: a pool destructor could run after the HIP runtime is gone.
+// A slot belongs to the device that was current when it was made (its event
+// and its device-side mapping are that device's): a lease only takes a free
+// slot of the calling thread's current device.
 struct HeaderSlot {
   uint32_t* host = nullptr;  // host pointer
   uint32_t* dev = nullptr;   // the same memory as the kernels address it
   hipEvent_t ev = nullptr;
+  int device = -1;
 };
 std::mutex g_hmu;
 std::vector<HeaderSlot> g_hfree;
 
 struct HeaderLease {
   HeaderSlot s;
+  // set once a plan kernel that writes this slot (and records its event) may
+  // have been enqueued; cleared when the caller has waited for that event.
+  // A lease dropped in between (an error path after the launch) waits for
+  // the event before the slot goes back to the pool, so the next caller's
+  // sentinel cannot be overwritten by a stale kernel.
+  bool in_flight = false;
   HeaderLease() {
+    int device = 0;
+    if (hipGetDevice(&device) != hipSuccess) return;
     {
       std::lock_guard<std::mutex> lk(g_hmu);
-      if (!g_hfree.empty()) {
-        s = g_hfree.back();
-        g_hfree.pop_back();
+      for (size_t i = g_hfree.size(); i-- > 0;) {
+        if (g_hfree[i].device != device) continue;
+        s = g_hfree[i];
+        g_hfree.erase(g_hfree.begin() + (std::ptrdiff_t)i);
         return;
       }
     }
+    s.device = device;
     void* h = nullptr;
     if (hipHostMalloc(&h, sizeof(uint32_t) * GS_MAX_CAMS * M_WORDS,
                       hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
@@ -194,6 +208,9 @@ struct HeaderLease {
   }
   ~HeaderLease() {
     if (!s.host) return;
+    // a kernel that may still write the slot: wait for it, or (the device
+    // failed) keep the slot out of the pool for good
+    if (in_flight && hipEventSynchronize(s.ev) != hipSuccess) return;
     std::lock_guard<std::mutex> lk(g_hmu);
     g_hfree.push_back(s);
   }
@@ -459,6 +476,7 @@ static int plan_read(const uint32_t (*host)[M_WORDS], int C, int prefiltered, in
 static int publish_wait(HeaderLease& hl, int C, hipStream_t s, bool record_only) {
   hipError_t he = hipSuccess;
   if (!record_only) he = hipEventSynchronize(hl.s.ev);
+  if (he == hipSuccess && !record_only) hl.in_flight = false;
   if (he == hipSuccess && !record_only) {
     // every header's last word is 0 once written (header_sentinel): an event
     // that did not cover the header's kernel must not hand back stale words
@@ -497,6 +515,7 @@ static int plan_impl(const gs_gaussians* g, const gs_camera* cams, int C, int pr
   if (!hl.ok()) return fail((int)hipErrorOutOfMemory, "cannot allocate the page-locked plan header buffer");
   header_sentinel(hl, C);
   CamBatch cb;
+  hl.in_flight = true;
   if (int e = plan_enqueue(g, cams, C, prefiltered, debug, geom, image, radii, hl.s.dev, hl.s.ev, cb, s))
     return e;
   // The one host read of the forward (CR/rasterizer_impl.cu:287), one for
@@ -633,7 +652,9 @@ static int backward_impl(const gs_gaussians* g, const gs_camera* cams, int C, co
   ra.dL_dpix = dL_dout_color; ra.dL_dfeat = dL_dout_feature; ra.dL_ddepth = dL_dout_depth;
   ra.dL_dalpha = dL_dout_alpha; ra.acc = acc; ra.dsem = dsem_pad ? dsem_pad : dL_dsemantic;
   {
-    StageTimer t(s, GS_STAGE_RENDER_BWD, true);
+    // with a padded feature width the stage also holds the feature-row copy:
+    // marker events around both launches instead of the blend's dispatch
+    StageTimer t(s, GS_STAGE_RENDER_BWD, dsem_pad == nullptr);
     if (!launch_render_bwd(ra, cb, s)) return fail(-1, "unsupported feature width %d", g->F);
     if (dsem_pad) launch_feature_grad_rows(dsem_pad, dL_dsemantic, P, g->F, accumulate ? 1 : 0, s);
   }
@@ -799,6 +820,7 @@ int gs_forward_batch(const gs_gaussians* g, const gs_camera* cams, int32_t C, in
   header_sentinel(hl, C);
   hipStream_t s = (hipStream_t)stream;
   CamBatch cb;
+  hl.in_flight = true;
   if (int e = plan_enqueue(g, cams, C, prefiltered, 0, geom, image, radii, hl.s.dev, hl.s.ev, cb, s))
     return e;
   const int W = cams[0].image_width, H = cams[0].image_height;
@@ -812,10 +834,8 @@ int gs_forward_batch(const gs_gaussians* g, const gs_camera* cams, int32_t C, in
   if (int e = render_impl(g, cams, C, 0, compat, geom, binning, image, capacity, radii, out_color, out_feature,
                           out_depth, out_alpha, sp, s))
     return e;
-  {
-    const hipError_t he = hipEventSynchronize(hl.s.ev);
-    if (he != hipSuccess) return fail((int)he, "num_rendered readback: %s", hipGetErrorString(he));
-  }
+  // the same wait and sentinel check as the two-phase plan (gs_forward_plan)
+  if (int e = publish_wait(hl, C, s, false)) return e;
   PlanInfo info;
   if (int e = plan_read(reinterpret_cast<const uint32_t(*)[M_WORDS]>(hl.s.host), C, prefiltered, 0, tiles,
                         num_rendered, num_instances, info))

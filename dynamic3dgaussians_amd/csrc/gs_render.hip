@@ -755,9 +755,6 @@ blend_done:
         const float Tp = blk ? t_hi : t_lo;
         if (small) {
           const uint32_t voff = (uint32_t)(pix + (size_t)(4 * (lane >> 5)) * HW) * 4u;
-#ifdef GS_EXP_FWD_NO_FEAT_STORE  // timing / traffic only: the feature planes are not written
-          continue;
-#endif
 #pragma unroll
           for (int fb = 0; fb < FB; ++fb)
 #pragma unroll
@@ -1158,12 +1155,7 @@ __global__ __launch_bounds__(64 * WPB_BWD) __attribute__((amdgpu_waves_per_eu(bw
       const uint32_t gi = FW > 0 ? f_bits(s_slot[lw][slot].w) : agid[t < NAG ? t : 0];
       float* dst = comp < A_FEAT ? acc + (size_t)ACC_STRIDE * gi + comp
                                  : dsem + (size_t)gi * FS + 16 * CB + (comp - A_FEAT);
-#ifdef GS_EXP_NO_ACC_ATOMIC
-      // timing only (results wrong): the atomic-free ceiling
-      if (slot < nb && s_out[i] == 12345.f) *dst = 0.f;
-#else
       if (slot < nb) atomicAdd(dst, s_out[i]);
-#endif
     }
     // features: C[slot][ch] = sum_p w[slot][p] dL/dF[p][ch]; lane l holds
     // channel 16cb + (l&15) of slots (l>>4)*4 + r
@@ -1173,11 +1165,7 @@ __global__ __launch_bounds__(64 * WPB_BWD) __attribute__((amdgpu_waves_per_eu(bw
       for (int r = 0; r < 4; ++r) {
         const int slot = (lane >> 4) * 4 + r;
         const uint32_t gi = fgid[r];
-#ifdef GS_EXP_NO_FEAT_ATOMIC
-        if (slot < nb && cf[cb][r] == 12345.f) dsem[(size_t)gi * FS + 16 * cb + g] = 0.f;
-#else
         if (slot < nb) atomicAdd(dsem + (size_t)gi * FS + 16 * cb + g, cf[cb][r]);
-#endif
       }
     }
   };

@@ -862,10 +862,6 @@ __global__ __launch_bounds__(NT) void tile_sort_kernel(TileArgs a0, CamBatch cb,
     if (threadIdx.x == 0) plist[r.x] = (uint32_t)keys[r.x];
     return;
   }
-#ifdef GS_EXP_SORT_COPY_ONLY  // timing-only variant: the segment copied unsorted (the launch's floor)
-  for (int i = threadIdx.x; i < n; i += NT) plist[r.x + i] = (uint32_t)keys[r.x + i];
-  return;
-#endif
   if (n <= cap) {
     // keys straight from global memory into the bucket sort's registers
     // (no LDS staging copy: sort 0.457-0.462 vs 0.470-0.471 ms per bench step)
