@@ -68,7 +68,7 @@ sys.path.insert(0, REPO)
 
 from dynamic3dgaussians_amd import _lib  # noqa: E402
 from dynamic3dgaussians_amd.camera import camera_rig  # noqa: E402
-from dynamic3dgaussians_amd.distributed import (GradBucket, ShardedAdam, rank_load_scale, shard_camera_windows,  # noqa: E402
+from dynamic3dgaussians_amd.distributed import (GradBucket, ShardedStep, rank_load_scale, shard_camera_windows,  # noqa: E402
                                                 shard_cameras)
 from dynamic3dgaussians_amd.optim import FusedAdam  # noqa: E402
 from dynamic3dgaussians_amd.rasterizer import (GaussianRasterizationSettings,  # noqa: E402
@@ -686,7 +686,7 @@ def main():
     # the torch-activation step); GS_BENCH_RAW=0 keeps torch's activations.
     raw = os.environ.get("GS_BENCH_RAW", "1") != "0"
     # The camera batch as one rank of N (N > 1, or a --proxy-world stand-in):
-    # Adam sharded over the ranks (distributed.ShardedAdam, ZeRO stage 1) --
+    # Adam sharded over the ranks (distributed.ShardedStep over ShardedAdam, ZeRO stage 1) --
     # reduce-scatter, Adam on the rank's 1/N of the parameters, all-gather --
     # with the backward writing its gradients straight into the exchange
     # buffer (grad_into).  GS_BENCH_ZERO=0: the all-reduce + full Adam on
@@ -697,15 +697,11 @@ def main():
             and (world > 1 or args.proxy_world > 1 or (zero_env == "force" and dist_on)))
     z_rank, z_world = (args.proxy_rank, args.proxy_world) if args.proxy_world else (rank, world)
     if zero:
+        # the package's sharded step (distributed.ShardedStep): with `overlap`
+        # geometry in line, features behind the next step (two gradient buffers)
         lrs = {g_["name"]: g_["lr"] for g_ in groups}
         z_coll = dist_on and (world > 1 or zero_env == "force")
-        if overlap:  # geometry in line, features behind the next step (two gradient buffers)
-            zgeo = ShardedAdam({k: v for k, v in params.items() if k != "semantic_feature"}, lrs, rank=z_rank,
-                               world=z_world, eps=1e-15, collectives=z_coll)
-            zfeat = ShardedAdam({"semantic_feature": params["semantic_feature"]}, lrs, rank=z_rank, world=z_world,
-                                eps=1e-15, n_grad_buffers=2, collectives=z_coll)
-        else:
-            zopt = ShardedAdam(params, lrs, rank=z_rank, world=z_world, eps=1e-15, collectives=z_coll)
+        zs = ShardedStep(params, lrs, rank=z_rank, world=z_world, eps=1e-15, collectives=z_coll, overlap=overlap)
     elif split_opt:
         opt = make_opt([g_ for g_ in groups if g_["name"] != "semantic_feature"])
         opt_feat = make_opt([g_ for g_ in groups if g_["name"] == "semantic_feature"])
@@ -724,9 +720,9 @@ def main():
                         for _ in range(2)]
     else:
         bucket = GradBucket(params, bind_grads=dist_on)
-    if split_opt:
+    if split_opt and not zero:
         side = torch.cuda.Stream(device=dev)
-        pipe = {"k": 0, "done": [None, None]}
+    pipe = {"k": 0, "done": [None, None]}
     g = torch.Generator(device=dev).manual_seed(1 + rank)
     H_, W_ = args.height, args.width
     up_color = torch.randn(3, H_, W_, device=dev, generator=g)
@@ -806,38 +802,22 @@ def main():
     arg_of = {"means3D": "means3D", "rgb_colors": "colors_precomp", "unnorm_rotations": "rotations",
               "logit_opacities": "opacities", "log_scales": "scales", "semantic_feature": "semantic_feature"}
 
-    zero_dest = {}  # step parity -> the backward's gradient destinations
-
-    def zero_buffers(k):
-        """(sharded optimizer, gradient buffer) pairs of step parity k."""
-        return [(zgeo, 0), (zfeat, k)] if overlap else [(zopt, 0)]
-
     def step_zero(parts):
-        """One rank's step with the sharded Adam: the backward writes the
-        gradients into the exchange buffers; geometry reduce-scatter + Adam
-        on the rank's slice + all-gather in line; with `overlap` the feature
-        exchange and update behind the next step's projection and binning
-        (their blend waits on the event), double-buffered."""
+        """One rank's step with the sharded Adam (distributed.ShardedStep):
+        the backward writes the gradients into the exchange buffers; geometry
+        reduce-scatter + Adam on the rank's slice + all-gather in line; with
+        `overlap` the feature exchange and update behind the next step's
+        projection and binning (their blend waits on the event),
+        double-buffered."""
         main = torch.cuda.current_stream(dev)
-        k = pipe["k"] if overlap else 0
-        kb = k % 2
-        pending = pipe["done"][kb] if overlap else None
-        if pending is not None:  # step k-2's exchange still reads gradient buffer kb
-            main.wait_event(pending)
+        zs.begin()
         rv = raw_rendervar(params, label, means2D_placeholder)
         if len(parts) == 1:
-            dest = zero_dest.get(kb)
-            if dest is None:
-                dest = zero_dest[kb] = {arg_of[n_]: t_ for o_, b_ in zero_buffers(kb)
-                                        for n_, t_ in o_.grad_views(b_).items()}
-            run_part(parts[0][0], parts[0][1], rv, ready=pipe["done"][(k - 1) % 2] if overlap else None,
-                     grad_into=dest)
+            run_part(parts[0][0], parts[0][1], rv, ready=zs.feature_ready, grad_into=zs.grad_into(arg_of))
         else:
             # sub-batches on their own streams accumulate through autograd
-            drain()
-            for o_, b_ in zero_buffers(kb):
-                o_.bind(b_)
-                o_.zero_grad(b_)
+            zs.drain()
+            zs.bind_grads()
             for _, _, st in parts:
                 st.wait_stream(main)
             for ras, ups, st in parts:
@@ -845,25 +825,13 @@ def main():
                     run_part(ras, ups, rv)
             for _, _, st in parts:
                 main.wait_stream(st)
-        if not overlap:
-            zopt.step(0)
-            return
-        zgeo.step(0)                                   # geometry: on the critical path
-        work = zfeat.reduce_scatter(kb, async_op=True)  # features: behind the next step
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            if work is not None:
-                work.wait()
-            zfeat.update(kb)
-            zfeat.all_gather()
-            ev = torch.cuda.Event()
-            ev.record(side)
-        pipe["done"][kb] = ev
-        pipe["k"] = k + 1
+        zs.finish()
 
     def drain():
         """Overlap mode: the main stream waits for every pending feature update."""
-        if split_opt:
+        if zero:
+            zs.drain()
+        elif split_opt:
             for ev in pipe["done"]:
                 if ev is not None:
                     torch.cuda.current_stream(dev).wait_event(ev)
@@ -953,9 +921,7 @@ def main():
         torch, GaussianRasterizer, one backward, the optimizer step)."""
         drain()
         if zero:
-            for o_, b_ in zero_buffers(0):
-                o_.bind(b_)
-                o_.zero_grad(b_)
+            zs.bind_grads()
         else:
             if overlap:
                 feat_buckets[0].bind()
@@ -970,8 +936,7 @@ def main():
             im, _, depth, _ = ras(**rv)
             torch.autograd.backward([im, depth], [up_color, up_depth])
         if zero:
-            for o_, b_ in zero_buffers(0):
-                o_.step(b_)
+            zs.finish(inline=True)
             return
         bucket.all_reduce()
         opt.step()
@@ -987,9 +952,7 @@ def main():
             return step_single_camera()
         drain()
         if zero:
-            for o_, b_ in zero_buffers(0):
-                o_.bind(b_)
-                o_.zero_grad(b_)
+            zs.bind_grads()
         else:
             if overlap:
                 feat_buckets[0].bind()
@@ -1031,8 +994,7 @@ def main():
         keys = [k for k in leaves if k != "means2D" and summed.get(k) is not None]
         torch.autograd.backward([rv[k] for k in keys], [summed[k] for k in keys])
         if zero:
-            for o_, b_ in zero_buffers(0):
-                o_.step(b_)
+            zs.finish(inline=True)
             return
         bucket.all_reduce()
         opt.step()
@@ -1058,6 +1020,12 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     _lib.timing_enable(True, stages=[dom])
+
+    def plan_counts():
+        """(forward calls, capacity retries) of the camera batch's sync-free plans."""
+        pl = [p_[0].plan for p_ in batch_parts if p_[0].plan is not None] if args.mode == "batch" else []
+        return sum(p_.calls for p_ in pl), sum(p_.retries for p_ in pl)
+    plan0 = plan_counts()
     t0 = time.perf_counter()
     host_marks = []
     for _ in range(args.steps):
@@ -1068,6 +1036,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    plan1 = plan_counts()
     stages = _lib.timing_read()
     _lib.timing_enable(False)
     drain()
@@ -1223,12 +1192,16 @@ def main():
                                "fwd+bwd of every camera + grad all-reduce + Adam",
                    "mode": ("camera batch (GaussianRasterizerBatch: one launch per stage for the rank's "
                             "cameras)" if args.mode == "batch" else "per camera (GaussianRasterizer drop-in)"),
-                   "optimizer": (f"sharded Adam (ZeRO-1, distributed.ShardedAdam): rank {z_rank}'s 1/{z_world} "
+                   "optimizer": (f"sharded Adam (ZeRO-1, distributed.ShardedStep): rank {z_rank}'s 1/{z_world} "
                                  "of the parameters, gradients written into the exchange buffer" if zero
                                  else optim_kind),
                    "streams": n_streams if args.mode == "percam" else len(batch_parts),
                    "forward": ("sync-free (gs_forward_batch: binning sized from the previous step)" if sync_free
                                and args.mode == "batch" else "two-phase (plan, host read, render)"),
+                   # the timed window's sync-free forwards and how many re-rendered with exact lengths
+                   # (0: every camera rendered once per step)
+                   "sync_free_calls_timed": plan1[0] - plan0[0],
+                   "sync_free_retries_timed": plan1[1] - plan0[1],
                    "binning_walk": ("3-D Morton order of the means (gs_gaussians.walk_order)"
                                     if args.mode == "batch" and any(p_[0]._walk is not None for p_ in batch_parts)
                                     else "id order"),

@@ -203,7 +203,8 @@ class GradBucket:
     def __init__(self, params: Iterable[torch.Tensor] | Mapping[str, torch.Tensor],
                  extras: Dict[str, torch.Tensor] | None = None,
                  extras_from: tuple[Mapping[str, torch.Tensor], Sequence[str]] | None = None,
-                 bind_grads: bool = False, keys: Sequence[str] | None = None, track_reached: bool = False):
+                 bind_grads: bool = False, keys: Sequence[str] | None = None, track_reached: bool = False,
+                 n_aux: int = 0):
         if isinstance(params, Mapping):
             self._param_src, self._param_keys = params, list(keys if keys is not None else params.keys())
             self.params = [params[k] for k in self._param_keys]
@@ -221,10 +222,16 @@ class GradBucket:
         self._extra_numel = {k: t.numel() for k, t in self.extras.items()}
         sizes = self._param_numel + list(self._extra_numel.values())
         self.sizes = sizes
-        dev = self.params[0].device
+        if not self.params and not self.extras:
+            raise ValueError("GradBucket: nothing to exchange")
+        dev = (self.params[0] if self.params else next(iter(self.extras.values()))).device
         self.track = bool(track_reached and bind_grads)
         n_flags = len(self.params) if self.track else 0
-        self.flat = torch.zeros(sum(sizes) + n_flags, dtype=torch.float32, device=dev)
+        # n_aux: a per-step slot summed as it is (all_reduce(aux=...)), e.g.
+        # ShardedStep's reached-parameter flags riding with the statistics
+        self.n_aux = int(n_aux)
+        self._aux_at = sum(sizes) + n_flags
+        self.flat = torch.zeros(sum(sizes) + n_flags + self.n_aux, dtype=torch.float32, device=dev)
         self.bound = bind_grads
         self._reached = [False] * len(self.params)
         self._unbound = set()
@@ -354,7 +361,7 @@ class GradBucket:
             torch.sub(t.reshape(-1), self._base[k].reshape(-1), out=self.flat[o:o + n])
             o += n
         if self.track:
-            self.flat[o:].copy_(torch.tensor(self._reached, dtype=torch.float32))
+            self.flat[o:o + len(self.params)].copy_(torch.tensor(self._reached, dtype=torch.float32))
 
     def unpack(self):
         o = 0
@@ -371,18 +378,25 @@ class GradBucket:
             torch.add(self._base[k].reshape(-1), self.flat[o:o + n], out=t.reshape(-1))
             o += n
 
-    def all_reduce(self, group=None):
+    def all_reduce(self, group=None, aux: Optional[torch.Tensor] = None):
         """pack -> one all_reduce(SUM) -> unpack.  Without a process group
-        (or with one rank) the values stay as they are."""
+        (or with one rank) the values stay as they are.  `aux`: n_aux floats
+        summed over the ranks in the same collective, in place."""
         self.check_live()
+        if aux is not None and aux.numel() != self.n_aux:
+            raise ValueError(f"GradBucket: aux of {aux.numel()} floats, the bucket holds {self.n_aux}")
         if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
             self.resync()
             return
         self.pack()
+        if aux is not None:
+            self.flat[self._aux_at:].copy_(aux.reshape(-1))
         dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
         self.unpack()
+        if aux is not None:
+            aux.reshape(-1).copy_(self.flat[self._aux_at:])
         if self.track:
-            reached = self.flat[len(self.flat) - len(self.params):].cpu()
+            reached = self.flat[self._aux_at - len(self.params):self._aux_at].cpu()
             for i, p in enumerate(self.params):
                 if reached[i] == 0:
                     p.grad = None
@@ -435,11 +449,18 @@ class ShardedAdam:
     reduce-scatter / all-gather as all-reduces of the whole buffer.
 
     Adam is torch.optim.Adam's (amsgrad off, no weight decay; gs_optim.h):
-    one step count for every parameter, bias corrections computed in double
-    on the host, per-parameter learning rates `lr[name]`.  At N = 1 it is
-    bit-identical to FusedAdam over the same parameters; at N > 1 the
-    gradient sums are the collective's.  Not the reference's optimizer
-    object (no param_groups / state surgery): densification rebuilds it.
+    a step count per parameter (a parameter no rank's loss reached is skipped
+    and keeps its count, as torch skips a .grad of None), bias corrections
+    computed in double on the host, per-parameter learning rates `lr[name]`
+    (update(lr=...) takes the current ones, e.g. from the reference
+    optimizer's param_groups).  At N = 1 it is bit-identical to FusedAdam over
+    the same parameters; at N > 1 the gradient sums are the collective's.
+    Not the reference's optimizer object: load_state() takes the moments and
+    step counts from one (torch.optim.Adam / FusedAdam state), export_state()
+    writes them back (all-gathering the moments) so the reference's
+    optimizer-state surgery (densification, external.py:157-213) can run on
+    it, and replace() rebinds a same-size replacement tensor with zeroed
+    moments (update_params_and_optimizer, external.py:143-155).
     """
 
     def __init__(self, params: Mapping[str, torch.Tensor], lr: Mapping[str, float], rank: Optional[int] = None,
@@ -494,7 +515,7 @@ class ShardedAdam:
             self.grad_shard = [g[self.lo:self.hi] for g in self.grad_flat]
         self.exp_avg = torch.zeros(self.chunk, dtype=torch.float32, device=dev)
         self.exp_avg_sq = torch.zeros(self.chunk, dtype=torch.float32, device=dev)
-        self.t = 0
+        self.steps = [0] * len(self.params)
         # the rank's slice as pieces of the parameters: (param index, flat start, flat end)
         self.pieces = []
         for i, (o, m) in enumerate(zip(self.offsets, sizes)):
@@ -548,19 +569,38 @@ class ShardedAdam:
         return dist.all_gather_into_tensor(self.param_flat, self.param_flat[self.lo:self.hi], group=self.group,
                                            async_op=async_op)
 
+    @property
+    def t(self) -> int:
+        """The largest per-parameter step count."""
+        return max(self.steps)
+
     # ------------------------------------------------------------ update
-    def update(self, k: int = 0) -> None:
-        """Adam on this rank's slice, from grad_shard[k] (one launch)."""
-        self.t += 1
-        bc1 = 1.0 - self.beta1 ** self.t
-        bc2s = (1.0 - self.beta2 ** self.t) ** 0.5
+    def update(self, k: int = 0, lr: Optional[Mapping[str, float]] = None,
+               reached: Optional[Sequence[bool]] = None) -> None:
+        """Adam on this rank's slice, from grad_shard[k] (one launch).
+        `lr`: {name: learning rate} for this step (missing names keep the
+        constructor's).  `reached`: per parameter (self.names order), whether
+        any rank's loss reached it -- unreached parameters are neither
+        updated nor counted (every rank must pass the same flags)."""
+        lrs = self.lr if lr is None else [float(lr.get(n, l)) for n, l in zip(self.names, self.lr)]
+        live = [True] * len(self.params) if reached is None else [bool(x) for x in reached]
+        if len(live) != len(self.params):
+            raise ValueError(f"ShardedAdam: {len(live)} reach flags for {len(self.params)} parameters")
+        for i, on in enumerate(live):
+            if on:
+                self.steps[i] += 1
         entries = []
         g = self.grad_shard[k]
         for i, a, b in self.pieces:
+            if not live[i]:
+                continue
+            t = self.steps[i]
+            bc1 = 1.0 - self.beta1 ** t
+            bc2s = (1.0 - self.beta2 ** t) ** 0.5
             s, e = a - self.lo, b - self.lo
             entries.append((self.param_flat[a:b], g[s:e], self.exp_avg[s:e], self.exp_avg_sq[s:e],
-                            (self.lr[i] / bc1) * -1, bc2s))
-        self._apply(k, entries)
+                            (lrs[i] / bc1) * -1, bc2s))
+        self._apply((k, tuple(live)), entries)
 
     def _apply(self, k, entries) -> None:
         if not entries:
@@ -583,8 +623,292 @@ class ShardedAdam:
                                             torch.cuda.current_stream(self.param_flat.device).cuda_stream),
                    "sharded adam step")
 
-    def step(self, k: int = 0) -> None:
+    def step(self, k: int = 0, lr: Optional[Mapping[str, float]] = None,
+             reached: Optional[Sequence[bool]] = None) -> None:
         """reduce_scatter(k) -> update(k) -> all_gather(), in line."""
         self.reduce_scatter(k)
-        self.update(k)
+        self.update(k, lr, reached)
         self.all_gather()
+
+    # ------------------------------------------------------------ state
+    def _slices(self, i: int):
+        """(flat start, flat end) of this rank's pieces of parameter i."""
+        return [(a, b) for j, a, b in self.pieces if j == i]
+
+    @torch.no_grad()
+    def load_state(self, optimizer) -> None:
+        """The moments (this rank's slice) and step counts of a torch-style
+        Adam's state (torch.optim.Adam / FusedAdam: state[p] = {'step',
+        'exp_avg', 'exp_avg_sq'}); parameters without state start at zero."""
+        for i, (p, o) in enumerate(zip(self.params, self.offsets)):
+            st = optimizer.state.get(p)
+            st = st if st else None
+            for a, b in self._slices(i):
+                s, e = a - self.lo, b - self.lo
+                if st is None:
+                    self.exp_avg[s:e].zero_()
+                    self.exp_avg_sq[s:e].zero_()
+                else:
+                    self.exp_avg[s:e].copy_(st["exp_avg"].reshape(-1)[a - o:b - o])
+                    self.exp_avg_sq[s:e].copy_(st["exp_avg_sq"].reshape(-1)[a - o:b - o])
+            self.steps[i] = int(float(st["step"])) if st is not None else 0
+
+    def _gather(self, x: torch.Tensor) -> torch.Tensor:
+        """Every rank's chunk of `x` (a moment) as one world * chunk buffer."""
+        full = torch.zeros(self.world * self.chunk, dtype=x.dtype, device=x.device)
+        full[self.lo:self.hi].copy_(x)
+        if self.world == 1:
+            return full
+        if not self.collectives:
+            raise RuntimeError("ShardedAdam: exporting the moments of a rank of N needs the process group")
+        if self._emulate:
+            dist.all_reduce(full, op=dist.ReduceOp.SUM, group=self.group)
+        else:
+            dist.all_gather_into_tensor(full, x.contiguous(), group=self.group)
+        return full
+
+    @torch.no_grad()
+    def export_state(self, optimizer) -> None:
+        """Write the full moments and step counts into optimizer.state (a
+        collective at N > 1: every rank calls it), e.g. before the
+        reference's densification surgery or a checkpoint."""
+        m, v = self._gather(self.exp_avg), self._gather(self.exp_avg_sq)
+        for i, (p, o) in enumerate(zip(self.params, self.offsets)):
+            if self.steps[i] == 0 and not optimizer.state.get(p):
+                continue  # never stepped: the reference optimizer has no state for it either
+            n = p.numel()
+            optimizer.state[p] = {"step": torch.tensor(float(self.steps[i]), dtype=torch.float32),
+                                  "exp_avg": m[o:o + n].view_as(p).clone(),
+                                  "exp_avg_sq": v[o:o + n].view_as(p).clone()}
+
+    @torch.no_grad()
+    def replace(self, name: str, tensor: torch.Tensor, reset_moments: bool = True) -> None:
+        """Rebind parameter `name` to `tensor` (same number of elements, e.g.
+        a new Parameter from update_params_and_optimizer, external.py:143-155):
+        its values move into the flat storage and its .data becomes the view;
+        with reset_moments its moments are zeroed.  The step count is kept."""
+        i = self.names.index(name)
+        old, o = self.params[i], self.offsets[i]
+        if tensor.numel() != old.numel():
+            raise ValueError(f"ShardedAdam.replace: '{name}' has {tensor.numel()} elements, "
+                             f"the layout {old.numel()}")
+        if tensor.dtype != torch.float32 or tensor.device != self.param_flat.device:
+            raise ValueError(f"ShardedAdam.replace: '{name}' must be fp32 on {self.param_flat.device}")
+        n = tensor.numel()
+        if tensor is not old:
+            self.param_flat[o:o + n].copy_(tensor.detach().reshape(-1))
+            tensor.data = self.param_flat[o:o + n].view_as(tensor)
+            self.params[i] = tensor
+        if reset_moments:
+            for a, b in self._slices(i):
+                self.exp_avg[a - self.lo:b - self.lo].zero_()
+                self.exp_avg_sq[a - self.lo:b - self.lo].zero_()
+
+
+class ShardedStep:
+    """One rank's optimizer step of the camera-sharded training step
+    (the reference's loss.backward() -> optimizer.step() ->
+    zero_grad(), train.py:424-433, with a step's cameras sharded over the
+    ranks): Adam sharded over the ranks (ZeRO stage 1, ShardedAdam) and, with
+    `overlap`, the feature gradients' exchange and update run behind the next
+    step.
+
+    Geometry (every parameter but `feature_key`): reduce-scatter, Adam on the
+    rank's slice, all-gather -- in line, on the step's critical path.
+    Features (`overlap`, the 32 of 46 floats per Gaussian at F = 32): two
+    gradient buffers, step k's backward writes buffer k % 2; finish() issues
+    its reduce-scatter asynchronously and runs the update and the all-gather
+    on a side stream, behind an event.  Step k+1's blend waits for that event
+    (`feature_ready` -> GaussianRasterizer(..., feature_ready=...) ->
+    gs_gaussians.feature_ready), so the projection and binning of step k+1
+    overlap the exchange; step k+2 waits for it in begin() before its
+    backward writes buffer k % 2 again.  Without `overlap` (no features, no
+    CUDA, or overlap=False) one ShardedAdam steps every parameter in line.
+
+    A step:
+
+        zs.begin()
+        out = rasterizer(..., feature_ready=zs.feature_ready, grad_into=zs.grad_into(arg_names))
+        torch.autograd.backward(outputs, upstream)      # or: zs.bind_grads() before any autograd path,
+        zs.finish()                                     #     or zs.load_grads() after it
+
+    and zs.drain() before anything reads the features outside that pattern
+    (another stream, the host, a checkpoint).  Moved out of bench.py's
+    step_zero (round 5) so the training driver (timesteps.TimestepDriver)
+    takes the same path the per-rank bench proxies measure.
+
+    `adam_cls`: the ShardedAdam class (tests substitute a torch restatement
+    of the update to run the plumbing on the CPU)."""
+
+    def __init__(self, params: Mapping[str, torch.Tensor], lr: Mapping[str, float], rank: Optional[int] = None,
+                 world: Optional[int] = None, group=None, eps: float = 1e-15, betas=(0.9, 0.999),
+                 overlap: Optional[bool] = None, feature_key: str = "semantic_feature",
+                 collectives: Optional[bool] = None, emulate: Optional[bool] = None, adam_cls=None):
+        adam_cls = ShardedAdam if adam_cls is None else adam_cls
+        self.names = list(params)
+        dev = params[self.names[0]].device
+        if overlap is None:
+            overlap = feature_key in params and dev.type == "cuda"
+        if overlap and (feature_key not in params or dev.type != "cuda" or len(self.names) < 2):
+            raise ValueError("ShardedStep(overlap=True) needs CUDA parameters with a feature tensor "
+                             f"'{feature_key}' and geometry")
+        self.overlap = bool(overlap)
+        self.feature_key = feature_key
+        kw = dict(rank=rank, world=world, group=group, eps=eps, betas=betas, collectives=collectives,
+                  emulate=emulate)
+        if self.overlap:
+            self.geo = adam_cls({k: params[k] for k in self.names if k != feature_key}, lr, **kw)
+            self.feat = adam_cls({feature_key: params[feature_key]}, lr, n_grad_buffers=2, **kw)
+            self.side = torch.cuda.Stream(device=dev)
+        else:
+            self.geo = adam_cls(dict(params), lr, **kw)
+            self.feat = None
+            self.side = None
+        self.device = dev
+        self.k = 0                   # steps finished
+        self._done = [None, None]    # per feature buffer: the event of the last exchange that read it
+        self._bound = False
+
+    # ------------------------------------------------------------ layout
+    @property
+    def opts(self) -> List[ShardedAdam]:
+        return [self.geo] + ([self.feat] if self.feat is not None else [])
+
+    @property
+    def params(self) -> Dict[str, torch.Tensor]:
+        return {n: p for o in self.opts for n, p in zip(o.names, o.params)}
+
+    @property
+    def rank(self) -> int:
+        return self.geo.rank
+
+    @property
+    def world(self) -> int:
+        return self.geo.world
+
+    def _buffers(self):
+        """(optimizer, gradient buffer index) pairs of the current step."""
+        return [(self.geo, 0)] + ([(self.feat, self.k % 2)] if self.feat is not None else [])
+
+    # ------------------------------------------------------------ a step
+    def begin(self) -> None:
+        """Start step k: the current stream waits until step k-2's feature
+        exchange no longer reads gradient buffer k % 2."""
+        if self.feat is None:
+            return
+        pending = self._done[self.k % 2]
+        if pending is not None:
+            torch.cuda.current_stream(self.device).wait_event(pending)
+
+    @property
+    def feature_ready(self):
+        """The event the step's blend waits for before reading the features
+        (step k-1's feature update), or None."""
+        return self._done[(self.k - 1) % 2] if self.feat is not None else None
+
+    def grad_into(self, arg_names: Optional[Mapping[str, str]] = None) -> Dict[str, torch.Tensor]:
+        """{name: view} destinations of this step's gradients, for the
+        camera batch's backward (GaussianRasterizerBatch(...)(...,
+        grad_into=...)); `arg_names` maps parameter names to the rasterizer's
+        argument names.  Written whole by that backward: no zeroing."""
+        out = {}
+        for o, b in self._buffers():
+            for n, v in o.grad_views(b).items():
+                out[arg_names[n] if arg_names is not None else n] = v
+        return out
+
+    def bind_grads(self) -> None:
+        """Every parameter's .grad becomes its (zeroed) view of this step's
+        buffers: autograd accumulates the step's gradients into them."""
+        for o, b in self._buffers():
+            o.bind(b)
+            o.zero_grad(b)
+        self._bound = True
+
+    @torch.no_grad()
+    def load_grads(self) -> List[bool]:
+        """Move the parameters' unbound .grad (from any autograd path) into
+        this step's buffers and clear them; returns per parameter (names
+        order of `params`) whether it had a gradient."""
+        flags = {}
+        for o, b in self._buffers():
+            views = o.grad_views(b)
+            for n, p in zip(o.names, o.params):
+                g = p.grad
+                flags[n] = g is not None
+                if g is None:
+                    views[n].zero_()
+                else:
+                    views[n].copy_(g)
+                p.grad = None
+        return [flags[n] for n in self.params]
+
+    def _split(self, lr, reached):
+        """Per-optimizer reach flags from flags in `params` order."""
+        if reached is None:
+            return [None for _ in self.opts]
+        by_name = dict(zip(self.params, reached))
+        return [[bool(by_name[n]) for n in o.names] for o in self.opts]
+
+    def finish(self, lr: Optional[Mapping[str, float]] = None, reached: Optional[Sequence[bool]] = None,
+               inline: bool = False) -> None:
+        """The optimizer step of step k (geometry in line; with `overlap`
+        and not `inline`, the features behind the next step).  `lr`,
+        `reached`: as ShardedAdam.update (reached in `params` order)."""
+        rg = self._split(lr, reached)
+        if self._bound:  # the views stay the gradients' home only for this step
+            for o in self.opts:
+                for p in o.params:
+                    p.grad = None
+            self._bound = False
+        if self.feat is None:
+            self.geo.step(0, lr, rg[0])
+            self.k += 1
+            return
+        kb = self.k % 2
+        self.geo.step(0, lr, rg[0])
+        if inline:
+            self.feat.step(kb, lr, rg[1])
+            self._done[kb] = None
+            self.k += 1
+            return
+        main = torch.cuda.current_stream(self.device)
+        work = self.feat.reduce_scatter(kb, async_op=True)
+        self.side.wait_stream(main)
+        with torch.cuda.stream(self.side):
+            if work is not None:
+                work.wait()
+            self.feat.update(kb, lr, rg[1])
+            self.feat.all_gather()
+            ev = torch.cuda.Event()
+            ev.record(self.side)
+        self._done[kb] = ev
+        self.k += 1
+
+    def drain(self) -> None:
+        """The current stream waits for every pending feature update."""
+        if self.feat is None:
+            return
+        cur = torch.cuda.current_stream(self.device)
+        for ev in self._done:
+            if ev is not None:
+                cur.wait_event(ev)
+
+    # ------------------------------------------------------------ state
+    def load_state(self, optimizer) -> None:
+        for o in self.opts:
+            o.load_state(optimizer)
+
+    def export_state(self, optimizer) -> None:
+        """Full moments and step counts into optimizer.state (a collective)."""
+        self.drain()
+        for o in self.opts:
+            o.export_state(optimizer)
+
+    def replace(self, name: str, tensor: torch.Tensor, reset_moments: bool = True) -> None:
+        self.drain()
+        for o in self.opts:
+            if name in o.names:
+                o.replace(name, tensor, reset_moments)
+                return
+        raise KeyError(name)

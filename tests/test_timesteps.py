@@ -15,6 +15,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from dynamic3dgaussians_amd.camera import camera_rig
+from dynamic3dgaussians_amd.distributed import ShardedAdam, ShardedStep
 from dynamic3dgaussians_amd.scene import camera_tensors, make_gaussians
 from dynamic3dgaussians_amd.timesteps import (TimestepDriver, initialize_post_first_timestep,
                                               initialize_per_timestep, update_params_and_optimizer)
@@ -288,3 +289,141 @@ def test_driver_loss_decreases_on_fit():
     drv = TimestepDriver(params, {}, opt, N_CAMS, render)
     losses = drv.timestep(0, 8, tg)
     assert losses[-1] < 0.8 * losses[0], losses
+
+
+# ------------------------------------------------------------ sharded optimizer step
+
+class _TorchAdamSlices(ShardedAdam):
+    """ShardedAdam with its update restated as torch.optim.Adam's own
+    single-tensor arithmetic (the CPU path of torch/optim/adam.py: lerp_,
+    mul_/addcmul_, (sqrt / bc2_sqrt) + eps, addcdiv_), so a sharded driver
+    on the CPU is held bit-for-bit to the plain driver's torch.optim.Adam.
+    (On the GPU the update is the HIP kernel, held to FusedAdam bit-for-bit
+    by tests/test_gpu_sharded_adam.py.)"""
+
+    def _apply(self, k, entries):
+        for p, g, m, v, step_size, bc2s in entries:
+            m.lerp_(g, 1 - self.beta1)
+            v.mul_(self.beta2).addcmul_(g, g, value=1 - self.beta2)
+            p.addcdiv_(m, (v.sqrt() / bc2s).add_(self.eps), value=step_size)
+
+
+def _sharded_factory(params, lr, rank, world, group):
+    return ShardedStep(params, lr, rank=rank, world=world, group=group, eps=1e-15, overlap=False,
+                       adam_cls=_TorchAdamSlices)
+
+
+def _run_driver(rank, world, sharded, densify=None, steps=(2, 2)):
+    """A 2-timestep run; a parameter reached by no loss ('idle', skipped by
+    Adam on both paths) and one reached only by rank 0's extra loss
+    ('rank0_only': updated on every rank from the union of the ranks' reach);
+    lr = 0 for log_scales after timestep 0 (initialize_post_first_timestep's
+    params_to_fix) -- the learning rates come from the optimizer each step."""
+    torch.manual_seed(0)
+    params = _leaf(_params())
+    lrs = dict(LRS)
+    if densify is None:  # (the toy densification handles per-Gaussian tensors only)
+        params["idle"] = torch.nn.Parameter(torch.ones(5, 2))
+        params["rank0_only"] = torch.nn.Parameter(torch.full((3,), 0.5))
+        lrs.update(idle=1e-2, rank0_only=1e-2)
+    opt = torch.optim.Adam([{"params": [params[k]], "name": k, "lr": lr} for k, lr in lrs.items()], lr=0.0,
+                           eps=1e-15)
+
+    def extra(pr, variables, rv, t):
+        out = 0.01 * (pr["means3D"] ** 2).mean()
+        if rank == 0 and "rank0_only" in pr:
+            out = out + (pr["rank0_only"] ** 2).sum()
+        return out
+
+    def post_first(pr, variables, optimizer):
+        for g in optimizer.param_groups:
+            if g["name"] == "log_scales":
+                g["lr"] = 0.0
+        variables["prev_pts"] = pr["means3D"].detach()
+        variables["prev_rot"] = torch.nn.functional.normalize(pr["unnorm_rotations"]).detach()
+        return variables
+
+    drv = TimestepDriver(params, {}, opt, N_CAMS, _splat_render(_rig()), rank=rank, world=world, densify=densify,
+                         extra_loss=extra, sharded=sharded)
+    losses = drv.run(steps[0], lambda t: steps[1], _targets, post_first=post_first)
+    state = {k: {n: v.detach().clone() for n, v in opt.state[p].items() if torch.is_tensor(v)}
+             for k, p in drv.params.items() if isinstance(p, torch.nn.Parameter) and opt.state.get(p)}
+    return ({k: v.detach().clone() for k, v in drv.params.items()},
+            {k: drv.variables[k].clone() for k in ("means2D_gradient_accum", "denom", "max_2D_radius")},
+            state, losses, drv.zs is not None)
+
+
+def _sharded_worker(rank, world, port, q, densify):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        out = []
+        for sharded in (False, _sharded_factory):
+            pr, var, st, losses, used = _run_driver(rank, world, sharded, _toy_densify if densify else None)
+            out.append(({k: v.numpy() for k, v in pr.items()}, {k: v.numpy() for k, v in var.items()},
+                        {k: {n: v.numpy() for n, v in d.items()} for k, d in st.items()}, losses, used))
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def _check_same(a, b, exact, what):
+    if exact:
+        np.testing.assert_array_equal(a, b, err_msg=what)
+    else:  # three ranks' sums: the collectives may add in different orders
+        np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-7, err_msg=what)
+
+
+def test_sharded_driver_one_rank_equals_plain_driver():
+    plain = _run_driver(0, 1, False)
+    shard = _run_driver(0, 1, _sharded_factory)
+    assert not plain[4] and shard[4]
+    for k in plain[0]:
+        _check_same(shard[0][k].numpy(), plain[0][k].numpy(), True, k)
+    for k in plain[1]:
+        _check_same(shard[1][k].numpy(), plain[1][k].numpy(), True, k)
+    # the optimizer holds the sharded step's state at the end of run()
+    assert set(shard[2]) == set(plain[2]) and "idle" not in plain[2]
+    for k in plain[2]:
+        for n in ("step", "exp_avg", "exp_avg_sq"):
+            _check_same(shard[2][k][n].numpy(), plain[2][k][n].numpy(), True, f"{k}.{n}")
+
+
+@pytest.mark.parametrize("world,densify", [(2, False), (3, False), (2, True)])
+def test_sharded_driver_equals_plain_bucket_driver(world, densify):
+    """The driver with distributed.ShardedStep (reduce-scatter, Adam on the
+    rank's slice, all-gather; statistics + reach flags in one small
+    all-reduce) against the plain GradBucket + torch.optim.Adam driver, both
+    over `world` gloo ranks for 2 timesteps x 2 iterations: the per-timestep
+    re-initialisation (replace with zeroed moments), the lr change after
+    timestep 0, an unreached and a rank-0-only parameter, and (densify=True)
+    the plain path through timestep 0's densification before the sharded
+    step takes over from the optimizer's state."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sharded_worker, args=(r, world, port, q, densify)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    exact = world == 2
+    for r in range(world):
+        (pp, vp, sp, lp, up), (ps, vs, ss, ls, us) = res[r]
+        assert not up and us
+        for k in pp:
+            _check_same(ps[k], pp[k], exact, f"rank {r} {k}")
+            np.testing.assert_array_equal(ps[k], res[0][1][0][k])  # every rank holds the same parameters
+        if not densify:
+            assert not np.array_equal(pp["rank0_only"], np.full(3, 0.5, np.float32))  # updated on every rank
+            np.testing.assert_array_equal(pp["idle"], np.ones((5, 2), np.float32))     # never updated
+        for k in vp:
+            _check_same(vs[k], vp[k], exact, f"rank {r} {k}")
+        assert set(ss) == set(sp)
+        for k in sp:
+            for n in sp[k]:
+                _check_same(ss[k][n], sp[k][n], exact, f"rank {r} {k}.{n}")
+        np.testing.assert_allclose(np.asarray(ls), np.asarray(lp), rtol=1e-5)

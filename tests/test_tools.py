@@ -77,8 +77,10 @@ def test_compare_params_bounds_by_the_learning_rate(tmp_path):
         paths[name] = str(tmp_path / f"{name}.npz")
         np.savez(paths[name], **run_like(shift))
     refs = [paths["a"], paths["b"], paths["c"]]
-    assert _run(["tools/compare_params.py", paths["chaos"]] + refs).returncode == 0
-    assert _run(["tools/compare_params.py", paths["error"]] + refs).returncode == 1
+    # strict by default (3 x floor); the lr-scaled bound only when asked for
+    assert _run(["tools/compare_params.py", paths["chaos"]] + refs).returncode == 1
+    assert _run(["tools/compare_params.py", "--lr-bound", paths["chaos"]] + refs).returncode == 0
+    assert _run(["tools/compare_params.py", "--lr-bound", paths["error"]] + refs).returncode == 1
 
 
 def test_pmc_split_averages_per_launch_and_splits_wave_cycles(tmp_path):
@@ -99,3 +101,48 @@ def test_pmc_split_averages_per_launch_and_splits_wave_cycles(tmp_path):
     assert row["SQ_WAVE_CYCLES"] == 1000 and row["launches"] == 2
     assert (row["frac_issuing"], row["frac_parked"], row["frac_issue_stalled"]) == (0.2, 0.7, 0.1)
     assert row["valu_per_wave"] == 277.0 and row["lds_per_wave"] == 66.0 and row["lds_conflict_frac"] == 0.35
+
+
+def _pmc_csv(path, rows):
+    import csv
+    with open(path, "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=["Dispatch_Id", "Kernel_Name", "Counter_Name", "Counter_Value"])
+        w.writeheader()
+        for d, k, c, v in rows:
+            w.writerow({"Dispatch_Id": d, "Kernel_Name": k, "Counter_Name": c, "Counter_Value": v})
+
+
+def test_pmc_tools_refuse_an_empty_or_extra_launch(tmp_path):
+    """tools/pmc_*.py count per rep of the profiled program (two reps of one
+    launch per stage): a render_fwd launch that rendered nothing (the
+    sync-free forward's first call, which retries) or an extra dispatch is
+    refused instead of diluting the per-launch average."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import pmc_traffic as T
+    good = [(1, "render_fwd_kernel<32, 0>", "SQ_INSTS_VALU", 900.0), (2, "render_bwd_kernel<32, 0>", "SQ_INSTS_VALU", 50.0),
+            (3, "tile_sort_kernel<256>", "SQ_INSTS_VALU", 7.0), (4, "tile_sort_kernel<512>", "SQ_INSTS_VALU", 3.0),
+            (5, "render_fwd_kernel<32, 0>", "SQ_INSTS_VALU", 910.0), (6, "render_bwd_kernel<32, 0>", "SQ_INSTS_VALU", 50.0),
+            (7, "tile_sort_kernel<256>", "SQ_INSTS_VALU", 7.0), (8, "tile_sort_kernel<512>", "SQ_INSTS_VALU", 3.0)]
+    rows = [dict(Dispatch_Id=d, Kernel_Name=k, Counter_Name=c, Counter_Value=v) for d, k, c, v in good]
+    out = T.per_rep(rows, "SQ_INSTS_VALU", reps=2)
+    assert out[("render_fwd", "render_fwd")] == 905.0
+    assert out[("sort", "tile_sort")] == 10.0  # both class launches of a rep summed
+    # one empty forward (3 dispatches for 2 reps) and one light rep
+    import pytest
+    with pytest.raises(T.UnevenLaunches):
+        T.per_rep(rows + [dict(Dispatch_Id=9, Kernel_Name="render_fwd_kernel<32, 0>", Counter_Name="SQ_INSTS_VALU",
+                               Counter_Value=0.0)], "SQ_INSTS_VALU", reps=2)
+    light = [dict(r) for r in rows]
+    light[0]["Counter_Value"] = 0.0
+    with pytest.raises(T.UnevenLaunches):
+        T.per_rep(light, "SQ_INSTS_VALU", reps=2)
+    # the command-line tool exits non-zero on such a file
+    p = str(tmp_path / "c.csv")
+    _pmc_csv(p, [(0, "render_fwd_kernel<32, 0>", "SQ_INSTS_VALU", 0.0)] + good)
+    r = subprocess.run([sys.executable, "pmc_generic.py", "27", p], cwd=os.path.join(ROOT, "tools"),
+                       capture_output=True, text=True)
+    assert r.returncode != 0 and "UnevenLaunches" in r.stderr, r.stdout + r.stderr
+    _pmc_csv(p, good)
+    r = subprocess.run([sys.executable, "pmc_generic.py", "1", p], cwd=os.path.join(ROOT, "tools"),
+                       capture_output=True, text=True)
+    assert r.returncode == 0 and json.loads(r.stdout)["kernels"]["render_fwd"]["SQ_INSTS_VALU"] == 905, r.stderr

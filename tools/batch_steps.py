@@ -5,6 +5,13 @@ rocprofv3 --pmc runs to count the bench's kernels per launch (one launch = all
 27 cameras).
 
     rocprofv3 --pmc FETCH_SIZE -- python3 tools/batch_steps.py --reps 2
+
+Every rep is one launch per stage of the same work: the forward is the
+two-phase plan -> render (sync_free=False; the sync-free forward's first call
+renders every camera empty and retries, which would add a launch of no work
+to the counts -- tools/pmc_*.py refuse such files).  --sync-free runs the
+sync-free forward after one warm call, for timing and stamps only (the warm
+call's launches would be counted too).
 """
 from __future__ import annotations
 
@@ -31,6 +38,7 @@ def main():
     ap.add_argument("--features", type=int, default=32)
     ap.add_argument("--size", type=int, default=800)
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--sync-free", action="store_true", help="the sync-free forward (one warm call first)")
     ap.add_argument("--stamps", action="store_true", help="read the stamps build's wave-lifetime shares")
     ap.add_argument("--dump-stamps", default="", help="with --stamps: save the raw per-wave stamps (npz)")
     a = ap.parse_args()
@@ -44,7 +52,7 @@ def main():
         viewmatrix=torch.from_numpy(c.viewmatrix.copy()).to(dev),
         projmatrix=torch.from_numpy(c.projmatrix.copy()).to(dev), sh_degree=0,
         campos=torch.from_numpy(c.campos.copy()).to(dev), compat="reference") for c in camera_rig(a.cams, W, H)]
-    ras = GaussianRasterizerBatch(sets)
+    ras = GaussianRasterizerBatch(sets, sync_free=a.sync_free)
     gen = torch.Generator(device=dev).manual_seed(1)
     C = a.cams
     up = [torch.randn(C, 3, H, W, device=dev, generator=gen), torch.randn(C, 1, H, W, device=dev, generator=gen)]
@@ -62,7 +70,7 @@ def main():
         L.gs_stamps_set.argtypes = [ctypes.c_void_p, ctypes.c_longlong]
         assert L.gs_stamps_set(ctypes.c_void_p(buf.data_ptr()), nf) == 0
         stamps = (buf, nf)
-    for _ in range(a.reps):
+    for rep in range(a.reps + (1 if a.sync_free else 0)):
         kw = dict(means3D=leaves["means3D"], means2D=torch.zeros(a.gaussians, 3, device=dev),
                   opacities=leaves["opacities"], colors_precomp=leaves["colors"], scales=leaves["scales"],
                   rotations=leaves["rotations"], label=label)
@@ -73,6 +81,10 @@ def main():
             im, radius, depth, _ = ras(**kw)
             torch.autograd.backward([im, depth], up)
     torch.cuda.synchronize()
+    if ras.plan is not None:
+        # the counted reps after the warm call rendered every camera once
+        print(f"sync-free retries: {ras.plan.retries} over {ras.plan.calls} calls", flush=True)
+        assert ras.plan.retries == 0, "a counted rep was rendered twice (binning capacity retry)"
     if a.stamps:
         import json
         st = stamps[0].cpu().numpy().reshape(-1, 8).astype(np.float64)

@@ -12,17 +12,23 @@ is heavy-tailed; a systematic error (a wrong exchange, a lost slice) moves
 most elements and shows in the trimmed mean.  The floor is the largest
 trimmed mean over the reference pairs.
 
+OK iff, for every tensor, the tested run's trimmed mean <= max(3 x floor,
+1e-9).  The plain mean and max are printed beside it.
+
 A run now and then (one gloo rehearsal run in six, the plain reference path
 included) lands far above the floor on every tensor at once: the atomic
 order's noise amplified through one early discrete event across the whole
-scene over the run's training steps.  An exchange error is different in
-kind -- a lost, doubled or stale contribution moves every element by the
-order of its learning rate per step -- so the bound is also scaled by it:
-OK iff, for every tensor, the tested run's trimmed mean <=
-max(3 x floor, 1e-3 x lr, 1e-9) (bench.py's learning rates, train.py:119-135).
-The plain mean and max are printed beside it.
+scene over the run's training steps.  An after-training comparison cannot
+tell that apart from a race, so the exchange's race check is step-level
+(tools/zov_check.py: each step's gradients against a replay from the
+parameters it read, the parameters read against an in-line Adam replay of
+the summed gradients, bit for bit).  `--lr-bound` (opt-in, for rehearsals
+whose step-level check has passed) also accepts a trimmed mean up to 1e-3 x
+the tensor's learning rate (bench.py's, train.py:119-135): an exchange error
+-- a lost, doubled or stale contribution -- moves every element by the order
+of its learning rate per step.
 
-    python tools/compare_params.py test.npz ref.npz ref_repeat.npz [ref_repeat2.npz ...]
+    python tools/compare_params.py [--lr-bound] test.npz ref.npz ref_repeat.npz [ref_repeat2.npz ...]
 """
 import json
 import sys
@@ -42,8 +48,11 @@ def trimmed_mean(d):
 
 
 def main():
-    t, a = np.load(sys.argv[1]), np.load(sys.argv[2])
-    reps = [np.load(p) for p in sys.argv[3:]]
+    argv = sys.argv[1:]
+    lr_bound = "--lr-bound" in argv
+    argv = [x for x in argv if x != "--lr-bound"]
+    t, a = np.load(argv[0]), np.load(argv[1])
+    reps = [np.load(p) for p in argv[2:]]
     if not reps:
         raise SystemExit("need at least one repeat of the reference")
     out, ok = {}, True
@@ -55,7 +64,7 @@ def main():
         out[k] = {"trimmed_mean": trimmed_mean(d), "floor_trimmed_mean": fl, "mean": float(d.mean()),
                   "max": float(d.max()), "floor_mean": max(float(f.mean()) for f in floors),
                   "floor_max": max(float(f.max()) for f in floors)}
-        bound = max(3 * fl, 1e-3 * LR.get(k, 0.0), 1e-9)
+        bound = max(3 * fl, 1e-3 * LR.get(k, 0.0) if lr_bound else 0.0, 1e-9)
         out[k]["bound"] = bound
         ok &= out[k]["trimmed_mean"] <= bound
     print(json.dumps(out, indent=1))

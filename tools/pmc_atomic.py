@@ -6,27 +6,22 @@ profiles/pmc_atomic.json for bench.py's roofline.atomics view.
 
     python tools/pmc_atomic.py ATOMIC_counter_collection.csv [CAMS]
 """
-import collections
 import csv
 import json
 import os
 import sys
 
+from pmc_traffic import per_rep
+
 KERNELS = {"render_bwd": "render_bwd", "render_fwd": "render_fwd", "preprocess_bwd": "preprocess_bwd"}
 
 
 def main():
-    tot = collections.defaultdict(float)
-    disp = collections.defaultdict(set)
-    for r in csv.DictReader(open(sys.argv[1])):
-        if not r["Counter_Name"].startswith("TCC_EA0_ATOMIC"):
-            continue
-        for key, stage in KERNELS.items():
-            if key in r["Kernel_Name"]:
-                tot[stage] += float(r["Counter_Value"])
-                disp[stage].add(r["Dispatch_Id"])
+    with open(sys.argv[1]) as f:
+        tot = {stage: v for (stage, _), v in per_rep(csv.DictReader(f), lambda c: c.startswith("TCC_EA0_ATOMIC"),
+                                                     stages=KERNELS).items()}
     cams = int(sys.argv[2]) if len(sys.argv) > 2 else 1
-    out = {"requests_per_camera": {k: int(tot[k] / len(disp[k]) / cams) for k in tot},
+    out = {"requests_per_camera": {k: int(tot[k] / cams) for k in tot},
            "bytes_per_request": 64, "cams_per_launch": cams,
            "method": "rocprofv3 --pmc TCC_EA0_ATOMIC_sum on tools/batch_steps.py (27-camera launches), "
                      "per launch / cameras per launch"}

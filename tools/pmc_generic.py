@@ -10,20 +10,19 @@ import csv
 import json
 import sys
 
-from pmc_traffic import STAGE_OF
+from pmc_traffic import per_rep
 
 
 def main():
     cams = int(sys.argv[1])
-    tot = collections.defaultdict(lambda: collections.defaultdict(float))
-    disp = collections.defaultdict(lambda: collections.defaultdict(set))
+    tot = collections.defaultdict(dict)
     for path in sys.argv[2:]:
-        for r in csv.DictReader(open(path)):
-            for key in STAGE_OF:
-                if key in r["Kernel_Name"]:
-                    tot[key][r["Counter_Name"]] += float(r["Counter_Value"])
-                    disp[key][r["Counter_Name"]].add(r["Dispatch_Id"])
-    out = {k: {c: round(v / len(disp[k][c]) / cams) for c, v in sorted(d.items())} for k, d in tot.items()}
+        with open(path) as f:
+            rows = list(csv.DictReader(f))
+        for c in sorted({r["Counter_Name"] for r in rows}):
+            for (_, key), v in per_rep(rows, c).items():  # refuses uneven launches
+                tot[key][c] = v
+    out = {k: {c: round(v / cams) for c, v in sorted(d.items())} for k, d in tot.items()}
     print(json.dumps({"per": "camera", "cams_per_launch": cams, "kernels": out}, indent=1))
 
 

@@ -21,18 +21,56 @@ STAGE_OF = {"preprocess_fwd": "preprocess", "tile_hist_kernel<false>": "scan", "
             "render_fwd": "render_fwd", "render_bwd": "render_bwd", "preprocess_bwd": "preprocess_bwd"}
 
 
-def per_kernel(path, counter):
-    tot = collections.defaultdict(float)
-    disp = collections.defaultdict(set)
-    for r in csv.DictReader(open(path)):
-        if r["Counter_Name"] != counter:
+# The counted program runs the same batch forward + backward REPS times
+# (tools/batch_steps.py --reps, two-phase forward): every kernel's dispatches
+# fall into REPS equal groups of equal work.  A group count that does not
+# divide, or a group with less work than the others (e.g. a sync-free
+# forward's first call, which renders every camera empty and retries), means
+# the counts are not of the workload they claim, and the tools refuse them.
+REPS = int(os.environ.get("PMC_REPS", "2"))
+TOL = float(os.environ.get("PMC_TOL", "0.2"))
+
+
+class UnevenLaunches(ValueError):
+    """A kernel's dispatches do not split into equal reps of equal work."""
+
+
+def per_rep(rows, counter, reps=None, tol=None, stages=None):
+    """{(stage, kernel key): counter sum per rep} over csv rows (dicts) whose
+    Counter_Name satisfies `counter` (a name or a predicate); raises
+    UnevenLaunches when a kernel's dispatches are not `reps` groups (in
+    dispatch order) of equal work within `tol`."""
+    reps = REPS if reps is None else int(reps)
+    tol = TOL if tol is None else float(tol)
+    stages = STAGE_OF if stages is None else stages
+    match = counter if callable(counter) else (lambda c: c == counter)
+    vals = collections.defaultdict(lambda: collections.defaultdict(float))
+    for r in rows:
+        if not match(r["Counter_Name"]):
             continue
         name = r["Kernel_Name"]
-        for key, stage in STAGE_OF.items():
+        for key, stage in stages.items():
             if key in name:
-                tot[(stage, key)] += float(r["Counter_Value"])
-                disp[(stage, key)].add(r["Dispatch_Id"])
-    return {k: tot[k] / len(disp[k]) for k in tot}
+                vals[(stage, key)][int(r["Dispatch_Id"])] += float(r["Counter_Value"])
+    out = {}
+    for k, d in vals.items():
+        ids = sorted(d)
+        if len(ids) % reps:
+            raise UnevenLaunches(f"{k[1]}: {len(ids)} dispatches for {reps} reps (a retried or extra launch)")
+        m = len(ids) // reps
+        sums = [sum(d[i] for i in ids[j * m:(j + 1) * m]) for j in range(reps)]
+        hi = max(sums)
+        if hi > 0 and min(sums) < (1.0 - tol) * hi:
+            raise UnevenLaunches(f"{k[1]}: per-rep work {[round(x) for x in sums]} differs by more than "
+                                 f"{tol:.0%} (an empty or partial launch)")
+        out[k] = sum(sums) / reps
+    return out
+
+
+def per_kernel(path, counter):
+    """Per rep (= per launch of each stage) sums of one counter."""
+    with open(path) as f:
+        return per_rep(csv.DictReader(f), counter)
 
 
 def main():

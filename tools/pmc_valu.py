@@ -8,22 +8,22 @@ import json
 import os
 import sys
 
-from pmc_traffic import STAGE_OF
+from pmc_traffic import per_rep
 
 
 def main():
-    tot = collections.defaultdict(lambda: collections.defaultdict(float))
-    disp = collections.defaultdict(set)
-    for r in csv.DictReader(open(sys.argv[1])):
-        for key, stage in STAGE_OF.items():
-            if key in r["Kernel_Name"]:
-                tot[key][r["Counter_Name"]] += float(r["Counter_Value"])
-                disp[key].add(r["Dispatch_Id"])
+    with open(sys.argv[1]) as f:
+        rows = list(csv.DictReader(f))
+    tot = collections.defaultdict(dict)
+    for c in sorted({r["Counter_Name"] for r in rows}):
+        for (_, key), v in per_rep(rows, c).items():  # refuses uneven launches
+            tot[key][c] = v
     cams = int(sys.argv[2]) if len(sys.argv) > 2 else 1
-    out = {"kernels": {k: {c: round(v / len(disp[k]) / cams) for c, v in d.items()} for k, d in tot.items()},
+    out = {"kernels": {k: {c: round(v / cams) for c, v in d.items()} for k, d in tot.items()},
            "per": "camera", "cams_per_launch": cams,
-           "method": "rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_SALU SQ_WAVES; per launch / cameras "
-                     f"per launch; tools/batch_steps.py ({cams} cameras per launch)"}
+           "method": "rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_SALU SQ_WAVES; per rep (one launch "
+                     f"per stage) / cameras per launch; tools/batch_steps.py ({cams} cameras per launch, "
+                     "two-phase forward, reps checked equal: pmc_traffic.per_rep)"}
     wl = os.environ.get("PMC_WORKLOAD")
     if wl:
         out["workload"] = json.loads(wl)
