@@ -21,7 +21,9 @@ def main():
             name = r["Kernel_Name"].split("(")[0].replace("void ", "")
             c = r["Counter_Name"]
             tot[name][c] += float(r["Counter_Value"])
-            disp[name][c].add(r["Dispatch_Id"])
+            # dispatch ids restart in every profiled process: a counter
+            # collected in two passes has twice the launches
+            disp[name][c].add((path, r["Dispatch_Id"]))
     out = {}
     for name, d in sorted(tot.items()):
         per = {c: v / max(1, len(disp[name][c])) for c, v in d.items()}
