@@ -370,6 +370,73 @@ __device__ inline Acc mfma_exact_split(const bf16x8& a, const bsplit& b, Acc c) 
   return c;
 }
 
+// ------------------------------------------------------------------ fp16 split products
+// The same contraction on the fp16 matrix cores (the bf16 rate) for operands
+// whose range is known: fp16 keeps 11 significant bits, so TWO pieces carry
+// an operand to 22-24 bits (x = h0 + h1 + r, h0 the fp16 rounding of x, h1
+// of x - h0; |r| <= 2^-24 |x| while x - h0 is a normal fp16) and a product
+// a*b is summed as h0 g0 + h0 g1 + h1 g0 (3 matrix instructions instead of
+// the bf16 split's 6; the dropped h1 g1 and remainders are ~3 * 2^-24 |ab|,
+// fp32's own rounding of a product), each piece product exact in fp32.
+// Range: an operand is scaled by a power of two into [2^-3, 2^16) wherever
+// its size allows (exact, undone on the fp32 sums), so h0 stays normal and
+// h1 exact; fp16 subnormals pass the conversions and the matrix inputs
+// unflushed (MODE.denorm, hipcc's default), so smaller values lose relative
+// precision only below 2^-24 of the operand's scale in absolute terms.
+// Per 8 values: 4 v_cvt_pk_f16_f32 + 8 v_fma_mix_f32 (the remainder x - h0
+// read straight from the packed half, negated, in one instruction) + 4
+// v_cvt_pk_f16_f32 = 2 vector instructions per value (the 3-piece bf16
+// split: 5.5).
+constexpr int NSH = 2;
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+struct hsplit {
+  f16x8 p[NSH];
+};
+__device__ inline float4_t mfma_f16(const f16x8& a, const f16x8& b, float4_t c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+__device__ inline uint32_t cvt_pk_f16(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, f16x2));
+}
+// a - (the fp16 in the low / high half of u), exact, one v_fma_mix_f32
+__device__ inline float f16_rem_lo(float a, uint32_t u) {
+  float r;
+  asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(u), "v"(a));
+  return r;
+}
+__device__ inline float f16_rem_hi(float a, uint32_t u) {
+  float r;
+  asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(u), "v"(a));
+  return r;
+}
+__device__ inline void split_f16(const float (&x)[8], hsplit& s) {
+  u32x4 w0, w1;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t u = cvt_pk_f16(x[2 * j], x[2 * j + 1]);
+    w0[j] = u;
+    w1[j] = cvt_pk_f16(f16_rem_lo(x[2 * j], u), f16_rem_hi(x[2 * j + 1], u));
+  }
+  s.p[0] = __builtin_bit_cast(f16x8, w0);
+  s.p[1] = __builtin_bit_cast(f16x8, w1);
+}
+// c += a * b over the pieces (h1 g0 and h0 g1 first, then h0 g0)
+__device__ inline float4_t mfma_hsplit(const hsplit& a, const hsplit& b, float4_t c) {
+  c = mfma_f16(a.p[1], b.p[0], c);
+  c = mfma_f16(a.p[0], b.p[1], c);
+  return mfma_f16(a.p[0], b.p[0], c);
+}
+// The power of two that scales a row whose largest magnitude is m into
+// [2^14, 2^15) (0 for an all-zero row; bounded so that its inverse stays a
+// normal fp32 together with the weights' scale).
+__device__ inline int row_scale_exp(float m) {
+  if (!(m > 0.f)) return 0;
+  const int e = __builtin_amdgcn_frexp_expf(m);  // m = f 2^e, f in [0.5, 1)
+  const int s = 15 - e;
+  return s < -100 ? -100 : (s > 100 ? 100 : s);
+}
+
 // ------------------------------------------------------------------ forward
 
 // Waves per SIMD the forward asks the register allocator for: 4 for the
@@ -865,7 +932,16 @@ __global__ __launch_bounds__(64 * WPB_BWD) __attribute__((amdgpu_waves_per_eu(bw
   // colour sums hold copies nobody reads.
   constexpr bool XW_LDS = (FW <= 4);
   constexpr int XR = FW == 0 ? 4 : 8;  // operand rows kept
-  __shared__ bf16x8 s_xw[WPB_BWD][XW_LDS ? 2 : 1][NSP][XR][4];
+  __shared__ f16x8 s_xw[WPB_BWD][XW_LDS ? 2 : 1][NSH][XR][4];
+  // per colour-block row: the factor that undoes its scale and the weights'
+  __shared__ __attribute__((aligned(16))) float s_rsc[WPB_BWD][16];
+  // The weights w = alpha T enter the fp16 contractions scaled by 2^W_EXP:
+  // reference mode walks back from T_final = 1 (Q1), so T <= 1e4 (the
+  // forward stops before T < 1e-4) and w in [1/255, 9.9e3] -> x4; fixed
+  // mode T <= 1, w in [3.9e-7, 0.99] -> x2^15.  The scale rides on T itself
+  // (T, w, dL/dopacity and u all carry it exactly; undone on the sums).
+  constexpr int W_EXP = COMPAT == COMPAT_REFERENCE ? 2 : 15;
+  constexpr float W_SCALE = (float)(1 << W_EXP);
   // batch weights w ([0]) and u ([1]) as [slot][pixel]: 64-float rows, 16-B
   // groups XOR-swizzled by the row (sw_idx) so that the flush's 16-row operand
   // reads and the per-lane writes are both conflict-free without padding; one
@@ -896,7 +972,7 @@ __global__ __launch_bounds__(64 * WPB_BWD) __attribute__((amdgpu_waves_per_eu(bw
   FINE_STAMP(tA);
 #endif
   const float T_final = inside ? 1 - alphas[pix] : 0.0f;
-  float T = T_final;
+  float T = T_final * W_SCALE;  // scaled (W_EXP)
   const uint32_t last = inside ? n_contrib[pix] : 0u;
   float dLp[3];
   // absent upstream gradients (NULL) are zeros
@@ -906,7 +982,7 @@ __global__ __launch_bounds__(64 * WPB_BWD) __attribute__((amdgpu_waves_per_eu(bw
   const float dLd = inside && dL_ddepth ? dL_ddepth[pix] : 0.f;
   const float dLa = inside && dL_dalpha ? dL_dalpha[pix] : 0.f;
   const float bg_dot = bg[0] * dLp[0] + bg[1] * dLp[1] + bg[2] * dLp[2];
-  const float tf_bg = T_final * bg_dot;  // the background term's per-pixel factor (exact in reference mode: T_final = 1)
+  const float tf_bg = (T_final * W_SCALE) * bg_dot;  // the background term's per-pixel factor, scaled like T
   float dLf_own[FIXED_FEAT ? F : 1];  // fixed mode: f . dL/dF feeds dL/dalpha
   if constexpr (FIXED_FEAT) {
 #pragma unroll
@@ -922,34 +998,28 @@ __global__ __launch_bounds__(64 * WPB_BWD) __attribute__((amdgpu_waves_per_eu(bw
   // strip row: column p % STRIP_W, row p / STRIP_W):
   //   Xw: row l&15 of the colour block: 0..2 dL/dC, 3 dL/dD, 4.. dL/dF (F < 16)
   //   Bf: dL/dF[p][16cb + (l&15)] (F >= 16; B operand of the feature blocks)
-  bsplit Xw[XW_LDS ? 1 : 2];
-  bsplit Bf[CB1][2];
+  // Both are fp16 two-piece splits (they meet the weights w in the fp16
+  // contractions), each row scaled by its own power of two (row_scale_exp of
+  // the row's largest magnitude over the strip's 64 pixels: the row's 16
+  // values in each of the 4 lanes l, l^16, l^32, l^48); fmul / s_rsc undo
+  // the row's scale and the weights' on the sums.
+  hsplit Xw[XW_LDS ? 1 : 2];
+  hsplit Bf[CB1][2];
+  float fmul[CB1];
   const int kp0 = 8 * (lane >> 4);  // first strip pixel of the lane at k-step 0
-  // the colour block operand of k-step s: into LDS (rows 0..3) or registers
-  auto store_xw = [&](const float (&x)[8], int s) {
-    if constexpr (XW_LDS) {
-      bsplit t;
-      split_bf16(x, t);
-      if ((lane & 15) < XR) {
-#pragma unroll
-        for (int i = 0; i < NSP; ++i) s_xw[lw][s][i][lane & 15][lane >> 4] = t.p[i];
-      }
-    } else {
-      split_bf16(x, Xw[s]);
-    }
-  };
   {
     const int row = lane & 15;
     const float* src = nullptr;
     if (row < 3) src = dL_dpix ? dL_dpix + (size_t)row * HW : nullptr;
     else if (row == 3) src = dL_ddepth;
     else if (row - 4 < FW) src = dL_dfeat ? dL_dfeat + (size_t)(16 * CB + row - 4) * HW : nullptr;
+    float xv[2][8], fv[CB1][2][8];
     // A lane's 8 pixels are one run of a strip row.  Fast path (the strip
     // lies inside the image, rows and planes 16-B aligned -- decided once per
     // wave): every operand row with two 16-B loads, all issued back to back
-    // and split after (a per-row branch made the compiler wait for each row
-    // before issuing the next).  Absent planes read the alpha image and are
-    // zeroed after.  Slow path: per-pixel loads with bounds.
+    // (a per-row branch made the compiler wait for each row before issuing
+    // the next).  Absent planes read the alpha image and are zeroed after.
+    // Slow path: per-pixel loads with bounds.
     const float* fplane0 = dL_dfeat ? dL_dfeat + (size_t)row * HW : nullptr;
     const bool lane_ok = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(fplane0) |
                            reinterpret_cast<uintptr_t>(alphas)) & 15) == 0;
@@ -977,34 +1047,67 @@ __global__ __launch_bounds__(64 * WPB_BWD) __attribute__((amdgpu_waves_per_eu(bw
       };
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        float x[8];
-        unpack(rw[s], src != nullptr, x);
-        store_xw(x, s);
+        unpack(rw[s], src != nullptr, xv[s]);
 #pragma unroll
-        for (int cb = 0; cb < CB; ++cb) {
-          unpack(rf[cb][s], fplane0 != nullptr, x);
-          split_bf16(x, Bf[cb][s]);
-        }
+        for (int cb = 0; cb < CB; ++cb) unpack(rf[cb][s], fplane0 != nullptr, fv[cb][s]);
       }
     } else {
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const int p8 = 32 * s + kp0;
         const int qy = qy0 + p8 / STRIP_W, qx = qx0 + p8 % STRIP_W;
-        float xw[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) xw[j] = (src && qx + j < W && qy < H) ? src[(size_t)qy * W + qx + j] : 0.f;
-        store_xw(xw, s);
+        for (int j = 0; j < 8; ++j) xv[s][j] = (src && qx + j < W && qy < H) ? src[(size_t)qy * W + qx + j] : 0.f;
 #pragma unroll
         for (int cb = 0; cb < CB; ++cb) {
           const float* fsrc = fplane0 ? fplane0 + (size_t)(16 * cb) * HW : nullptr;
-          float xf[8];
 #pragma unroll
-          for (int j = 0; j < 8; ++j) xf[j] = (fsrc && qx + j < W && qy < H) ? fsrc[(size_t)qy * W + qx + j] : 0.f;
-          split_bf16(xf, Bf[cb][s]);
+          for (int j = 0; j < 8; ++j)
+            fv[cb][s][j] = (fsrc && qx + j < W && qy < H) ? fsrc[(size_t)qy * W + qx + j] : 0.f;
         }
       }
     }
+    // scale each row into [2^14, 2^15) by a power of two (exact), split
+    auto scale_row = [&](float (&v)[2][8]) -> int {
+      float m = 0.f;
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(v[s][j]));
+      m = fmaxf(m, __shfl_xor(m, 16, 64));
+      m = fmaxf(m, __shfl_xor(m, 32, 64));
+      const int e = row_scale_exp(m);
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[s][j] = ldexpf(v[s][j], e);
+      return e;
+    };
+    {
+      const int e = scale_row(xv);
+      if (lane < 16) s_rsc[lw][lane] = ldexpf(1.f, -e - W_EXP);
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        if constexpr (XW_LDS) {
+          hsplit t;
+          split_f16(xv[s], t);
+          if ((lane & 15) < XR) {
+#pragma unroll
+            for (int i = 0; i < NSH; ++i) s_xw[lw][s][i][lane & 15][lane >> 4] = t.p[i];
+          }
+        } else {
+          split_f16(xv[s], Xw[s]);
+        }
+      }
+    }
+#pragma unroll
+    for (int cb = 0; cb < CB; ++cb) {
+      const int e = scale_row(fv[cb]);
+      fmul[cb] = ldexpf(1.f, -e - W_EXP);
+#pragma unroll
+      for (int s = 0; s < 2; ++s) split_f16(fv[cb][s], Bf[cb][s]);
+    }
+    if constexpr (CB == 0) fmul[0] = 0.f;
   }
 
 #ifdef GS_STAMPS
@@ -1046,25 +1149,25 @@ __global__ __launch_bounds__(64 * WPB_BWD) __attribute__((amdgpu_waves_per_eu(bw
     for (int s = 0; s < NKS; ++s) {
       const int p0 = 32 * s + 8 * (lane >> 4);
       {
-        // the weights w: colour block and features
-        bsplit Ws;
+        // the weights w (scaled by 2^W_EXP): colour block and features, fp16
+        hsplit Ws;
         {
           float x[8];
           const float4 a0 = *reinterpret_cast<const float4*>(&s_wu[lw][0][sw_idx(g, p0)]);
           const float4 a1 = *reinterpret_cast<const float4*>(&s_wu[lw][0][sw_idx(g, p0 + 4)]);
           x[0] = a0.x; x[1] = a0.y; x[2] = a0.z; x[3] = a0.w; x[4] = a1.x; x[5] = a1.y; x[6] = a1.z; x[7] = a1.w;
-          split_bf16(x, Ws);
+          split_f16(x, Ws);
         }
         if constexpr (XW_LDS) {
-          bsplit xw;
+          hsplit xw;
 #pragma unroll
-          for (int i = 0; i < NSP; ++i) xw.p[i] = s_xw[lw][s][i][lane & (XR - 1)][(lane >> 4) & 3];
-          cw = mfma_split(xw, Ws, cw);
+          for (int i = 0; i < NSH; ++i) xw.p[i] = s_xw[lw][s][i][lane & (XR - 1)][(lane >> 4) & 3];
+          cw = mfma_hsplit(xw, Ws, cw);
         } else {
-          cw = mfma_split(Xw[s], Ws, cw);
+          cw = mfma_hsplit(Xw[s], Ws, cw);
         }
 #pragma unroll
-        for (int cb = 0; cb < CB; ++cb) cf[cb] = mfma_split(Ws, Bf[cb][s], cf[cb]);
+        for (int cb = 0; cb < CB; ++cb) cf[cb] = mfma_hsplit(Ws, Bf[cb][s], cf[cb]);
       }
       // the weights u: geometry rows, the monomials 1, X, Y, X^2, XY, Y^2 of
       // the lane's pixels (X = 2 (px - cx) = 2 col - (STRIP_W - 1),
@@ -1101,6 +1204,18 @@ __global__ __launch_bounds__(64 * WPB_BWD) __attribute__((amdgpu_waves_per_eu(bw
         xu = __builtin_bit_cast(bf16x8, xw);
       }
       cu = mfma_exact_split(xu, Us, cu);
+    }
+    // undo the scales: colour-block row (l>>4)*4 + r (its row's and the
+    // weights'), feature channel l&15 (fmul), the weights' on u
+    {
+      const float4 rs = *reinterpret_cast<const float4*>(&s_rsc[lw][(lane >> 4) * 4]);
+      cw[0] *= rs.x;
+      cw[1] *= rs.y;
+      cw[2] *= rs.z;
+      cw[3] *= rs.w;
+#pragma unroll
+      for (int cb = 0; cb < CB; ++cb) cf[cb] *= fmul[cb];
+      cu *= 1.0f / W_SCALE;
     }
     // lane l < 16 holds rows 0..3 of slot l; rows 4, 5 of cu come from lane l + 16
     const float s_xy = __shfl_down(cu[0], 16, 64);

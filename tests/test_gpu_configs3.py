@@ -83,7 +83,8 @@ def test_eight_rank_driver_step_matches_per_camera_autograd():
     for r in range(WORLD):
         params = {k: torch.nn.Parameter(v.clone()) for k, v in base.items()}
         opt = torch.optim.SGD([{"params": [params[k]], "name": k, "lr": 0.0} for k in params], lr=0.0)
-        drv = TimestepDriver(params, {}, opt, C, render, rank=r, world=WORLD)
+        # the plain bucket path (its bound .grad views are what this test sums)
+        drv = TimestepDriver(params, {}, opt, C, render, rank=r, world=WORLD, sharded=False)
         assert len(drv.cams) in (3, 4)
         loss += drv.step(tg)
         for k in tot:
