@@ -590,12 +590,18 @@ static int render_impl(const gs_gaussians* g, const gs_camera* cams, int C, int 
   ra.bg = cams[0].background;
   ra.out_color = out_color; ra.out_feature = out_feature; ra.out_depth = out_depth; ra.out_alpha = out_alpha;
   ra.n_contrib = at<uint32_t>(image, il.n_contrib);
+  ra.fmax = at<uint32_t>(image, il.fmax);
   if (g->feature_ready) {
     const hipError_t e = hipStreamWaitEvent(s, (hipEvent_t)g->feature_ready, 0);
     if (e != hipSuccess) return fail((int)e, "waiting for feature_ready: %s", hipGetErrorString(e));
   }
   {
-    StageTimer t(s, GS_STAGE_RENDER_FWD, true);
+    // the matrix-core widths first take the features' per-channel range
+    // (after the wait: the features may just have been updated); the stage
+    // then holds both launches
+    const bool mf = g->F >= 32;
+    StageTimer t(s, GS_STAGE_RENDER_FWD, !mf);
+    if (mf) launch_feature_absmax(g->semantic_feature, g->P, g->F, at<uint32_t>(image, il.fmax), s);
     if (!launch_render_fwd(ra, cb, s)) return fail(-1, "unsupported feature width %d", g->F);
   }
   return check("render", debug, s);

@@ -137,7 +137,7 @@ struct SortLayout {
 // histograms (turned into per-block offsets), tile totals and the 8-word
 // header (gs_meta.h).
 struct ImgLayout {
-  size_t ranges, n_contrib, thist, ttotal, bsum, meta, order, smax, total;
+  size_t ranges, n_contrib, thist, ttotal, bsum, meta, order, smax, fmax, total;
   int64_t tiles;
   __host__ __device__ ImgLayout(int W, int H) {
     tiles = (int64_t)((W + TILE - 1) / TILE) * ((H + TILE - 1) / TILE);
@@ -153,6 +153,9 @@ struct ImgLayout {
     // 16-B load gives a blend workgroup its tile and list
     order = o;     o = align_up(o + sizeof(uint32_t) * 4 * t, 256);
     smax = o;      o = align_up(o + sizeof(uint32_t) * 4 * t, 256);  // per strip item: longest pixel walk (forward -> backward)
+    // per feature channel (F <= 64): the largest |feature| as float bits, for
+    // the forward's fp16 feature contraction (camera 0's buffer of a batch)
+    fmax = o;      o = align_up(o + sizeof(uint32_t) * 64, 256);
     total = o;
   }
 };

@@ -82,6 +82,9 @@ struct RenderArgs {
   float* out_depth;
   float* out_alpha;
   uint32_t* n_contrib;
+  // F >= 32: per channel the largest |feature| of the table (float bits,
+  // launch_feature_absmax; the whole batch's, camera 0's image buffer)
+  const uint32_t* fmax;
 };
 
 // Row stride (floats) of the feature gradients the backward blend adds into:
@@ -93,6 +96,9 @@ __host__ __device__ constexpr int feature_grad_stride(int F) {
   return (F < 16 || F % 16 == 0) ? F : (F + 15) / 16 * 16;
 }
 void launch_feature_grad_rows(const float* pad, float* out, int64_t P, int F, int accumulate, hipStream_t s);
+// out[c] = bits of max_g |feats[g][c]| (c < F <= 64), zeroed first: the
+// scales of the forward's fp16 feature contraction (render_fwd, F >= 32)
+void launch_feature_absmax(const float* feats, int64_t P, int F, uint32_t* out, hipStream_t s);
 
 struct RenderBwdArgs {
   int W, H, grid_x, num_tiles, F, compat, P;

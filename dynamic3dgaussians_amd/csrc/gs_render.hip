@@ -427,6 +427,22 @@ __device__ inline float4_t mfma_hsplit(const hsplit& a, const hsplit& b, float4_
   c = mfma_f16(a.p[0], b.p[1], c);
   return mfma_f16(a.p[0], b.p[0], c);
 }
+__device__ inline f32x16 mfma_f16(const f16x8& a, const f16x8& b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+// c += a * x with x split here (its two pieces made one after the other):
+// h1 g0 first, then h0 g1, h0 g0
+__device__ inline f32x16 mfma_hsplit_x(const hsplit& a, const float (&x)[8], f32x16 c) {
+  u32x4 w0, w1;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) w0[j] = cvt_pk_f16(x[2 * j], x[2 * j + 1]);
+  const f16x8 b0 = __builtin_bit_cast(f16x8, w0);
+  c = mfma_f16(a.p[1], b0, c);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) w1[j] = cvt_pk_f16(f16_rem_lo(x[2 * j], w0[j]), f16_rem_hi(x[2 * j + 1], w0[j]));
+  c = mfma_f16(a.p[0], __builtin_bit_cast(f16x8, w1), c);
+  return mfma_f16(a.p[0], b0, c);
+}
 // The power of two that scales a row whose largest magnitude is m into
 // [2^14, 2^15) (0 for an all-zero row; bounded so that its inverse stays a
 // normal fp32 together with the weights' scale).
@@ -552,6 +568,12 @@ __global__ __launch_bounds__(64 * WPB_FWD) __attribute__((amdgpu_waves_per_eu(fw
   // pointer arithmetic per row cost 3 more vector instructions per row and
   // spilled registers at the 128-VGPR cap
   const uint64_t fbytes = (uint64_t)ca.P * F * 4u;
+  // fp16 feature contraction: the weights w = alpha T in [3.9e-7, 0.99]
+  // (T >= 1e-4, alpha >= 1/255) enter scaled by 2^15, the features by their
+  // channel's power of two (fmax); acc holds both scales until the stores
+  constexpr int FW_EXP = 15;
+  constexpr float FW_SCALE = (float)(1 << FW_EXP);
+  const uint32_t* __restrict__ fmax = ca.fmax;
   const auto frsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(feats), (short)0,
                                                        (int)(uint32_t)clamp_u32(fbytes), 0x00020000);
   auto flush = [&](int n) {
@@ -565,8 +587,10 @@ __global__ __launch_bounds__(64 * WPB_FWD) __attribute__((amdgpu_waves_per_eu(fw
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
     for (int fb = 0; fb < FB; ++fb) {
-      bsplit A;
+      hsplit A;
       {
+        // the channel's scale (its largest |feature| into [2^14, 2^15))
+        const float fs = ldexpf(1.f, row_scale_exp(__uint_as_float(fmax[fb * 32 + (ln & 31)])));
         float fa[8];
         // 32-bit row offsets through a buffer resource: one address
         // instruction per row instead of 64-bit pointer arithmetic
@@ -579,9 +603,9 @@ __global__ __launch_bounds__(64 * WPB_FWD) __attribute__((amdgpu_waves_per_eu(fw
           const uint32_t g = gk[j];
           const uint32_t off = (g * (uint32_t)F + (uint32_t)(fb * 32 + (ln & 31))) * 4u;
           const float v = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(frsrc, (int)off, 0, 0));
-          fa[j] = k < n ? v : 0.f;
+          fa[j] = k < n ? v * fs : 0.f;
         }
-        split_bf16(fa, A);
+        split_f16(fa, A);
       }
 #pragma unroll
       for (int blk = 0; blk < 2; ++blk) {
@@ -589,9 +613,9 @@ __global__ __launch_bounds__(64 * WPB_FWD) __attribute__((amdgpu_waves_per_eu(fw
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int k = 8 * h + j;
-          x[j] = k < n ? s_fw[lw][k][(ln & 31) + 32 * blk] : 0.f;
+          x[j] = k < n ? s_fw[lw][k][(ln & 31) + 32 * blk] * FW_SCALE : 0.f;
         }
-        acc[2 * fb + blk] = mfma_split_x(A, x, acc[2 * fb + blk]);
+        acc[2 * fb + blk] = mfma_hsplit_x(A, x, acc[2 * fb + blk]);
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -804,7 +828,17 @@ blend_done:
   }
   if constexpr (MF) {
     // acc[2*fb + blk] holds out_feat^T: lane l, register r ->
-    // channel fb*32 + (r&3) + 8(r>>2) + 4(l>>5), strip pixel (l&31) + 32 blk.
+    // channel fb*32 + (r&3) + 8(r>>2) + 4(l>>5), strip pixel (l&31) + 32 blk;
+    // undo the channel's and the weights' scales (exact powers of two)
+#pragma unroll
+    for (int fb = 0; fb < FB; ++fb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ch = fb * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const float un = ldexpf(1.f, -row_scale_exp(__uint_as_float(fmax[ch])) - FW_EXP);
+        acc[2 * fb][r] *= un;
+        acc[2 * fb + 1][r] *= un;
+      }
     float t_lo, t_hi;
     swap32(T, T, t_lo, t_hi);  // T of strip pixel (l&31) and (l&31)+32
     // Buffer stores: one per-lane byte offset (pixel + the lane's channel
@@ -1442,6 +1476,33 @@ __global__ __launch_bounds__(256) void feature_grad_rows_kernel(const float* __r
   const int64_t g = i / F, c = i - g * F;
   const float v = pad[g * FS + c];
   out[i] = accumulate ? out[i] + v : v;
+}
+// Per-channel largest |feature| (float bits; non-negative floats order as
+// their bits, so atomicMax on the bits is a float max): 256 / F rows per
+// block step, each thread one channel, coalesced row reads.
+__global__ __launch_bounds__(256) void feature_absmax_kernel(const float* __restrict__ f, int64_t P, int F,
+                                                             uint32_t* __restrict__ out) {
+  __shared__ uint32_t s_m[64];
+  const int t = threadIdx.x, per = 256 / F;
+  if (t < 64) s_m[t] = 0u;
+  __syncthreads();
+  if (t < per * F) {
+    const int c = t % F;
+    float m = 0.f;
+    for (int64_t r = (int64_t)blockIdx.x * per + t / F; r < P; r += (int64_t)gridDim.x * per)
+      m = fmaxf(m, fabsf(f[r * F + c]));
+    atomicMax(&s_m[c], __float_as_uint(m));
+  }
+  __syncthreads();
+  if (t < F) atomicMax(&out[t], s_m[t]);
+}
+void launch_feature_absmax(const float* feats, int64_t P, int F, uint32_t* out, hipStream_t s) {
+  (void)hipMemsetAsync(out, 0, sizeof(uint32_t) * 64, s);
+  if (P <= 0 || F <= 0 || F > 64 || !feats) return;
+  const int per = 256 / F;
+  const int64_t blocks = (P + per - 1) / per;
+  hipLaunchKernelGGL(feature_absmax_kernel, dim3((unsigned)(blocks < 1024 ? blocks : 1024)), dim3(256), 0, s,
+                     feats, P, F, out);
 }
 void launch_feature_grad_rows(const float* pad, float* out, int64_t P, int F, int accumulate, hipStream_t s) {
   const int64_t n = P * (int64_t)F;
