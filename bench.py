@@ -1180,8 +1180,11 @@ def main():
         "higher_is_better": True, "scaling": "strong" if strong else "weak", "vs_baseline": None,
         "dtype": "f32",
         "dtype_note": ("fp32 blend on the vector ALUs; the feature blend and the backward's per-Gaussian "
-                       "sums as MFMA contractions of 3-piece bf16 splits (products to 2^-26 relative, "
-                       "fp32 accumulation): tests/test_gpu_parity.py holds them to the oracle at 1e-5 / 1e-4"),
+                       "sums as matrix-core contractions of split operands with fp32 accumulation -- the "
+                       "weights w = alpha T and their partners as fp16 two-piece splits under power-of-two "
+                       "scales (products to ~3 x 2^-24 relative), the geometry weights as 3-piece bf16 "
+                       "splits (2^-26): tests/test_gpu_parity.py and test_gpu_envelope.py hold them to the "
+                       "oracle at 1e-5 / 1e-4 and within 10x its fp32 summation-order spread"),
         "data": "synthetic",
         "config": {"workload": (f"rank {args.proxy_rank} of {args.proxy_world} of {args.gaussians // 1000}k "
                                 f"Gaussians x {args.cams_total} cams split ({args.split})" if args.proxy_world else

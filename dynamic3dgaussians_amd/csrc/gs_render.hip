@@ -1478,31 +1478,42 @@ __global__ __launch_bounds__(256) void feature_grad_rows_kernel(const float* __r
   out[i] = accumulate ? out[i] + v : v;
 }
 // Per-channel largest |feature| (float bits; non-negative floats order as
-// their bits, so atomicMax on the bits is a float max): 256 / F rows per
-// block step, each thread one channel, coalesced row reads.
+// their bits, so atomicMax on the bits is a float max).  Each thread owns one
+// 4-channel group of a row (F % 4 == 0 for every matrix-core width) and walks
+// rows 16-B load by 16-B load: a block step covers 256 / (F/4) whole rows,
+// contiguous, so a wave's loads are one coalesced run.
 __global__ __launch_bounds__(256) void feature_absmax_kernel(const float* __restrict__ f, int64_t P, int F,
                                                              uint32_t* __restrict__ out) {
   __shared__ uint32_t s_m[64];
-  const int t = threadIdx.x, per = 256 / F;
+  const int t = threadIdx.x, G = F >> 2, per = 256 / G;
   if (t < 64) s_m[t] = 0u;
   __syncthreads();
-  if (t < per * F) {
-    const int c = t % F;
-    float m = 0.f;
-    for (int64_t r = (int64_t)blockIdx.x * per + t / F; r < P; r += (int64_t)gridDim.x * per)
-      m = fmaxf(m, fabsf(f[r * F + c]));
-    atomicMax(&s_m[c], __float_as_uint(m));
+  if (t < per * G) {
+    const int gq = t % G;
+    float4 m = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4* __restrict__ f4 = reinterpret_cast<const float4*>(f);
+    for (int64_t r = (int64_t)blockIdx.x * per + t / G; r < P; r += (int64_t)gridDim.x * per) {
+      const float4 v = f4[r * G + gq];
+      m.x = fmaxf(m.x, fabsf(v.x));
+      m.y = fmaxf(m.y, fabsf(v.y));
+      m.z = fmaxf(m.z, fabsf(v.z));
+      m.w = fmaxf(m.w, fabsf(v.w));
+    }
+    atomicMax(&s_m[4 * gq], __float_as_uint(m.x));
+    atomicMax(&s_m[4 * gq + 1], __float_as_uint(m.y));
+    atomicMax(&s_m[4 * gq + 2], __float_as_uint(m.z));
+    atomicMax(&s_m[4 * gq + 3], __float_as_uint(m.w));
   }
   __syncthreads();
   if (t < F) atomicMax(&out[t], s_m[t]);
 }
 void launch_feature_absmax(const float* feats, int64_t P, int F, uint32_t* out, hipStream_t s) {
   (void)hipMemsetAsync(out, 0, sizeof(uint32_t) * 64, s);
-  if (P <= 0 || F <= 0 || F > 64 || !feats) return;
-  const int per = 256 / F;
-  const int64_t blocks = (P + per - 1) / per;
-  hipLaunchKernelGGL(feature_absmax_kernel, dim3((unsigned)(blocks < 1024 ? blocks : 1024)), dim3(256), 0, s,
-                     feats, P, F, out);
+  if (P <= 0 || F <= 0 || F > 64 || (F & 3) || !feats) return;
+  const int per = 256 / (F >> 2);
+  const int64_t blocks = (P + 4 * per - 1) / (4 * per);  // ~4 rows per thread
+  hipLaunchKernelGGL(feature_absmax_kernel, dim3((unsigned)(blocks < 2048 ? (blocks > 0 ? blocks : 1) : 2048)),
+                     dim3(256), 0, s, feats, P, F, out);
 }
 void launch_feature_grad_rows(const float* pad, float* out, int64_t P, int F, int accumulate, hipStream_t s) {
   const int64_t n = P * (int64_t)F;

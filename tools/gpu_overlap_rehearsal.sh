@@ -15,6 +15,12 @@ R=$GRAFT_REPO_ROOT
 cd $R
 O=$R/gpurun_out/${TAG:-overlap}
 mkdir -p $O
+# the step-level race check first (tools/zov_check.py: each step's gradients vs
+# a replay from what it read, the reads vs an in-line Adam replay, bit for bit)
+GS_BENCH_SHARE_GPU=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+  --master-addr 127.0.0.1 --master-port 29560 tools/zov_check.py > $O/zov_check.json 2> $O/zov_check.err \
+  || { tail -20 $O/zov_check.err; cat $O/zov_check.json; exit 1; }
+python -c "import json; d=json.load(open('$O/zov_check.json')); print('zov_check ok:', d['ok'], 'max grad rel:', max(max(r.values()) for x in d['ranks'] for r in x['grad_rel']))"
 A="--gpus 2 --steps 3 --warmup 1 --gaussians 100000 --cams 4 --width 400 --height 400 --no-cpu-baseline"
 run() {  # name, port, extra env
   env GS_BENCH_BACKEND=gloo GS_BENCH_SHARE_GPU=1 $3 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 \

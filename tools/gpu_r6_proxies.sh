@@ -1,0 +1,13 @@
+# Round 6: the configs[3] per-rank proxies (tools/gpu_r5_proxies.sh, 3
+# interleaved runs of the 8 ranks) on this tree, after a quick check of the
+# forward's feature-range pre-pass (kernel trace of a short bench).
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+cd $R
+O=$R/gpurun_out/${TAG:-r06px}
+mkdir -p $O
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt -o kt --output-format csv -- python3 $R/bench.py --no-cpu-baseline --steps 5 --warmup 2 > $O/kt.json 2> $O/kt.err || { tail $O/kt.err; exit 1; }
+cd $R && grep -E "absmax|render_fwd|Name" $O/kt/kt_kernel_stats.csv | cut -c1-160 | head -8
+rm -f $O/kt/kt_kernel_trace.csv
+TAG=${TAG:-r06px} bash tools/gpu_r5_proxies.sh

@@ -52,6 +52,11 @@ GEO = [k for k in LRS if k != "semantic_feature"]
 
 
 def main():
+    # the JSON line is the only output on stdout (gloo / RCCL print banners
+    # there): fd 1 goes to stderr for the run, the line to the saved fd
+    sys.stdout.flush()
+    line_fd = os.dup(1)
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     backend = os.environ.get("GS_ZOV_BACKEND", "gloo")
@@ -149,8 +154,9 @@ def main():
     reports = [None] * world
     dist.all_gather_object(reports, report)
     if rank == 0:
-        print(json.dumps({"ok": all_ok, "steps": steps, "gaussians": P, "cams_per_rank": C, "ranks": reports}),
-              flush=True)
+        with os.fdopen(line_fd, "w") as out:
+            out.write(json.dumps({"ok": all_ok, "steps": steps, "gaussians": P, "cams_per_rank": C,
+                                  "ranks": reports}) + "\n")
     dist.destroy_process_group()
     sys.exit(0 if all_ok else 1)
 
