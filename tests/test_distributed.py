@@ -445,7 +445,7 @@ def test_replaced_bucket_releases_surviving_parameters_hooks():
     params = {"means3D": torch.nn.Parameter(torch.randn(P, 3)), "cam_m": torch.nn.Parameter(torch.zeros(1, 3))}
     opt = torch.optim.Adam([{"params": [v], "name": k, "lr": 1e-3} for k, v in params.items()])
     drv = TimestepDriver(params, {}, opt, 1, render=lambda rv, cams: (None, None), world=2)
-    old = weakref.ref(drv.bucket)
+    old = weakref.ref(drv._live_bucket())  # the plain path's bucket (built at its first step)
     # densification: means3D replaced, cam_m survives
     params["means3D"] = torch.nn.Parameter(torch.randn(2 * P, 3))
     opt.param_groups[0]["params"][0] = params["means3D"]
