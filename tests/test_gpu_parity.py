@@ -460,3 +460,63 @@ def test_unnormalised_quaternions_q7(compat):
         if b.size == 0 or not np.any(b):
             continue
         assert H.rel_l2(a, b) <= 1e-4, (name, H.rel_l2(a, b))
+
+
+# ---------------------------------------------------------------- fp16 split ranges
+
+@pytest.mark.parametrize("compat", ["reference", "fixed"])
+@pytest.mark.parametrize("F", [32, 36])
+def test_fp16_split_contractions_across_channel_ranges(compat, F):
+    """The forward's feature contraction and the backward's weight
+    contractions run on fp16 two-piece splits under power-of-two scales: per
+    feature channel (forward, from the table's largest |feature|) and per
+    upstream-gradient row (backward, per strip).  Channels and rows whose
+    magnitudes differ by up to 1e12 -- a zero channel, 1e6 and 1e-6 channels,
+    a channel mixing 1e4 and 1e-4 rows, colour / depth / feature gradients at
+    1e-3 .. 1e5 and a zero gradient plane -- each hold the parity bar on their
+    own scale: every forward feature plane and every backward feature-gradient
+    channel within 1e-5 / 1e-4 relative of the oracle's."""
+    inp = H.scene(P=3000, F=F)
+    f = inp["semantic_feature"].clone()
+    f[:, 0] = 0.0
+    f[:, 1] *= 1e6
+    f[:, 2] *= 1e-6
+    f[::2, 3] *= 1e4
+    f[1::2, 3] *= 1e-4
+    inp["semantic_feature"] = f.contiguous()
+    g = H.gpu_forward(inp, compat)
+    o = H.oracle_forward(inp, compat)
+    assert g[0] == o[0]
+    fg, fo = g[2].cpu().numpy(), o[2]
+    for ch in range(F):
+        ref = fo[ch]
+        if not np.any(ref):
+            assert not np.any(fg[ch]), ch
+            continue
+        # per channel: its own magnitude (1e-5 relative of the plane's largest value,
+        # the forward bar; one flipped alpha decision aside)
+        bad = np.abs(fg[ch] - ref) > 1e-5 * np.abs(ref).max()
+        assert bad.mean() <= 1e-3, (ch, bad.mean())
+    dc, df, dd, da = H.upstream_grads(inp["image_height"], inp["image_width"], F)
+    dc = dc * torch.tensor([1e-3, 1.0, 1e5]).view(3, 1, 1)
+    dd = dd * 1e3
+    df = df.clone()
+    df[4] = 0.0
+    df[5] *= 1e-8
+    df[6] *= 1e5
+    grads = (dc, df, dd, da)
+    gb = H.gpu_backward(inp, g, grads, compat)
+    ob = H.oracle_backward(inp, o, grads, compat)
+    for name, a, b in zip(GRAD_NAMES, gb, ob):
+        if b.size == 0 or not np.any(b):
+            continue
+        assert H.rel_l2(a, b) <= 1e-4, (name, H.rel_l2(a, b))
+    ds_g, ds_o = gb[2], ob[2]
+    for ch in range(F):
+        if not np.any(ds_o[:, ch]):
+            assert not np.any(ds_g[:, ch]), ch
+            continue
+        assert H.rel_l2(ds_g[:, ch], ds_o[:, ch]) <= 1e-4, (ch, H.rel_l2(ds_g[:, ch], ds_o[:, ch]))
+    dc_g, dc_o = gb[1], ob[1]
+    for ch in range(3):  # the colour rows' own scales (1e-3 .. 1e5 apart)
+        assert H.rel_l2(dc_g[:, ch], dc_o[:, ch]) <= 1e-4, (ch, H.rel_l2(dc_g[:, ch], dc_o[:, ch]))
