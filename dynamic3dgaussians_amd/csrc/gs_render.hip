@@ -249,11 +249,8 @@ __device__ inline float gauss_exp(float p) { return __builtin_amdgcn_exp2f(p); }
 __device__ inline float4 half_conic(const float4& q0, const float4& q1) {
   return make_float4((-0.5f * HC_SCALE) * q0.z, -HC_SCALE * q0.w, (-0.5f * HC_SCALE) * q1.x, 0.0f);
 }
-// power = h.x dx^2 + h.y dx dy + h.z dy^2 as dx (h.x dx + h.y dy) + (h.z dy) dy:
-// 3 products and 2 fma (the term-by-term form took 4 and 2); one fixed order
-// shared by both blend kernels, so their alpha decisions agree bit for bit
 __device__ inline float gauss_power(float dx, float dy, const float4& h) {
-  return fmaf(dx, fmaf(h.x, dx, h.y * dy), (h.z * dy) * dy);
+  return fmaf(h.x * dx, dx, fmaf(h.z * dy, dy, (h.y * dx) * dy));
 }
 
 // Can the Gaussian reach alpha >= 1/255 at any pixel centre of the strip

@@ -50,11 +50,14 @@ def _fwd_bwd_vs_oracle(inp, compat, F):
     grads = H.upstream_grads(Hh, W, F)
     gb = H.gpu_backward(inp, g, grads, compat)
     ob = H.oracle_backward(inp, o, grads, compat)
+    report = {}
     for name, a, b in zip(GRAD_NAMES, gb, ob):
         assert a.shape == b.shape, name
         if b.size == 0 or not np.any(b):
             assert not np.any(a) or np.abs(a).max() < 1e-6, name
             continue
+        report[name] = (H.rel_l2(a[keep], b[keep]), H.rel_l2(a, b))
+        print(f"{compat} {name}: kept {report[name][0]:.2e} all {report[name][1]:.2e}")
         assert H.rel_l2(a[keep], b[keep]) <= 1e-4, (name, H.rel_l2(a[keep], b[keep]))
         if compat == "fixed" or flipped.size == 0:
             assert H.rel_l2(a, b) <= 1e-4, (name, H.rel_l2(a, b))
