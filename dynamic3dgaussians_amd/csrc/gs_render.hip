@@ -1481,10 +1481,18 @@ __global__ __launch_bounds__(256) void feature_grad_rows_kernel(const float* __r
 // their bits, so atomicMax on the bits is a float max).  Each thread owns one
 // 4-channel group of a row (F % 4 == 0 for every matrix-core width) and walks
 // rows 16-B load by 16-B load: a block step covers 256 / (F/4) whole rows,
-// contiguous, so a wave's loads are one coalesced run.
+// contiguous, so a wave's loads are one coalesced run.  The blocks' maxima
+// meet in FMAX_REPS replicas of the table (same-address float atomics
+// serialise at the memory side: 2,048 blocks into one 32-word table took
+// 31 us per 300k x 32 table, the whole pass's time); the last block to finish
+// (a counter) folds the replicas into out[0 .. F).
+constexpr int FMAX_REPS = 32;
 __global__ __launch_bounds__(256) void feature_absmax_kernel(const float* __restrict__ f, int64_t P, int F,
                                                              uint32_t* __restrict__ out) {
+  uint32_t* __restrict__ rep = out + 64;                        // FMAX_REPS x 64
+  uint32_t* __restrict__ done = out + 64 + 64 * FMAX_REPS;      // block counter
   __shared__ uint32_t s_m[64];
+  __shared__ bool s_last;
   const int t = threadIdx.x, G = F >> 2, per = 256 / G;
   if (t < 64) s_m[t] = 0u;
   __syncthreads();
@@ -1492,7 +1500,17 @@ __global__ __launch_bounds__(256) void feature_absmax_kernel(const float* __rest
     const int gq = t % G;
     float4 m = make_float4(0.f, 0.f, 0.f, 0.f);
     const float4* __restrict__ f4 = reinterpret_cast<const float4*>(f);
-    for (int64_t r = (int64_t)blockIdx.x * per + t / G; r < P; r += (int64_t)gridDim.x * per) {
+    const int64_t step = (int64_t)gridDim.x * per;
+    int64_t r = (int64_t)blockIdx.x * per + t / G;
+    // two rows in flight per thread
+    for (; r + step < P; r += 2 * step) {
+      const float4 v = f4[r * G + gq], u = f4[(r + step) * G + gq];
+      m.x = fmaxf(m.x, fmaxf(fabsf(v.x), fabsf(u.x)));
+      m.y = fmaxf(m.y, fmaxf(fabsf(v.y), fabsf(u.y)));
+      m.z = fmaxf(m.z, fmaxf(fabsf(v.z), fabsf(u.z)));
+      m.w = fmaxf(m.w, fmaxf(fabsf(v.w), fabsf(u.w)));
+    }
+    if (r < P) {
       const float4 v = f4[r * G + gq];
       m.x = fmaxf(m.x, fabsf(v.x));
       m.y = fmaxf(m.y, fabsf(v.y));
@@ -1505,10 +1523,20 @@ __global__ __launch_bounds__(256) void feature_absmax_kernel(const float* __rest
     atomicMax(&s_m[4 * gq + 3], __float_as_uint(m.w));
   }
   __syncthreads();
-  if (t < F) atomicMax(&out[t], s_m[t]);
+  if (t < F) atomicMax(&rep[(blockIdx.x % FMAX_REPS) * 64 + t], s_m[t]);
+  __threadfence();  // the replica atomics complete before this block counts itself
+  __syncthreads();
+  if (t == 0) s_last = atomicAdd(done, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!s_last || t >= F) return;
+  uint32_t mx = 0u;
+  for (int k = 0; k < FMAX_REPS; ++k)
+    mx = max(mx, __hip_atomic_load(&rep[k * 64 + t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  out[t] = mx;
 }
 void launch_feature_absmax(const float* feats, int64_t P, int F, uint32_t* out, hipStream_t s) {
-  (void)hipMemsetAsync(out, 0, sizeof(uint32_t) * 64, s);
+  // the table, its replicas and the block counter (FMAX_WORDS, gs_common.h)
+  (void)hipMemsetAsync(out, 0, sizeof(uint32_t) * FMAX_WORDS, s);
   if (P <= 0 || F <= 0 || F > 64 || (F & 3) || !feats) return;
   const int per = 256 / (F >> 2);
   const int64_t blocks = (P + 4 * per - 1) / (4 * per);  // ~4 rows per thread

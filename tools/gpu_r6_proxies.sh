@@ -10,4 +10,11 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt -o kt --output-format csv -- python3 $R/bench.py --no-cpu-baseline --steps 5 --warmup 2 > $O/kt.json 2> $O/kt.err || { tail $O/kt.err; exit 1; }
 cd $R && grep -E "absmax|render_fwd|Name" $O/kt/kt_kernel_stats.csv | cut -c1-160 | head -8
 rm -f $O/kt/kt_kernel_trace.csv
+# the other configs (configs[1] drop-in F = 0 / 32, configs[4] per rank)
+bash tools/gpu_configs.sh || exit 3
+cp gpurun_out/configs.jsonl $O/configs.jsonl
+python -c "
+import json
+for l in open('$O/configs.jsonl'):
+    d = json.loads(l); print('config', d['config']['workload'][:60], d['ms_per_step'], {k: round(v, 3) for k, v in d['stages_ms_per_step'].items()})"
 TAG=${TAG:-r06px} bash tools/gpu_r5_proxies.sh
