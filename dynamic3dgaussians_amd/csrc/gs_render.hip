@@ -1524,14 +1524,22 @@ __global__ __launch_bounds__(256) void feature_absmax_kernel(const float* __rest
   }
   __syncthreads();
   if (t < F) atomicMax(&rep[(blockIdx.x % FMAX_REPS) * 64 + t], s_m[t]);
-  __threadfence();  // the replica atomics complete before this block counts itself
+  // the replica atomics are performed (acknowledged: s_waitcnt 0) before this
+  // block counts itself -- a wait, not an agent-scope fence, whose L2
+  // write-back per block cost 150 us over 2,048 blocks
+  __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
-  if (t == 0) s_last = atomicAdd(done, 1u) == gridDim.x - 1;
+  if (t == 0) s_last = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
   __syncthreads();
   if (!s_last || t >= F) return;
-  uint32_t mx = 0u;
+  // read through the atomics' own path (a returning max of 0 at the memory
+  // side), not through an L2 that may hold the memset's zeros
+  // (an opaque 0: the compiler turns an RMW it can see is idempotent into a
+  // plain atomic load)
+  uint32_t zero = 0u, mx = 0u;
+  asm volatile("" : "+v"(zero));
   for (int k = 0; k < FMAX_REPS; ++k)
-    mx = max(mx, __hip_atomic_load(&rep[k * 64 + t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    mx = max(mx, __hip_atomic_fetch_max(&rep[k * 64 + t], zero, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   out[t] = mx;
 }
 void launch_feature_absmax(const float* feats, int64_t P, int F, uint32_t* out, hipStream_t s) {

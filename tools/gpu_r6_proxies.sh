@@ -6,6 +6,9 @@ R=$GRAFT_REPO_ROOT
 cd $R
 O=$R/gpurun_out/${TAG:-r06px}
 mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fused.py -x -q --timeout 300 \
+  --timeout-method thread -p no:cacheprovider > $O/parity.log 2>&1 || { tail -30 $O/parity.log; exit 4; }
+tail -1 $O/parity.log
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt -o kt --output-format csv -- python3 $R/bench.py --no-cpu-baseline --steps 5 --warmup 2 > $O/kt.json 2> $O/kt.err || { tail $O/kt.err; exit 1; }
 cd $R && grep -E "absmax|render_fwd|Name" $O/kt/kt_kernel_stats.csv | cut -c1-160 | head -8
