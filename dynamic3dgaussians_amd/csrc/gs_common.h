@@ -136,8 +136,6 @@ struct SortLayout {
 // Image buffer (per pixel / per tile), also the binning plan: per-block tile
 // histograms (turned into per-block offsets), tile totals and the 8-word
 // header (gs_meta.h).
-// feature_absmax_kernel's scratch: the 64-word table, 32 replicas, a counter
-constexpr int FMAX_WORDS = 64 + 64 * 32 + 1;
 struct ImgLayout {
   size_t ranges, n_contrib, thist, ttotal, bsum, meta, order, smax, fmax, total;
   int64_t tiles;
@@ -156,9 +154,8 @@ struct ImgLayout {
     order = o;     o = align_up(o + sizeof(uint32_t) * 4 * t, 256);
     smax = o;      o = align_up(o + sizeof(uint32_t) * 4 * t, 256);  // per strip item: longest pixel walk (forward -> backward)
     // per feature channel (F <= 64): the largest |feature| as float bits, for
-    // the forward's fp16 feature contraction (camera 0's buffer of a batch),
-    // with the pass's replicas and block counter behind it
-    fmax = o;      o = align_up(o + sizeof(uint32_t) * FMAX_WORDS, 256);
+    // the forward's fp16 feature contraction (camera 0's buffer of a batch)
+    fmax = o;      o = align_up(o + sizeof(uint32_t) * 64, 256);
     total = o;
   }
 };

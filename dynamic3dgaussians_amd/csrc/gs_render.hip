@@ -1480,19 +1480,16 @@ __global__ __launch_bounds__(256) void feature_grad_rows_kernel(const float* __r
 // Per-channel largest |feature| (float bits; non-negative floats order as
 // their bits, so atomicMax on the bits is a float max).  Each thread owns one
 // 4-channel group of a row (F % 4 == 0 for every matrix-core width) and walks
-// rows 16-B load by 16-B load: a block step covers 256 / (F/4) whole rows,
-// contiguous, so a wave's loads are one coalesced run.  The blocks' maxima
-// meet in FMAX_REPS replicas of the table (same-address float atomics
-// serialise at the memory side: 2,048 blocks into one 32-word table took
-// 31 us per 300k x 32 table, the whole pass's time); the last block to finish
-// (a counter) folds the replicas into out[0 .. F).
-constexpr int FMAX_REPS = 32;
+// rows 16-B load by 16-B load, two in flight: a block step covers 256 / (F/4)
+// whole rows, contiguous, so a wave's loads are one coalesced run.  At most
+// 256 blocks: every block ends in F global float-max atomics on the one
+// table, and those cost ~10 ns per block at the memory side whatever the
+// addresses (tools/micro/absmax_bench.hip, 300k x 32: the read alone 9-10 us
+// at any grid; with the atomics 13 us at 256 blocks, 30 us at 2,048, 52 at
+// 4,096 -- replicas of the table did not change it).
 __global__ __launch_bounds__(256) void feature_absmax_kernel(const float* __restrict__ f, int64_t P, int F,
                                                              uint32_t* __restrict__ out) {
-  uint32_t* __restrict__ rep = out + 64;                        // FMAX_REPS x 64
-  uint32_t* __restrict__ done = out + 64 + 64 * FMAX_REPS;      // block counter
   __shared__ uint32_t s_m[64];
-  __shared__ bool s_last;
   const int t = threadIdx.x, G = F >> 2, per = 256 / G;
   if (t < 64) s_m[t] = 0u;
   __syncthreads();
@@ -1502,7 +1499,6 @@ __global__ __launch_bounds__(256) void feature_absmax_kernel(const float* __rest
     const float4* __restrict__ f4 = reinterpret_cast<const float4*>(f);
     const int64_t step = (int64_t)gridDim.x * per;
     int64_t r = (int64_t)blockIdx.x * per + t / G;
-    // two rows in flight per thread
     for (; r + step < P; r += 2 * step) {
       const float4 v = f4[r * G + gq], u = f4[(r + step) * G + gq];
       m.x = fmaxf(m.x, fmaxf(fabsf(v.x), fabsf(u.x)));
@@ -1523,32 +1519,14 @@ __global__ __launch_bounds__(256) void feature_absmax_kernel(const float* __rest
     atomicMax(&s_m[4 * gq + 3], __float_as_uint(m.w));
   }
   __syncthreads();
-  if (t < F) atomicMax(&rep[(blockIdx.x % FMAX_REPS) * 64 + t], s_m[t]);
-  // the replica atomics are performed (acknowledged: s_waitcnt 0) before this
-  // block counts itself -- a wait, not an agent-scope fence, whose L2
-  // write-back per block cost 150 us over 2,048 blocks
-  __builtin_amdgcn_s_waitcnt(0);
-  __syncthreads();
-  if (t == 0) s_last = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
-  __syncthreads();
-  if (!s_last || t >= F) return;
-  // read through the atomics' own path (a returning max of 0 at the memory
-  // side), not through an L2 that may hold the memset's zeros
-  // (an opaque 0: the compiler turns an RMW it can see is idempotent into a
-  // plain atomic load)
-  uint32_t zero = 0u, mx = 0u;
-  asm volatile("" : "+v"(zero));
-  for (int k = 0; k < FMAX_REPS; ++k)
-    mx = max(mx, __hip_atomic_fetch_max(&rep[k * 64 + t], zero, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  out[t] = mx;
+  if (t < F) atomicMax(&out[t], s_m[t]);
 }
 void launch_feature_absmax(const float* feats, int64_t P, int F, uint32_t* out, hipStream_t s) {
-  // the table, its replicas and the block counter (FMAX_WORDS, gs_common.h)
-  (void)hipMemsetAsync(out, 0, sizeof(uint32_t) * FMAX_WORDS, s);
+  (void)hipMemsetAsync(out, 0, sizeof(uint32_t) * 64, s);
   if (P <= 0 || F <= 0 || F > 64 || (F & 3) || !feats) return;
   const int per = 256 / (F >> 2);
-  const int64_t blocks = (P + 4 * per - 1) / (4 * per);  // ~4 rows per thread
-  hipLaunchKernelGGL(feature_absmax_kernel, dim3((unsigned)(blocks < 2048 ? (blocks > 0 ? blocks : 1) : 2048)),
+  const int64_t blocks = (P + 2 * per - 1) / (2 * per);
+  hipLaunchKernelGGL(feature_absmax_kernel, dim3((unsigned)(blocks < 256 ? (blocks > 0 ? blocks : 1) : 256)),
                      dim3(256), 0, s, feats, P, F, out);
 }
 void launch_feature_grad_rows(const float* pad, float* out, int64_t P, int F, int accumulate, hipStream_t s) {
