@@ -40,11 +40,11 @@ if VARIANT:
 # timing) and is never rebuilt.
 VARIANT_FLAGS = {"": [], "stats": ["-DGS_STATS"], "stamps": ["-DGS_STAMPS"],
                  "stamps_fine": ["-DGS_STAMPS", "-DGS_STAMPS_FINE"],
-                 "exp_nofeat": [], "exp_noatomic": [],  # the backward's atomics (tools/variants.py)
+                 "exp_nofeat": [], "exp_noacc": [], "exp_noatomic": [],  # the backward's atomics (tools/variants.py)
                  "exp_fwd_nofeatst": [],  # traffic of the feature planes
                  "exp_sort_copy": [],  # the tile sort's floor: copy, no sort
                  "ctl": []}  # the product's flags under a variant's (ctypes) binding: the A/B control
-PATCHED = ("exp_nofeat", "exp_noatomic", "exp_fwd_nofeatst", "exp_sort_copy")
+PATCHED = ("exp_nofeat", "exp_noacc", "exp_noatomic", "exp_fwd_nofeatst", "exp_sort_copy")
 ARCH = os.environ.get("GSPLAT_OFFLOAD_ARCH", "gfx950")
 
 # Per-file flags.  The preprocess kernels are compiled without FMA

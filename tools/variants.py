@@ -35,6 +35,7 @@ _SORT_COPY = ("gs_tiles.hip",
 
 PATCHES = {
     "exp_nofeat": [_FEAT_ATOMIC],
+    "exp_noacc": [_ACC_ATOMIC],
     "exp_noatomic": [_FEAT_ATOMIC, _ACC_ATOMIC],
     "exp_fwd_nofeatst": [_FWD_FEAT_STORE],
     "exp_sort_copy": [_SORT_COPY],
