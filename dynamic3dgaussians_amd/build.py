@@ -43,8 +43,9 @@ VARIANT_FLAGS = {"": [], "stats": ["-DGS_STATS"], "stamps": ["-DGS_STAMPS"],
                  "exp_nofeat": [], "exp_noacc": [], "exp_noatomic": [],  # the backward's atomics (tools/variants.py)
                  "exp_fwd_nofeatst": [],  # traffic of the feature planes
                  "exp_sort_copy": [],  # the tile sort's floor: copy, no sort
+                 "exp_rot_all": [],  # strip_of_block's XCD rotation at C >= 8 too
                  "ctl": []}  # the product's flags under a variant's (ctypes) binding: the A/B control
-PATCHED = ("exp_nofeat", "exp_noacc", "exp_noatomic", "exp_fwd_nofeatst", "exp_sort_copy")
+PATCHED = ("exp_nofeat", "exp_noacc", "exp_noatomic", "exp_fwd_nofeatst", "exp_sort_copy", "exp_rot_all")
 ARCH = os.environ.get("GSPLAT_OFFLOAD_ARCH", "gfx950")
 
 # Per-file flags.  The preprocess kernels are compiled without FMA

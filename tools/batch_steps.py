@@ -84,6 +84,7 @@ def main():
     if ras.plan is not None:
         # the counted reps after the warm call rendered every camera once
         print(f"sync-free retries: {ras.plan.retries} over {ras.plan.calls} calls", flush=True)
+        print("num_instances", list(ras.plan.num_instances), flush=True)
         assert ras.plan.retries == 0, "a counted rep was rendered twice (binning capacity retry)"
     if a.stamps:
         import json

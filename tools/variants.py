@@ -33,12 +33,18 @@ _SORT_COPY = ("gs_tiles.hip",
               "  return;\n"
               "  if (n <= cap) {\n    // keys straight from global memory")
 
+# strip_of_block: the XCD rotation at every camera count (C >= 8 too)
+_ROT_ALL = ("gs_render.hip",
+            "    u = k * 8 + ((x + (C < CAM_GROUP ? k : 0)) & 7);\n",
+            "    u = k * 8 + ((x + k) & 7);\n")
+
 PATCHES = {
     "exp_nofeat": [_FEAT_ATOMIC],
     "exp_noacc": [_ACC_ATOMIC],
     "exp_noatomic": [_FEAT_ATOMIC, _ACC_ATOMIC],
     "exp_fwd_nofeatst": [_FWD_FEAT_STORE],
     "exp_sort_copy": [_SORT_COPY],
+    "exp_rot_all": [_ROT_ALL],
 }
 
 
