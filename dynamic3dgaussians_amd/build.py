@@ -44,8 +44,9 @@ VARIANT_FLAGS = {"": [], "stats": ["-DGS_STATS"], "stamps": ["-DGS_STAMPS"],
                  "exp_fwd_nofeatst": [],  # traffic of the feature planes
                  "exp_sort_copy": [],  # the tile sort's floor: copy, no sort
                  "exp_rot_all": [],  # strip_of_block's XCD rotation at C >= 8 too
+                 "exp_fwd_row0": [],  # render_fwd's feature rows from 8 cached rows (gather latency)
                  "ctl": []}  # the product's flags under a variant's (ctypes) binding: the A/B control
-PATCHED = ("exp_nofeat", "exp_noacc", "exp_noatomic", "exp_fwd_nofeatst", "exp_sort_copy", "exp_rot_all")
+PATCHED = ("exp_nofeat", "exp_noacc", "exp_noatomic", "exp_fwd_nofeatst", "exp_sort_copy", "exp_rot_all", "exp_fwd_row0")
 ARCH = os.environ.get("GSPLAT_OFFLOAD_ARCH", "gfx950")
 
 # Per-file flags.  The preprocess kernels are compiled without FMA

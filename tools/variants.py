@@ -38,6 +38,13 @@ _ROT_ALL = ("gs_render.hip",
             "    u = k * 8 + ((x + (C < CAM_GROUP ? k : 0)) & 7);\n",
             "    u = k * 8 + ((x + k) & 7);\n")
 
+# render_fwd's flush: every feature row read from row (g & 7) -- always
+# cached -- instead of the batch's Gaussians: the gather latency's share
+_FWD_ROW0 = ("gs_render.hip",
+             "          const uint32_t off = (g * (uint32_t)F + (uint32_t)(fb * 32 + (ln & 31))) * 4u;\n",
+             "          const uint32_t off = ((g & 7u) * (uint32_t)F + (uint32_t)(fb * 32 + (ln & 31))) * 4u;"
+             "  // timing only\n")
+
 PATCHES = {
     "exp_nofeat": [_FEAT_ATOMIC],
     "exp_noacc": [_ACC_ATOMIC],
@@ -45,6 +52,7 @@ PATCHES = {
     "exp_fwd_nofeatst": [_FWD_FEAT_STORE],
     "exp_sort_copy": [_SORT_COPY],
     "exp_rot_all": [_ROT_ALL],
+    "exp_fwd_row0": [_FWD_ROW0],
 }
 
 
