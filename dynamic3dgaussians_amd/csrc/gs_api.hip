@@ -261,6 +261,7 @@ TileArgs tile_args(int P, int W, int H, void* geom, void* image, const int32_t* 
   t.meta = at<uint32_t>(image, il.meta);
   t.ranges = at<uint2>(image, il.ranges);
   t.order = at<uint4>(image, il.order);
+  t.fmax = at<uint32_t>(image, il.fmax);
   return t;
 }
 }  // namespace

@@ -96,8 +96,9 @@ __host__ __device__ constexpr int feature_grad_stride(int F) {
   return (F < 16 || F % 16 == 0) ? F : (F + 15) / 16 * 16;
 }
 void launch_feature_grad_rows(const float* pad, float* out, int64_t P, int F, int accumulate, hipStream_t s);
-// out[c] = bits of max_g |feats[g][c]| (c < F <= 64), zeroed first: the
-// scales of the forward's fp16 feature contraction (render_fwd, F >= 32)
+// out[c] = bits of max_g |feats[g][c]| (c < F <= 64), into a table the
+// caller zeroed (tile_order_kernel, earlier on the stream): the scales of the
+// forward's fp16 feature contraction (render_fwd, F >= 32)
 void launch_feature_absmax(const float* feats, int64_t P, int F, uint32_t* out, hipStream_t s);
 
 struct RenderBwdArgs {
@@ -163,6 +164,7 @@ struct TileArgs {
   uint32_t* meta;        // 4
   uint2* ranges;         // num_tiles
   uint4* order;          // num_tiles: dispatch records {tile, range.x, range.y, 0}, longest list first
+  uint32_t* fmax;        // 64: the forward's feature-range table (camera 0's), zeroed by tile_order_kernel
   uint64_t* keys;        // L
   uint64_t* keys2;       // L (sort twin for long tiles)
   uint32_t* plist;       // L

@@ -1522,7 +1522,7 @@ __global__ __launch_bounds__(256) void feature_absmax_kernel(const float* __rest
   if (t < F) atomicMax(&out[t], s_m[t]);
 }
 void launch_feature_absmax(const float* feats, int64_t P, int F, uint32_t* out, hipStream_t s) {
-  (void)hipMemsetAsync(out, 0, sizeof(uint32_t) * 64, s);
+  // `out` is zero already (tile_order_kernel)
   if (P <= 0 || F <= 0 || F > 64 || (F & 3) || !feats) return;
   const int per = 256 / (F >> 2);
   const int64_t blocks = (P + 2 * per - 1) / (2 * per);

@@ -507,8 +507,12 @@ __global__ __launch_bounds__(OFF_T) void tile_offsets_kernel(const uint32_t* __r
 __global__ __launch_bounds__(OFF_T) void tile_order_kernel(const uint32_t* __restrict__ ttotal0, int T,
                                                            const uint32_t* __restrict__ meta0,
                                                            const uint2* __restrict__ ranges0,
-                                                           uint4* __restrict__ order0, CamBatch cb, SortCover cv) {
+                                                           uint4* __restrict__ order0, uint32_t* __restrict__ fmax,
+                                                           CamBatch cb, SortCover cv) {
   const int64_t io = blockIdx.x * cb.img_stride;  // one workgroup per camera
+  // the forward's feature-range table starts at zero (launch_feature_absmax
+  // runs later on the stream; this saves it a fill launch)
+  if (blockIdx.x == 0 && threadIdx.x < 64) fmax[threadIdx.x] = 0u;
   const uint32_t* __restrict__ ttotal = shift_bytes(ttotal0, io);
   const uint32_t* __restrict__ meta = shift_bytes(meta0, io);
   const uint2* __restrict__ ranges = shift_bytes(ranges0, io);
@@ -935,7 +939,7 @@ void launch_tile_plan(const TileArgs& a, const CamBatch& cb, int prefiltered, ui
 
 void launch_tile_order(const TileArgs& a, const CamBatch& cb, const SortCover& cv, hipStream_t s) {
   hipLaunchKernelGGL(tile_order_kernel, dim3(cb.C), dim3(OFF_T), 0, s, a.ttotal, a.num_tiles, a.meta, a.ranges, a.order,
-                     cb, cv);
+                     a.fmax, cb, cv);
 }
 
 void launch_tile_bucket(const TileArgs& a, const CamBatch& cb, hipStream_t s) {
