@@ -12,6 +12,7 @@
 
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/gs_knn.h"
@@ -162,7 +163,6 @@ thread_local PlanInfo g_plan;
 struct HeaderSlot {
   uint32_t* host = nullptr;  // host pointer
   uint32_t* dev = nullptr;   // the same memory as the kernels address it
-  hipEvent_t ev = nullptr;
   int device = -1;
 };
 std::mutex g_hmu;
@@ -170,12 +170,17 @@ std::vector<HeaderSlot> g_hfree;
 
 struct HeaderLease {
   HeaderSlot s;
-  // set once a plan kernel that writes this slot (and records its event) may
-  // have been enqueued; cleared when the caller has waited for that event.
-  // A lease dropped in between (an error path after the launch) waits for
-  // the event before the slot goes back to the pool, so the next caller's
+  // set once a plan kernel that writes this slot may have been enqueued (on
+  // `stream`); cleared when the caller has seen every header written.  A
+  // lease dropped in between (an error path after the launch) synchronizes
+  // that stream before the slot goes back to the pool, so the next caller's
   // sentinel cannot be overwritten by a stale kernel.
   bool in_flight = false;
+  hipStream_t stream = nullptr;
+  void launched(hipStream_t s_) {
+    in_flight = true;
+    stream = s_;
+  }
   HeaderLease() {
     int device = 0;
     if (hipGetDevice(&device) != hipSuccess) return;
@@ -194,11 +199,7 @@ struct HeaderLease {
                       hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
       return;
     void* d = nullptr;
-    // device-scope release: tile_offsets_kernel's stores to this host memory
-    // are system-scope atomics behind a system fence of their own
-    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess ||
-        hipEventCreateWithFlags(&s.ev, hipEventReleaseToDevice) !=
-            hipSuccess) {
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
       (void)hipHostFree(h);
       s = HeaderSlot{};
       return;
@@ -210,7 +211,7 @@ struct HeaderLease {
     if (!s.host) return;
     // a kernel that may still write the slot: wait for it, or (the device
     // failed) keep the slot out of the pool for good
-    if (in_flight && hipEventSynchronize(s.ev) != hipSuccess) return;
+    if (in_flight && hipStreamSynchronize(stream) != hipSuccess) return;
     std::lock_guard<std::mutex> lk(g_hmu);
     g_hfree.push_back(s);
   }
@@ -396,8 +397,7 @@ static int debug_check_lists(const TileArgs& ta, const CamBatch& cb, const void*
 // The plan's kernels (preprocess, tile histogram, column scan, offsets), the
 // headers published to hdr_dev (mapped host memory) by the last of them.
 static int plan_enqueue(const gs_gaussians* g, const gs_camera* cams, int C, int prefiltered, int debug, void* geom,
-                        void* image, int32_t* radii, uint32_t* hdr_dev, hipEvent_t done, CamBatch& cb,
-                        hipStream_t s) {
+                        void* image, int32_t* radii, uint32_t* hdr_dev, CamBatch& cb, hipStream_t s) {
   const int P = g->P;
   const int W = cams[0].image_width, H = cams[0].image_height;
   if (int e = make_batch(cams, C, P, W, H, cb)) return e;
@@ -436,7 +436,7 @@ static int plan_enqueue(const gs_gaussians* g, const gs_camera* cams, int C, int
   if (int e = check("preprocess", debug, s)) return e;
   {
     StageTimer t(s, GS_STAGE_SCAN);
-    launch_tile_plan(ta, cb, prefiltered, hdr_dev, done, s);
+    launch_tile_plan(ta, cb, prefiltered, hdr_dev, s);
   }
   return check("tile plan", debug, s);
 }
@@ -474,23 +474,34 @@ static int plan_read(const uint32_t (*host)[M_WORDS], int C, int prefiltered, in
 // stored them to the mapped buffer and its dispatch records hl's event (an
 // in-stream copy of the device headers instead measured slower, DESIGN.md
 // section 4).  record_only: do not wait yet.
-static int publish_wait(HeaderLease& hl, int C, hipStream_t s, bool record_only) {
-  hipError_t he = hipSuccess;
-  if (!record_only) he = hipEventSynchronize(hl.s.ev);
-  if (he == hipSuccess && !record_only) hl.in_flight = false;
-  if (he == hipSuccess && !record_only) {
-    // every header's last word is 0 once written (header_sentinel): an event
-    // that did not cover the header's kernel must not hand back stale words
-    bool stale = false;
-    for (int c = 0; c < C; ++c) stale = stale || hl.s.host[c * M_WORDS + M_WORDS - 1] != 0u;
-    if (stale) {
-      he = hipStreamSynchronize(s);
-      for (int c = 0; c < C && he == hipSuccess; ++c)
-        if (hl.s.host[c * M_WORDS + M_WORDS - 1] != 0u)
-          return fail(-4, "plan header of camera %d was not written (event / header path)", c);
+// Wait until the plan kernel has written every camera's header: the host
+// polls each header's last word (header_sentinel: 0 once written, stored by
+// tile_offsets_kernel after the rest and a system fence), yielding the core
+// between reads.  Every few thousand reads it asks whether the stream has
+// drained: a stream done or failed with a header still unwritten is an error,
+// not a hang.  No event rides on the plan kernel (its completion signal idled
+// the GPU 15-27 us behind it, profiles/r06gaps3/).
+static int publish_wait(HeaderLease& hl, int C, hipStream_t s) {
+  auto written = [&]() {
+    for (int c = 0; c < C; ++c)
+      if (__atomic_load_n(&hl.s.host[c * M_WORDS + M_WORDS - 1], __ATOMIC_ACQUIRE) != 0u) return false;
+    return true;
+  };
+  for (uint32_t spin = 1; !written(); ++spin) {
+    if ((spin & 4095u) == 0u) {
+      const hipError_t q = hipStreamQuery(s);
+      if (q == hipSuccess) {
+        if (written()) break;
+        for (int c = 0; c < C; ++c)
+          if (__atomic_load_n(&hl.s.host[c * M_WORDS + M_WORDS - 1], __ATOMIC_ACQUIRE) != 0u)
+            return fail(-4, "plan header of camera %d was not written (header path)", c);
+      } else if (q != hipErrorNotReady) {
+        return fail((int)q, "num_rendered readback: %s", hipGetErrorString(q));
+      }
     }
+    std::this_thread::yield();
   }
-  if (he != hipSuccess) return fail((int)he, "num_rendered readback: %s", hipGetErrorString(he));
+  hl.in_flight = false;
   return 0;
 }
 
@@ -516,14 +527,14 @@ static int plan_impl(const gs_gaussians* g, const gs_camera* cams, int C, int pr
   if (!hl.ok()) return fail((int)hipErrorOutOfMemory, "cannot allocate the page-locked plan header buffer");
   header_sentinel(hl, C);
   CamBatch cb;
-  hl.in_flight = true;
-  if (int e = plan_enqueue(g, cams, C, prefiltered, debug, geom, image, radii, hl.s.dev, hl.s.ev, cb, s))
+  hl.launched(s);
+  if (int e = plan_enqueue(g, cams, C, prefiltered, debug, geom, image, radii, hl.s.dev, cb, s))
     return e;
   // The one host read of the forward (CR/rasterizer_impl.cu:287), one for
   // the whole batch: the list instance counts size the binning buffer; the
   // reference's counts and the rest of the headers ride along.
   const TileArgs ta = tile_args(P, cams[0].image_width, cams[0].image_height, geom, image);
-  if (int e = publish_wait(hl, C, s, false)) return e;
+  if (int e = publish_wait(hl, C, s)) return e;
   PlanInfo info;
   if (int e = plan_read(reinterpret_cast<const uint32_t(*)[M_WORDS]>(hl.s.host), C, prefiltered, debug,
                         (int64_t)ta.grid_x * ta.grid_y, num_rendered, num_instances, info))
@@ -827,13 +838,12 @@ int gs_forward_batch(const gs_gaussians* g, const gs_camera* cams, int32_t C, in
   header_sentinel(hl, C);
   hipStream_t s = (hipStream_t)stream;
   CamBatch cb;
-  hl.in_flight = true;
-  if (int e = plan_enqueue(g, cams, C, prefiltered, 0, geom, image, radii, hl.s.dev, hl.s.ev, cb, s))
+  hl.launched(s);
+  if (int e = plan_enqueue(g, cams, C, prefiltered, 0, geom, image, radii, hl.s.dev, cb, s))
     return e;
   const int W = cams[0].image_width, H = cams[0].image_height;
   const TileArgs ta = tile_args(P, W, H, geom, image);
   const int64_t tiles = (int64_t)ta.grid_x * ta.grid_y;
-  if (int e = publish_wait(hl, C, s, true)) return e;
   // Every stage behind the plan is enqueued before the host looks at the
   // headers: the GPU goes on from the plan to the bucket, sort and blend
   // launches while the host waits for the event.
@@ -842,7 +852,7 @@ int gs_forward_batch(const gs_gaussians* g, const gs_camera* cams, int32_t C, in
                           out_depth, out_alpha, sp, s))
     return e;
   // the same wait and sentinel check as the two-phase plan (gs_forward_plan)
-  if (int e = publish_wait(hl, C, s, false)) return e;
+  if (int e = publish_wait(hl, C, s)) return e;
   PlanInfo info;
   if (int e = plan_read(reinterpret_cast<const uint32_t(*)[M_WORDS]>(hl.s.host), C, prefiltered, 0, tiles,
                         num_rendered, num_instances, info))

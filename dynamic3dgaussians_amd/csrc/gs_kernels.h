@@ -194,10 +194,9 @@ __host__ __device__ inline TileArgs cam_tile_args(const TileArgs& a0, const CamB
   return a;
 }
 // plan: per-block tile histograms, tile totals and offsets, ranges, header
-// (also stored to hdr_host[c * M_WORDS ..] when non-null: mapped host memory;
-// `done`, when non-null, is recorded by the dispatch of the header's kernel)
-void launch_tile_plan(const TileArgs& a, const CamBatch& cb, int prefiltered, uint32_t* hdr_host, hipEvent_t done,
-                      hipStream_t s);
+// (also stored to hdr_host[c * M_WORDS ..] when non-null: mapped host memory,
+// its last word stored last, after a system fence -- the host polls it)
+void launch_tile_plan(const TileArgs& a, const CamBatch& cb, int prefiltered, uint32_t* hdr_host, hipStream_t s);
 // render: bucket the instances by tile, then sort every tile by (depth, id).
 // max_len = the plan header's longest tile (host copy), or -1 if unknown.
 void launch_tile_bucket(const TileArgs& a, const CamBatch& cb, hipStream_t s);

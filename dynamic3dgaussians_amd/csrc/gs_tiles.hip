@@ -486,12 +486,17 @@ __global__ __launch_bounds__(OFF_T) void tile_offsets_kernel(const uint32_t* __r
     // The host's copy of the header: page-locked, device-mapped, coherent
     // host memory written here directly (vector stores at system scope), so
     // no copy command sits in the stream between the plan and the render
-    // launches; the host reads it after an event recorded behind this kernel.
+    // launches.  The host polls the last word (its sentinel, 0 once written):
+    // the other words first, a system fence, then the sentinel, so a host that
+    // sees the sentinel sees the header.  (An event on this dispatch instead
+    // idled the GPU 15-27 us behind it per step: profiles/r06gaps3/.)
     if (hdr_host) {
       uint32_t* o = hdr_host + (size_t)blockIdx.x * M_WORDS;
 #pragma unroll
-      for (int w = 0; w < M_WORDS; ++w) __hip_atomic_store(o + w, h[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      for (int w = 0; w < M_WORDS - 1; ++w)
+        __hip_atomic_store(o + w, h[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __threadfence_system();
+      __hip_atomic_store(o + M_WORDS - 1, h[M_WORDS - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
 }
@@ -910,8 +915,7 @@ static int count_mode() {  // 0 auto, 1 diff, 2 per instance
   return v;
 }
 
-void launch_tile_plan(const TileArgs& a, const CamBatch& cb, int prefiltered, uint32_t* hdr_host, hipEvent_t done,
-                      hipStream_t s) {
+void launch_tile_plan(const TileArgs& a, const CamBatch& cb, int prefiltered, uint32_t* hdr_host, hipStream_t s) {
   const int T = a.num_tiles;
   const size_t nd = (size_t)(a.grid_x + 1) * (a.grid_y + 1);
   const int mode = count_mode();
@@ -927,14 +931,10 @@ void launch_tile_plan(const TileArgs& a, const CamBatch& cb, int prefiltered, ui
   }
   hipLaunchKernelGGL(tile_rowscan_kernel, dim3((T + RS_T - 1) / RS_T, cb.C), dim3(RS_THREADS), 0, s, a.thist, a.ttotal, T,
                      cb);
-  // the host waits for `done`: an event of this dispatch itself, not a
-  // marker packet between it and the render launches behind it
-  if (done)
-    hipExtLaunchKernelGGL(tile_offsets_kernel, dim3(cb.C), dim3(OFF_T), 0, s, nullptr, done, 0u, a.ttotal, T, a.bsum,
-                          a.ranges, a.meta, prefiltered, cb, hdr_host);
-  else
-    hipLaunchKernelGGL(tile_offsets_kernel, dim3(cb.C), dim3(OFF_T), 0, s, a.ttotal, T, a.bsum, a.ranges, a.meta,
-                       prefiltered, cb, hdr_host);
+  // the host polls the headers' sentinels (publish_wait, gs_api.hip): no
+  // event, no marker packet between this kernel and the render launches
+  hipLaunchKernelGGL(tile_offsets_kernel, dim3(cb.C), dim3(OFF_T), 0, s, a.ttotal, T, a.bsum, a.ranges, a.meta,
+                     prefiltered, cb, hdr_host);
 }
 
 void launch_tile_order(const TileArgs& a, const CamBatch& cb, const SortCover& cv, hipStream_t s) {
