@@ -511,11 +511,23 @@ class BinningPlan:
         self.hint = [int(x) for x in hint]
 
 
+def batch_backward_scratch(means3D, semantic_feature, C: int):
+    """An uninitialised scratch tensor of the batch backward's size
+    (gs_batch_backward_scratch_bytes at the compiled feature width), for a
+    caller that has the forward zero it (rasterize_gaussians_batch zero_fill)
+    and hands it to the backward."""
+    L_ = _lib.load()
+    P = means3D.size(0)
+    Fu = semantic_feature.numel() // max(P, 1) if _present(semantic_feature) else 0
+    n = L_.gs_batch_backward_scratch_bytes(P, _feature_width(Fu), int(C))
+    return torch.empty(max(16, n), dtype=torch.uint8, device=means3D.device)
+
+
 def rasterize_gaussians_batch(background, means3D, colors, semantic_feature, opacity, scales, rotations,
                               scale_modifier, cov3D_precomp, viewmatrices, projmatrices, c_x, c_y, tan_fovx,
                               tan_fovy, image_height, image_width, sh, degree, campos, prefiltered, debug,
                               *, compat=None, activate=False, windows=None, feature_ready=None, plan_state=None,
-                              walk_order=None):
+                              walk_order=None, zero_fill=None):
     """The forward of C cameras at once (gs_forward_plan_batch +
     gs_forward_render_batch): the arguments of rasterize_gaussians with
     per-camera matrices stacked ([C,4,4] or [C,16], campos [C,3]) and the
@@ -536,7 +548,10 @@ def rasterize_gaussians_batch(background, means3D, colors, semantic_feature, opa
     out with (what the backward takes); the exact counts are in
     plan_state.num_instances.  `walk_order`: an int32 device tensor of the P
     ids in the order the binning passes walk them (spatial_order), or None
-    (gs_gaussians.walk_order; outputs do not depend on it)."""
+    (gs_gaussians.walk_order; outputs do not depend on it).  `zero_fill`: a
+    device tensor the blend zeroes (its whole bytes, rounded down to 16) --
+    the backward's scratch, handed to rasterize_gaussians_batch_backward
+    with scratch_zeroed=True (gs_gaussians.zero_fill, ABI 13)."""
     L_ = _lib.load()
     sync_free = plan_state is not None and not debug
     cm = _compat_code(compat)
@@ -560,7 +575,7 @@ def rasterize_gaussians_batch(background, means3D, colors, semantic_feature, opa
                                     int(image_width), _opt(sh), int(degree), campos, bool(prefiltered),
                                     bool(debug), cm, bool(activate), _windows_arg(windows, C_),
                                     _event_handle(feature_ready), cap,
-                                    plan_state.hint if sync_free else [], _opt(walk_order),
+                                    plan_state.hint if sync_free else [], _opt(walk_order), _opt(zero_fill),
                                     torch.cuda.current_stream(means3D.device).cuda_stream)
         except RuntimeError as ex:
             raise _lib.GsplatError(str(ex)) from None
@@ -589,6 +604,11 @@ def rasterize_gaussians_batch(background, means3D, colors, semantic_feature, opa
                 and walk_order.numel() == inp.P and walk_order.device == dev):
             raise RuntimeError("walk_order must be a contiguous int32 device tensor of P ids")
         g.walk_order = walk_order.data_ptr()
+    if zero_fill is not None:
+        if not (zero_fill.is_contiguous() and zero_fill.device == dev):
+            raise RuntimeError("zero_fill must be a contiguous device tensor")
+        g.zero_fill = zero_fill.data_ptr()
+        g.zero_fill_bytes = (zero_fill.numel() * zero_fill.element_size()) & ~15
     out_color = torch.empty(C, 3, H, W, **f32)
     out_feature = torch.empty(C, inp.F, H, W, **f32)
     out_depth = torch.empty(C, 1, H, W, **f32)
@@ -639,7 +659,8 @@ def rasterize_gaussians_batch_backward(background, means3D, radii, colors, seman
                                        dL_dout_depth, dL_dout_alpha, sh, degree, campos, geomBuffer,
                                        num_instances, binningBuffer, imageBuffer, alphas, debug, *,
                                        compat=None, grad_mask=None, densify=None, opacity=None,
-                                       activate=False, windows=None, out=None):
+                                       activate=False, windows=None, out=None, scratch=None,
+                                       scratch_zeroed=False):
     """The backward of a camera batch (gs_backward_batch): the arguments of
     rasterize_gaussians_backward with stacked per-camera matrices, scalars
     and upstream gradients ([C, ...]), in the binding's positional camera
@@ -652,7 +673,10 @@ def rasterize_gaussians_batch_backward(background, means3D, radii, colors, seman
     a gradient bucket, distributed.ShardedAdam.grad_views): those gradients
     are WRITTEN there (every element, not accumulated) instead of into fresh
     tensors; each must be a contiguous fp32 device tensor of the gradient's
-    element count (dsem at the compiled feature width)."""
+    element count (dsem at the compiled feature width).  `scratch`: the
+    backward's scratch (gs_batch_backward_scratch_bytes) kept from the
+    forward, `scratch_zeroed`: the forward's blend zeroed it
+    (rasterize_gaussians_batch zero_fill; GS_FLAG_SCRATCH_ZEROED)."""
     L_ = _lib.load()
     cm = _compat_code(compat)
     if activate and not _present(opacity):
@@ -675,6 +699,7 @@ def rasterize_gaussians_batch_backward(background, means3D, radii, colors, seman
                                       None if densify is None else list(densify), _opt(opacity), bool(activate),
                                       _windows_arg(windows, len(c_x)),
                                       [out.get(k, _NO_DEST) for k in _buffer_shapes(0, 0, 0)] if out else [],
+                                      _opt(scratch), bool(scratch_zeroed),
                                       torch.cuda.current_stream(means3D.device).cuda_stream)
         except RuntimeError as ex:
             raise _lib.GsplatError(str(ex)) from None
@@ -726,7 +751,14 @@ def rasterize_gaussians_batch_backward(background, means3D, radii, colors, seman
                 raise RuntimeError(f"densify statistics must be contiguous fp32 ({P},) tensors on {dev}")
         g.densify_accum, g.densify_denom, g.max_radius = (t.data_ptr() for t in densify)
     NI = (ctypes.c_int64 * C)(*[int(x) for x in num_instances])
-    scratch = torch.empty(L_.gs_batch_backward_scratch_bytes(P, inp.F, C), dtype=torch.uint8, device=dev)
+    nscr = L_.gs_batch_backward_scratch_bytes(P, inp.F, C)
+    if scratch is None:
+        scratch = torch.empty(nscr, dtype=torch.uint8, device=dev)
+    else:
+        if not (scratch.is_contiguous() and scratch.device == dev and scratch.numel() * scratch.element_size() >= nscr):
+            raise RuntimeError(f"scratch must be a contiguous device tensor of {nscr} bytes on {dev}")
+        if scratch_zeroed:
+            g.flags |= _lib.GS_FLAG_SCRATCH_ZEROED
     stream = _stream(dev)
     p = lambda t: t.data_ptr() if (t is not None and t.numel()) else None  # noqa: E731
     check(L_.gs_backward_batch(ctypes.byref(g), cams, C, radii_c.data_ptr(), int(bool(debug)), cm,

@@ -16,9 +16,10 @@ _lock = threading.Lock()
 _lib = None
 
 c_void_p = ctypes.c_void_p
-ABI_VERSION = 12  # include/gsplat_hip.h GS_ABI_VERSION
+ABI_VERSION = 13  # include/gsplat_hip.h GS_ABI_VERSION
 GS_FLAG_ACCUMULATE = 1  # include/gsplat_hip.h
 GS_FLAG_ACTIVATE = 2  # include/gsplat_hip.h: raw opacity / scale / rotation parameters
+GS_FLAG_SCRATCH_ZEROED = 4  # include/gsplat_hip.h: the backward's scratch was zeroed by the forward
 c_int32, c_int64, c_float, c_size_t = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_size_t
 
 GS_COMPAT = {"reference": 0, "fixed": 1}
@@ -32,7 +33,8 @@ class GsGaussians(ctypes.Structure):
                 ("rotations", c_void_p), ("cov3D_precomp", c_void_p),
                 ("scale_modifier", c_float), ("flags", ctypes.c_uint32),
                 ("grad_mask", c_void_p), ("densify_accum", c_void_p), ("densify_denom", c_void_p),
-                ("max_radius", c_void_p), ("feature_ready", c_void_p), ("walk_order", c_void_p)]
+                ("max_radius", c_void_p), ("feature_ready", c_void_p), ("walk_order", c_void_p),
+                ("zero_fill", c_void_p), ("zero_fill_bytes", c_int64)]
 
 
 class GsCamera(ctypes.Structure):

@@ -603,6 +603,17 @@ static int render_impl(const gs_gaussians* g, const gs_camera* cams, int C, int 
   ra.out_color = out_color; ra.out_feature = out_feature; ra.out_depth = out_depth; ra.out_alpha = out_alpha;
   ra.n_contrib = at<uint32_t>(image, il.n_contrib);
   ra.fmax = at<uint32_t>(image, il.fmax);
+  if (g->zero_fill) {
+    if ((reinterpret_cast<uintptr_t>(g->zero_fill) & 15) || g->zero_fill_bytes < 0 || (g->zero_fill_bytes & 15))
+      return fail(-1, "zero_fill must be 16-B aligned and a multiple of 16 bytes long");
+    ra.zero = static_cast<float4*>(g->zero_fill);
+    ra.zero_n = g->zero_fill_bytes / 16;
+    if (ra.num_tiles <= 0) {  // no blend launch to carry it
+      (void)hipMemsetAsync(g->zero_fill, 0, (size_t)g->zero_fill_bytes, s);
+      ra.zero = nullptr;
+      ra.zero_n = 0;
+    }
+  }
   if (g->feature_ready) {
     const hipError_t e = hipStreamWaitEvent(s, (hipEvent_t)g->feature_ready, 0);
     if (e != hipSuccess) return fail((int)e, "waiting for feature_ready: %s", hipGetErrorString(e));
@@ -645,7 +656,9 @@ static int backward_impl(const gs_gaussians* g, const gs_camera* cams, int C, co
   const GeomLayout gl(P);
   const ImgLayout il(W, H);
   float* acc = static_cast<float*>(scratch);
-  (void)hipMemsetAsync(acc, 0, sizeof(float) * (size_t)ACC_STRIDE * P * C, s);
+  // the accumulation records start at zero: filled here, or already zeroed by
+  // the forward's blend (gs_gaussians.zero_fill + GS_FLAG_SCRATCH_ZEROED)
+  if (!(g->flags & GS_FLAG_SCRATCH_ZEROED)) (void)hipMemsetAsync(acc, 0, sizeof(float) * (size_t)ACC_STRIDE * P * C, s);
   const bool accumulate = (g->flags & GS_FLAG_ACCUMULATE) != 0;
   // the blend kernel adds the feature gradients atomically: zero first unless
   // the output already holds the sums to add to; a padded-stride width adds

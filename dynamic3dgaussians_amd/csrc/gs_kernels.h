@@ -85,6 +85,10 @@ struct RenderArgs {
   // F >= 32: per channel the largest |feature| of the table (float bits,
   // launch_feature_absmax; the whole batch's, camera 0's image buffer)
   const uint32_t* fmax;
+  // a region the launch zeroes alongside (gs_gaussians.zero_fill), zero_n
+  // 16-B words; each workgroup its 1/gridDim share
+  float4* zero;
+  int64_t zero_n;
 };
 
 // Row stride (floats) of the feature gradients the backward blend adds into:

@@ -462,6 +462,16 @@ template <int F>
 constexpr int fwd_waves_per_simd() {
   return F == 32 ? 4 : F == 36 ? 3 : 1;  // F = 36: 0.188 vs 0.205 ms per camera at 4 (spills)
 }
+// This workgroup's share of a region the forward zeroes for the backward
+// (gs_gaussians.zero_fill): 16-B stores issued as the strip's last memory
+// operations, so nothing the wave waits for queues behind them.
+__device__ inline void zero_share(float4* __restrict__ z, int64_t n) {
+  if (!z || n <= 0) return;
+  const int64_t per = (n + (int64_t)gridDim.x - 1) / (int64_t)gridDim.x;
+  const int64_t z0 = (int64_t)blockIdx.x * per, z1 = z0 + per < n ? z0 + per : n;
+  for (int64_t i = z0 + (threadIdx.x & 63); i < z1; i += 64) z[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
 template <int F, int COMPAT>
 __global__ __launch_bounds__(64 * WPB_FWD) __attribute__((amdgpu_waves_per_eu(fwd_waves_per_simd<F>(), 8))) void render_fwd_kernel(
     RenderArgs a0, CamBatch cb) {
@@ -533,6 +543,7 @@ __global__ __launch_bounds__(64 * WPB_FWD) __attribute__((amdgpu_waves_per_eu(fw
       if (out_alpha) out_alpha[pix] = 0.f;
       for (int c = 0; c < F; ++c) out_feature[(size_t)c * HW + pix] = 0.f;
     }
+    zero_share(a0.zero, a0.zero_n);
     return;
   }
 
@@ -880,6 +891,7 @@ blend_done:
       }
     }
   }
+  zero_share(a0.zero, a0.zero_n);
 #ifdef GS_STAMPS
   STAMP(ts3);
   __builtin_amdgcn_s_waitcnt(0);

@@ -295,10 +295,17 @@ forward_batch(const Tensor& bg, const Tensor& means3D, const OptT& colors, const
               int64_t degree, const Tensor& campos, bool prefiltered, bool debug, int64_t compat, bool activate,
               const std::vector<std::vector<int64_t>>& windows, int64_t feature_ready,
               const std::vector<int64_t>& capacity, const std::vector<int64_t>& hint, const OptT& walk_order,
-              int64_t stream) {
+              const OptT& zero_fill, int64_t stream) {
   Inputs in(means3D, colors, sem, opacity, scales, rotations, scale_modifier, cov3D, sh, degree);
   if (activate) in.g.flags |= GS_FLAG_ACTIVATE;
   in.g.feature_ready = reinterpret_cast<gs_event_t>(feature_ready);
+  if (present(zero_fill)) {  // the backward's scratch, zeroed by the blend (gs_gaussians.zero_fill)
+    const Tensor& z = *zero_fill;
+    if (z.device() != in.dev || !z.is_contiguous())
+      throw std::runtime_error("zero_fill must be a contiguous device tensor");
+    in.g.zero_fill = z.data_ptr();
+    in.g.zero_fill_bytes = (int64_t)(z.numel() * z.element_size()) & ~(int64_t)15;
+  }
   if (present(walk_order)) {
     const Tensor& w = *walk_order;
     if (w.scalar_type() != at::kInt || w.device() != in.dev || !w.is_contiguous() || w.numel() != in.P)
@@ -384,7 +391,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tenso
     const std::vector<int64_t>& num_instances, const OptT& binning, const Tensor& img, const Tensor& alphas,
     bool debug, int64_t compat, const OptT& grad_mask, c10::optional<std::vector<Tensor>> densify,
     const OptT& opacity, bool activate, const std::vector<std::vector<int64_t>>& windows,
-    const std::vector<Tensor>& out, int64_t stream) {
+    const std::vector<Tensor>& out, const OptT& scratch_in, bool scratch_zeroed, int64_t stream) {
   if (activate && !present(opacity)) throw std::runtime_error("activate=True needs the raw opacities");
   Inputs in(means3D, colors, sem, activate ? opacity : c10::nullopt, scales, rotations, scale_modifier, cov3D, sh,
             degree);
@@ -439,8 +446,18 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tenso
     in.g.densify_denom = d[1].data_ptr<float>();
     in.g.max_radius = d[2].data_ptr<float>();
   }
-  Tensor scratch = at::empty({(int64_t)gs_batch_backward_scratch_bytes(P, (int32_t)in.F, (int32_t)C)},
-                             f32.dtype(at::kByte));
+  // the scratch: the caller's (kept from the forward, which may have zeroed
+  // it: scratch_zeroed -> GS_FLAG_SCRATCH_ZEROED) or a fresh one
+  const int64_t nscr = (int64_t)gs_batch_backward_scratch_bytes(P, (int32_t)in.F, (int32_t)C);
+  Tensor scratch;
+  if (present(scratch_in)) {
+    scratch = *scratch_in;
+    if (scratch.device() != in.dev || !scratch.is_contiguous() || scratch.numel() * scratch.element_size() < nscr)
+      throw std::runtime_error("scratch must be a contiguous device tensor of " + std::to_string(nscr) + " bytes");
+    if (scratch_zeroed) in.g.flags |= GS_FLAG_SCRATCH_ZEROED;
+  } else {
+    scratch = at::empty({nscr}, f32.dtype(at::kByte));
+  }
   const Tensor bin = binning.has_value() ? *binning : Tensor();
   auto fp = [](const Tensor& t) -> const float* { return t.defined() ? t.data_ptr<float>() : nullptr; };
   check(gs_backward_batch(&in.g, k.cams.data(), (int32_t)C, radii_c.data_ptr<int32_t>(), debug ? 1 : 0, (int)compat,

@@ -20,6 +20,8 @@ default, "reference"); see DESIGN.md "Quirks".
 """
 from __future__ import annotations
 
+import os
+
 from typing import NamedTuple, Optional, Tuple
 
 import torch
@@ -446,12 +448,20 @@ class _RasterizeGaussiansBatch(torch.autograd.Function):
         rotations = _empty_like_none(rotations)
         cov3Ds_precomp = _empty_like_none(cov3Ds_precomp)
         tx, ty = cams.tx, cams.ty
+        # the backward's scratch, zeroed by the forward's blend (whose HBM is
+        # mostly idle) instead of a fill launch before the backward blend
+        # (gs_gaussians.zero_fill, ABI 13): only when a backward can follow
+        scratch = None
+        if (any(ctx.needs_input_grad) and means3D.is_cuda and means3D.size(0) > 0
+                and os.environ.get("GS_FORWARD_ZERO_SCRATCH", "1") != "0"):
+            scratch = _C.batch_backward_scratch(means3D, semantic_feature, C)
         out = _C.rasterize_gaussians_batch(
             rs0.bg, means3D, colors_precomp, semantic_feature, opacities, scales, rotations, rs0.scale_modifier,
             cov3Ds_precomp, views, projs, [p[0] for p in pp], [p[1] for p in pp], tx, ty, rs0.image_height,
             rs0.image_width, sh, rs0.sh_degree, cpos, rs0.prefiltered, rs0.debug, compat=compat,
             activate=raw_params, windows=cams.windows, feature_ready=feature_ready, plan_state=plan_state,
-            walk_order=walk_order)
+            walk_order=walk_order, zero_fill=scratch)
+        ctx.scratch, ctx.scratch_zeroed = scratch, scratch is not None
         num_rendered, color, feature_map, depth, alpha, radii, geom, binning, img, num_instances = out
         ctx.rs0 = rs0
         ctx.cams = (views, projs, cpos, pp, tx, ty, cams.windows)
@@ -490,7 +500,9 @@ class _RasterizeGaussiansBatch(torch.autograd.Function):
             cov3Ds_precomp, views, projs, *cam4, grad_color, grad_out_feature, grad_depth, grad_alpha, sh,
             rs0.sh_degree, cpos, geom, ctx.num_instances, binning, img, alpha, rs0.debug, compat=ctx.compat,
             grad_mask=label if fuse else None, densify=ctx.densify_out, opacity=raw_opacities,
-            activate=ctx.raw_params, windows=windows, out=ctx.grad_into)
+            activate=ctx.raw_params, windows=windows, out=ctx.grad_into, scratch=ctx.scratch,
+            scratch_zeroed=ctx.scratch_zeroed)
+        ctx.scratch_zeroed = False  # a second backward (retain_graph) finds it written
         (grad_means2D, grad_colors_precomp, grad_semantic_feature, grad_opacities, grad_means3D,
          grad_cov3Ds_precomp, grad_sh, grad_scales, grad_rotations) = grads
         if ctx.sem_shape is not None:

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 12
+#define GS_ABI_VERSION 13
 
 /* compat modes: numerics of the as-shipped reference vs corrected ones */
 #define GS_COMPAT_REFERENCE 0
@@ -64,6 +64,12 @@ typedef void *gs_event_t; /* a hipEvent_t */
  * params2rendervar).  Replaces ~20 elementwise launches of the caller's
  * activations and their backward per step. */
 #define GS_FLAG_ACTIVATE 2u
+/* GS_FLAG_SCRATCH_ZEROED (ABI 13, gs_backward / gs_backward_batch only; no
+ * reference analogue): the scratch buffer is already zero -- a forward zeroed
+ * it through gs_gaussians.zero_fill and nothing has written it since -- so the
+ * backward skips its zero fill of the accumulation records.  Set it for the
+ * first backward of a forward only. */
+#define GS_FLAG_SCRATCH_ZEROED 4u
 
 /* Per-Gaussian inputs (device pointers, fp32, row-major/contiguous).
  * Mirrors the tensor arguments of RasterizeGaussiansCUDA
@@ -119,6 +125,15 @@ typedef struct gs_gaussians {
    * per-tile runs are long and its key stores coalesce.  Debug mode checks
    * that it is a permutation (gs_check_walk_order). */
   const int32_t *walk_order;
+  /* Optional (ABI 13; no reference analogue): a device region the forward's
+   * blend launch zeroes (zero_fill_bytes, a multiple of 16, 16-B aligned), or
+   * NULL.  A caller that keeps the backward's scratch from the forward
+   * (gs_batch_backward_scratch_bytes) hands it here and to the backward with
+   * GS_FLAG_SCRATCH_ZEROED: the zeroing then rides in the VALU-bound blend,
+   * whose HBM is mostly idle, instead of a fill launch before the backward
+   * blend (0.5 GB at the 27-camera bench step). */
+  void *zero_fill;
+  int64_t zero_fill_bytes;
 } gs_gaussians;
 
 /* Camera / raster settings (GaussianRasterizationSettings,

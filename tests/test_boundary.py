@@ -46,7 +46,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_sizes():
     L = _lib.load()
-    assert L.gs_version() == _lib.ABI_VERSION == 12
+    assert L.gs_version() == _lib.ABI_VERSION == 13
     assert L.gs_geom_buffer_bytes(1) >= 64  # one 64-B render record at least
     for a, b in [(1000, 2000), (10_000, 300_000)]:
         assert L.gs_geom_buffer_bytes(b) > L.gs_geom_buffer_bytes(a)

@@ -272,3 +272,36 @@ def _C_forward(src, s):
         s.tanfovx, s.tanfovy, s.image_height, s.image_width, torch.Tensor([]), 0, s.campos, False, False)
     torch.cuda.synchronize()
     return out
+
+
+@pytest.mark.parametrize("F", [0, 32, 36])
+def test_forward_zeroed_scratch_and_a_second_backward(F, P=12000, W=160, H=128, C=4):
+    """The batch forward zeroes the backward's scratch inside its blend
+    (gs_gaussians.zero_fill, ABI 13) and the first backward skips its fill
+    (GS_FLAG_SCRATCH_ZEROED) -- test_batch_matches_per_camera holds those
+    gradients to the per-camera calls, which zero their own scratch.  A
+    second backward of the same forward (retain_graph), whose scratch the
+    first one wrote, must zero it again: it adds the same gradients."""
+    src = _scene(P, F, False, seed=5 + F)
+    sets = _settings(camera_rig(C, W, H), W, H, "reference")
+    gen = torch.Generator(device=DEV).manual_seed(9)
+    ups = [torch.randn(C, 3, H, W, device=DEV, generator=gen), torch.randn(C, 1, H, W, device=DEV, generator=gen)]
+    if F:
+        ups.append(torch.randn(C, F, H, W, device=DEV, generator=gen))
+
+    def run(twice):
+        leaves = {k: v.clone().requires_grad_(True) for k, v in src.items()}
+        out = GaussianRasterizerBatch(sets)(means2D=torch.zeros(P, 3, device=DEV), label=torch.ones(P, device=DEV),
+                                            **leaves)
+        outs = [out[0], out[3], out[2]] if F else [out[0], out[2]]
+        torch.autograd.backward(outs, ups, retain_graph=twice)
+        first = {k: v.grad.clone() for k, v in leaves.items()}
+        if twice:
+            torch.autograd.backward(outs, ups)
+        return first, {k: v.grad.clone() for k, v in leaves.items()}
+
+    g1, _ = run(False)
+    g2, both = run(True)
+    for k in g1:
+        assert _rel(g2[k], g1[k]) < 1e-5, (k, _rel(g2[k], g1[k]))
+        assert _rel(both[k], 2 * g1[k]) < 1e-5, (k, _rel(both[k], 2 * g1[k]))
