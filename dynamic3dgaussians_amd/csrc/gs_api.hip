@@ -152,13 +152,13 @@ thread_local PlanInfo g_plan;
 
 // Host landing areas of the plan headers (GS_MAX_CAMS x M_WORDS words each):
 // page-locked, device-mapped, coherent host memory that tile_offsets_kernel
-// writes directly, plus an event recorded behind the plan kernels.  Leased
+// writes directly (the host polls a sentinel word, publish_wait).  Leased
 // per call from a process-wide pool, so the number of buffers is bounded by
 // the number of concurrent callers (not by the threads that ever called:
 // thread pools and autograd workers would otherwise each pin one for good).
 // Never freed: a pool destructor could run after the HIP runtime is gone.
-// A slot belongs to the device that was current when it was made (its event
-// and its device-side mapping are that device's): a lease only takes a free
+// A slot belongs to the device that was current when it was made (its
+// device-side mapping is that device's): a lease only takes a free
 // slot of the calling thread's current device.
 struct HeaderSlot {
   uint32_t* host = nullptr;  // host pointer
@@ -471,9 +471,8 @@ static int plan_read(const uint32_t (*host)[M_WORDS], int C, int prefiltered, in
 }
 
 // The headers' way to the host after plan_enqueue: tile_offsets_kernel
-// stored them to the mapped buffer and its dispatch records hl's event (an
-// in-stream copy of the device headers instead measured slower, DESIGN.md
-// section 4).  record_only: do not wait yet.
+// stores them to the mapped buffer (an in-stream copy of the device headers
+// instead measured slower).
 // Wait until the plan kernel has written every camera's header: the host
 // polls each header's last word (header_sentinel: 0 once written, stored by
 // tile_offsets_kernel after the rest and a system fence), yielding the core
@@ -859,7 +858,7 @@ int gs_forward_batch(const gs_gaussians* g, const gs_camera* cams, int32_t C, in
   const int64_t tiles = (int64_t)ta.grid_x * ta.grid_y;
   // Every stage behind the plan is enqueued before the host looks at the
   // headers: the GPU goes on from the plan to the bucket, sort and blend
-  // launches while the host waits for the event.
+  // launches while the host polls the headers.
   const SortPlan sp = hinted_sort_plan(hint, tiles);
   if (int e = render_impl(g, cams, C, 0, compat, geom, binning, image, capacity, radii, out_color, out_feature,
                           out_depth, out_alpha, sp, s))
