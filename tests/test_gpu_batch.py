@@ -305,3 +305,32 @@ def test_forward_zeroed_scratch_and_a_second_backward(F, P=12000, W=160, H=128, 
     for k in g1:
         assert _rel(g2[k], g1[k]) < 1e-5, (k, _rel(g2[k], g1[k]))
         assert _rel(both[k], 2 * g1[k]) < 1e-5, (k, _rel(both[k], 2 * g1[k]))
+
+
+def test_misaligned_zero_fill_is_refused_and_the_next_call_renders(monkeypatch, P=4000, W=96, H=64, C=2):
+    """A zero_fill region that is not 16-B aligned is refused by the C ABI
+    (status -1, gs_render_impl) after the plan kernels were enqueued; the
+    header slot that call leased goes back to the pool once its stream is
+    drained, and the next call on the same device renders the same images
+    as a call with the fill turned off."""
+    import dynamic3dgaussians_amd._C as C_
+    src = _scene(P, 32, False, seed=13)
+    sets = _settings(camera_rig(C, W, H), W, H, "reference")
+    make = C_.batch_backward_scratch
+
+    def render():
+        leaves = {k: v.clone().requires_grad_(True) for k, v in src.items()}
+        return GaussianRasterizerBatch(sets)(means2D=torch.zeros(P, 3, device=DEV),
+                                             label=torch.ones(P, device=DEV), **leaves)
+
+    monkeypatch.setattr(C_, "batch_backward_scratch", lambda *a: make(*a)[1:])
+    with pytest.raises(Exception, match="zero_fill"):
+        render()
+    monkeypatch.setattr(C_, "batch_backward_scratch", make)
+    out = render()
+    monkeypatch.setenv("GS_FORWARD_ZERO_SCRATCH", "0")
+    ref = render()
+    torch.cuda.synchronize()
+    for a, b in zip(out[:5], ref[:5]):
+        if torch.is_tensor(a) and a.is_floating_point():
+            assert torch.equal(a, b)
